@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark of the d_render path on MI355X: Mrays/s + fps + HBM roofline fraction.
+
+One step = one frame: clear the output, ray-cast every pixel of the frame (each
+rank its own image tiles), and for N > 1 gather the tiles to rank 0 (RCCL over
+xGMI) and assemble the frame.  The distribution volume is generated in HBM
+before timing (synthetic, seeded) and replicated per GPU.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1024x8]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (contract in the task statement).  The metric
+formula is the reference's own benchmark line, 1e-6*W*H/t (C:1065-1067).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (volume edge, bins, W, H)
+    "128x1": (128, 1, 256, 256),
+    "256x4": (256, 4, 512, 512),
+    "512x8": (512, 8, 1920, 1080),
+    "1024x8": (1024, 8, 1920, 1080),
+}
+SEED = 20261015
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="1024x8", choices=sorted(CONFIGS))
+    ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 7])
+    ap.add_argument("--camera", default="C0", choices=["C0", "C1"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-row-stride", type=int, default=0,
+                    help="CPU baseline renders every k-th row (0 = auto)")
+    ap.add_argument("--traffic-json", default="",
+                    help="rocprofv3 PMC summary (tools/pmc_traffic.py) for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(pkg, cfg_name, m, method, row_stride):
+    """The CPU oracle (C, OpenMP) ray-casting the same scene on this host's cores."""
+    import __graft_entry__ as graft
+    orc = graft.load_oracle()
+    n, nb, W, H = CONFIGS[cfg_name]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    if row_stride <= 0:
+        row_stride = {128: 1, 256: 2, 512: 8, 1024: 8}[n]
+    vol = orc.synth_volume(n, n, n, nb, SEED, threads)
+    p = orc.make_params(W, H, m, query_method=method, m7_dims=(n, n, n))
+    t0 = time.perf_counter()
+    _, _, _, samples = orc.render(vol, p, row_start=0, row_stride=row_stride, nthreads=threads,
+                                  want_float=False, want_steps=False)
+    dt = time.perf_counter() - t0
+    rows = len(range(0, H, row_stride))
+    rays = rows * W
+    del vol
+    return {
+        "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+        "sample": (f"oracle/vr_oracle.c (-O3, OpenMP) on every {row_stride}th row of the "
+                   f"{W}x{H} frame ({rays} rays, {samples} samples, {dt:.2f} s), "
+                   f"full {n}^3x{nb} volume in host RAM"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as graft
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0:
+            print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
+                  file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    pkg = graft.load_package()
+    n, nb, W, H = CONFIGS[args.config]
+    m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
+         else pkg.camera.display_inv_view((30.0, 45.0)))
+
+    stream = torch.cuda.Stream(device=dev)
+    pkg.set_stream(stream)
+    pkg.synthesize((n, n, n), nb, SEED)
+
+    lists = pkg.tiles.tile_lists(W, H, world)
+    n_slots = lists.shape[1]
+    frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    with torch.cuda.stream(stream):
+        if world > 1:
+            packed = torch.zeros(n_slots * 256, dtype=torch.int32, device=dev)
+            my_list = torch.from_numpy(lists[rank].view(np.int32).copy()).to(dev)
+            all_lists = torch.from_numpy(lists.view(np.int32).copy()).to(dev)
+            desc = pkg.make_desc(packed, W, H, m, query_method=args.method,
+                                 d_tile_list=my_list, n_tiles=n_slots)
+        else:
+            desc = pkg.make_desc(frame, W, H, m, query_method=args.method)
+    torch.cuda.synchronize()
+
+    ev = []
+
+    def step(timed):
+        with torch.cuda.stream(stream):
+            if world > 1:
+                packed.zero_()
+            else:
+                frame.zero_()  # C:208
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            pkg.render(desc)
+            if timed:
+                e1.record(stream)
+                ev.append((e0, e1))
+            if world > 1:
+                gathered = pkg.tiles.gather_packed(packed, world, rank)
+                if rank == 0:
+                    pkg.unscatter_tiles(gathered, all_lists, world, n_slots, frame, W, H)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # algorithmic bytes of one launch on this rank: U*S_rec + pixels*4
+    u = pkg.count_footprint(desc)
+    pixels = W * H if world == 1 else int(np.sum(lists[rank] != pkg.tiles.PAD)) * 256
+    alg_bytes = u * nb * 4 + pixels * 4
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("config") == args.config and tj.get("n_gpus", 1) == world:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = W * H / (elapsed / args.steps) / 1e6
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(pkg, args.config, m, args.method, args.cpu_row_stride)
+        out = {
+            "metric": f"Mrays/s at {n}^3 x {nb}-bin volume, {W}x{H}",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "fps": round(1e3 / ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32 (f64 decode terms)",
+            "data": f"synthetic seeded distribution volume (seed {SEED}, DESIGN.md s5)",
+            "config": {
+                "workload": f"{n}^3 x {nb}-bin distribution volume, {W}x{H}, camera "
+                            f"{args.camera}, queryMethod {args.method}",
+                "volume": [n, n, n], "bins": nb, "image": [W, H], "camera": args.camera,
+                "query_method": args.method, "density": 0.05,
+                "parallelism": f"image tiles x{world}" + (" + RCCL gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": (f"k_march<{nb},{args.method},false>" if args.method != 7
+                           else f"k_march_m7<{nb}>"),
+                "kernel_ms": round(kern_ms, 4),
+                "alg_bytes_per_launch": int(alg_bytes), "U_records": int(u),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/*
+ * vr.h -- C-ABI of libvr.so, the MI355X (gfx950) drop-in for the d_render path
+ * of ykou/Volume-Rendering-Based-on-Distribution-Data.
+ *
+ * Citations: K = volumeRender_kernel.cu, C = volumeRender.cpp (reference).
+ *
+ * Part 1 -- the reference's own extern "C" entry points (declared C:156-170),
+ * same names, argument order and meaning.  vr_dim3 / vr_extent are
+ * layout-identical to dim3 (3 x uint32) and cudaExtent/hipExtent (3 x size_t),
+ * so a caller written against the reference header links unchanged.
+ *
+ * Part 2 -- extensions (vr_*): explicit-parameter render with tile lists for
+ * the multi-GPU image split, on-device synthetic volumes, the footprint counter
+ * used for the roofline, and error reporting.  The library never calls exit():
+ * failures are recorded for vr_last_error() (the reference's checkCudaErrors
+ * printed and exited, C:201-216).
+ *
+ * Threading: like the reference, all state is module-global and the entry
+ * points are not thread-safe (K:22-88, 116).  One process drives one GPU.
+ */
+#ifndef VR_H
+#define VR_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdbool.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { uint32_t x, y, z; } vr_dim3;                /* == dim3       */
+typedef struct { size_t width, height, depth; } vr_extent;   /* == cudaExtent */
+typedef struct { int32_t x, y, z, w; } vr_int4;               /* == int4       */
+typedef struct { float x, y; } vr_float2;                     /* == float2     */
+
+/* ---------------- Part 1: reference entry points ------------------------- */
+
+/* Replaces render_kernel, K:2387-2401.  Launches the per-ray march into the
+ * caller-owned device buffer d_output (imageW*imageH packed RGBA8, row-major,
+ * A<<24|B<<16|G<<8|R).  Miss pixels are not written (caller zeroes, C:208).
+ * gridSize/blockSize are accepted for ABI compatibility; the library picks its
+ * own gfx950 launch geometry (16x16-pixel tiles, one 8x8 ray block per wave).
+ * volumeSize is used exactly where the reference uses it: the method-7 corner
+ * grid (K:322-352).  queryMethod: 1 mean, 2 variance, 3 entropy,
+ * 7 software-interpolated mean.  4/5/6 and 8/9/0 need the fractal codec and
+ * the flexible-block pre-pass (out of scope): the call records an error and
+ * writes nothing.  Asynchronous on the library stream (default: null stream),
+ * like the reference's default-stream launch. */
+void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output,
+                   uint32_t imageW, uint32_t imageH, float density, float brightness,
+                   float transferOffset, float transferScale, int queryMethod,
+                   vr_extent volumeSize);
+
+/* Replaces copyInvViewMatrix, K:2403-2406: 3 rows of float4 (48 bytes). */
+void copyInvViewMatrix(float *invViewMatrix, size_t sizeofMatrix);
+
+/* Replaces initCuda, K:1893-2358 (declared C:157-163 with arg 1 as void*).
+ * h_histogram: fp32 records, record r = bins [r*B, r*B+B) where
+ * B = histogramSize.width and r = x + X*(y + Y*z) -- the reference's layered
+ * layout (bin, r % height, r / height) is exactly this AoS order (K:363-364).
+ * histogramSize.height*depth must equal volumeSize.width*height*depth.
+ * The codec / flexible-block arrays (args 4-18) feed methods 4-6 and 8/9/0
+ * only; they are accepted and ignored. */
+void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
+              vr_int4 *h_codebook, vr_extent codebookSize, float *h_templates,
+              vr_extent templatesSize, vr_float2 *h_errorsbook, vr_extent errorsbookSize,
+              vr_int4 *h_codebookSpanLow, vr_int4 *h_codebookSpanHigh,
+              vr_int4 *h_flexibleCodebook, vr_float2 *h_flexibleErrorsbook,
+              vr_int4 *h_simpleLow, vr_int4 *h_simpleHigh, int *h_simpleCount,
+              vr_float2 *h_simpleHistogram, float *h_flexibleTemplates);
+
+/* Replaces freeCudaBuffers, K:2360-2385. */
+void freeCudaBuffers(void);
+
+/* Replaces setTextureFilterMode, K:1889-1891.  In the reference it switches the
+ * filter of the integer index volume `tex`, which methods 1/2/3 never sample;
+ * the flag is stored and has no effect on any supported method. */
+void setTextureFilterMode(bool bLinearFilter);
+
+/* Replaces basicDataProcessing, K:1798-1887.  The reference pre-bakes per-voxel
+ * mean/variance/entropy into a float4 texture; this library decodes the
+ * statistic from the distribution records at every step inside the march, so
+ * there is nothing to pre-bake.  Validates that a volume is resident. */
+void basicDataProcessing(void);
+
+/* Replaces dataProcessing, K:1735-1796 (flexible-block pre-pass, methods
+ * 8/9/0): out of scope in this build; records an error. */
+void dataProcessing(void);
+
+/* ---------------- Part 2: extensions ------------------------------------- */
+
+#define VR_OK 0
+#define VR_ERR_ARG -1
+#define VR_ERR_STATE -2
+#define VR_ERR_HIP -3
+#define VR_ERR_UNSUPPORTED -4
+
+/* last error message ("" if none); vr_clear_error resets it */
+const char *vr_last_error(void);
+int vr_last_status(void);
+void vr_clear_error(void);
+
+/* Volume residency.  bins: fp32 AoS records as in initCuda.
+ * where: 0 = host pointer (copied), 1 = device pointer (copied),
+ *        2 = device pointer adopted (not freed by the library). */
+int vr_init_distribution(const float *bins, vr_extent dims, int nbins, int where);
+
+/* Generate the seeded synthetic distribution volume of DESIGN.md section 5
+ * directly in HBM (library-owned). */
+int vr_synthesize(vr_extent dims, int nbins, uint64_t seed);
+
+/* dims, bin count and device pointer of the resident volume */
+int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins);
+
+/* Stream for all subsequent launches (hipStream_t; NULL = null stream). */
+int vr_set_stream(void *stream);
+
+/* Explicit-parameter render.  With d_tile_list == NULL the whole frame is
+ * rendered into d_output[y*width + x].  Otherwise the n_tiles 16x16-pixel
+ * tiles named by d_tile_list (tile id = ty*ceil(width/16) + tx, device array)
+ * are rendered into a packed buffer: tile slot s occupies
+ * d_output[s*256 .. s*256+255] in row-major 16x16 order.  Entries of
+ * 0xFFFFFFFF in the tile list are padding and are skipped.
+ * d_output_f (optional) receives the saturated float RGBA of every written
+ * pixel, d_steps (optional) the samples taken (-1 for a miss; written for
+ * every pixel inside the image). */
+typedef struct {
+    uint32_t *d_output;
+    float *d_output_f;
+    int32_t *d_steps;
+    uint32_t width, height;
+    float inv_view[12];
+    float density, brightness, transfer_offset, transfer_scale;
+    int query_method;
+    vr_extent volume_size;          /* method-7 grid (render_kernel's volumeSize) */
+    const uint32_t *d_tile_list;
+    uint32_t n_tiles;
+} vr_render_desc;
+
+int vr_render(const vr_render_desc *desc);
+
+/* U of SURVEY.md 8(d): distinct voxel records in the union of the trilinear
+ * footprints of all samples taken (methods 1/2/3).  Synchronous; allocates a
+ * bitset of voxels/8 bytes.  Returns U, or a negative status. */
+int64_t vr_count_footprint(const vr_render_desc *desc);
+
+/* Rank-0 assembly of the multi-GPU frame: d_packed holds n_ranks x n_slots
+ * tiles (each 256 uint32) gathered from the ranks, d_tile_lists the matching
+ * n_ranks x n_slots tile ids (0xFFFFFFFF = padding); every listed tile is
+ * copied into d_frame (width x height, pixels outside the image dropped). */
+int vr_unscatter_tiles(const uint32_t *d_packed, const uint32_t *d_tile_lists,
+                       uint32_t n_ranks, uint32_t n_slots, uint32_t *d_frame,
+                       uint32_t width, uint32_t height);
+
+/* number of 16x16 tiles of a width x height frame */
+uint32_t vr_tiles_x(uint32_t width);
+uint32_t vr_tiles_y(uint32_t height);
+
+/* library version string */
+const char *vr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VR_H */

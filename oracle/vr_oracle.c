@@ -1,0 +1,491 @@
+/*
+ * vr_oracle.c -- CPU restatement of the reference d_render path
+ * (ykou/Volume-Rendering-Based-on-Distribution-Data, volumeRender_kernel.cu = K,
+ * volumeRender.cpp = C).
+ *
+ * TEST INFRASTRUCTURE ONLY -- see vr_oracle.h.  Never linked into the product.
+ *
+ * Evaluation rules ("canonical arithmetic"):
+ *  - every expression is evaluated with ISO C semantics exactly as written in
+ *    the reference source: float/double promotions as the source implies,
+ *    left-to-right association, NO fused multiply-add (built with
+ *    -ffp-contract=off);
+ *  - rsqrtf(x) is taken as 1.0f/sqrtf(x) (both correctly rounded);
+ *  - the float overload log(float) is taken as (float)log((double)x);
+ *  - texture fetches follow the CUDA texture-fetch rules: point sampling
+ *    i = floor(u*N); linear sampling xB = u*N - 0.5, i = floor(xB),
+ *    alpha = frac(xB) held in 9-bit fixed point with 8 fractional bits
+ *    (rounded to nearest even); clamp addressing (coordinate clamped to
+ *    [0,1] first, which gives the same texels as index clamping and a
+ *    defined answer for NaN);  1-D/3-D linear blends are
+ *    (1-a)*t0 + a*t1, x first, then y, then z.
+ */
+#include "vr_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* log(2.0) in double, correctly rounded (K:766 `log(2.0)`) */
+#define LN2_D 0x1.62e42fefa39efp-1
+
+typedef struct { float x, y, z; } f3;
+typedef struct { float x, y, z, w; } f4;
+
+/* transfer function, K:2323-2326 */
+static const f4 TF[9] = {
+    {0.0f, 0.0f, 0.0f, 0.0f}, {1.0f, 0.0f, 0.0f, 1.0f}, {1.0f, 0.5f, 0.0f, 1.0f},
+    {1.0f, 1.0f, 0.0f, 1.0f}, {0.0f, 1.0f, 0.0f, 1.0f}, {0.0f, 1.0f, 1.0f, 1.0f},
+    {0.0f, 0.0f, 1.0f, 1.0f}, {1.0f, 0.0f, 1.0f, 1.0f}, {0.0f, 0.0f, 0.0f, 0.0f},
+};
+
+static inline float logf_cr(float x) { return (float)log((double)x); }
+
+/* 9-bit fixed point weight with 8 fractional bits */
+static inline float q8(float a) { return rintf(a * 256.0f) * (1.0f / 256.0f); }
+
+static inline float clamp01(float u) { return fminf(fmaxf(u, 0.0f), 1.0f); }
+
+/* linear-filter texel pair + quantised weight for one axis */
+static inline void lin_axis(float u, int n, int *i0, int *i1, float *a) {
+    u = clamp01(u);
+    float xb = u * (float)n - 0.5f;
+    float fl = floorf(xb);
+    float fr = xb - fl;
+    int i = (int)fl;
+    int j = i + 1;
+    *a = q8(fr);
+    *i0 = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+    *i1 = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+}
+
+/* point-filter texel, normalised coordinates, clamp (tex, K:62, 2161-2165) */
+static inline int point_axis(float u, int n) {
+    u = clamp01(u);
+    int i = (int)floorf(u * (float)n);
+    return i > n - 1 ? n - 1 : i;
+}
+
+static inline float lerpq(float a, float b, float t) { return (1.0f - t) * a + t * b; }
+
+void orc_transfer(float x, float out[4]) {
+    int i0, i1;
+    float a;
+    lin_axis(x, 9, &i0, &i1, &a);
+    out[0] = lerpq(TF[i0].x, TF[i1].x, a);
+    out[1] = lerpq(TF[i0].y, TF[i1].y, a);
+    out[2] = lerpq(TF[i0].z, TF[i1].z, a);
+    out[3] = lerpq(TF[i0].w, TF[i1].w, a);
+}
+
+/* __saturatef: clamp to [0,1], NaN -> 0 */
+static inline float sat(float x) {
+    if (!(x > 0.0f)) return 0.0f;
+    return x > 1.0f ? 1.0f : x;
+}
+
+/* rgbaFloatToInt, K:186-193 (truncating float->uint) */
+uint32_t orc_pack(const float rgba[4]) {
+    float r = sat(rgba[0]), g = sat(rgba[1]), b = sat(rgba[2]), a = sat(rgba[3]);
+    return ((uint32_t)(a * 255.0f) << 24) | ((uint32_t)(b * 255.0f) << 16) |
+           ((uint32_t)(g * 255.0f) << 8) | (uint32_t)(r * 255.0f);
+}
+
+/* K:736-738: float MaxHistogram = 0.0217; binWidth = (Max - Min) / (float)nBins */
+static inline float bin_width(int nbins) {
+    const float maxh = (float)0.0217;
+    const float minh = 0.0f;
+    return (maxh - minh) / (float)nbins;
+}
+
+/* K:742-747 (also K:359-366): mean += p * (binWidth * i + binWidth / 2.0) */
+static inline float raw_mean(const float *p, int nbins) {
+    const float bw = bin_width(nbins);
+    float mean = 0.0f;
+    for (int i = 0; i < nbins; i++) {
+        double c = (double)(bw * (float)i) + (double)bw / 2.0;
+        mean = (float)((double)mean + (double)p[i] * c);
+    }
+    return mean;
+}
+
+float orc_corner_mean(const float *rec, int nbins) { return raw_mean(rec, nbins); }
+
+static inline float entropy_norm(int nbins) {
+    /* K:769: log((float)nBins) / log(2.0f), both float overloads */
+    return logf_cr((float)nbins) / logf_cr(2.0f);
+}
+
+/* d_basicDataProcessing statistics, K:742-773 */
+static void stats3(const float *p, int nbins, float enorm, int want, float out[3]) {
+    const float maxh = (float)0.0217;
+    float mean = raw_mean(p, nbins);
+    float var = 0.0f;
+    if (want & 2) {
+        for (int i = 0; i < nbins; i++) { /* K:750-755 */
+            float d = ((float)i / (float)nbins) * maxh - mean;
+            var = var + p[i] * d * d;
+        }
+    }
+    out[0] = (float)((double)mean / 0.0217);   /* K:758 */
+    out[1] = (float)((double)var / 0.000021);  /* K:759 */
+    float ent = 0.0f;
+    if (want & 4) {
+        for (int i = 0; i < nbins; i++) { /* K:762-767 */
+            float pr = p[i];
+            double t = pr <= 0 ? 0.0 : ((double)logf_cr(pr) / LN2_D);
+            ent = (float)((double)ent + (double)pr * t);
+        }
+        ent = -ent;          /* K:768 */
+        ent = ent / enorm;   /* K:769 */
+    }
+    out[2] = ent;
+}
+
+void orc_record_stats(const float *rec, int nbins, float out[3]) {
+    stats3(rec, nbins, entropy_norm(nbins), 7, out);
+}
+
+/* ------------------------------------------------------------------------ */
+/* per-ray march, K:272-717                                                  */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+    const float *vol;
+    int nx, ny, nz, nb;
+    float enorm;
+    uint64_t *mark; /* optional footprint bitset */
+} vol_t;
+
+static inline const float *rec_at(const vol_t *v, int x, int y, int z) {
+    size_t idx = ((size_t)z * (size_t)v->ny + (size_t)y) * (size_t)v->nx + (size_t)x;
+    return v->vol + idx * (size_t)v->nb;
+}
+
+static inline void mark_voxel(const vol_t *v, int x, int y, int z) {
+    size_t idx = ((size_t)z * (size_t)v->ny + (size_t)y) * (size_t)v->nx + (size_t)x;
+    __atomic_fetch_or(&v->mark[idx >> 6], (uint64_t)1 << (idx & 63), __ATOMIC_RELAXED);
+}
+
+/* methods 1/2/3: tex3D(originalQueryTex, p) with hardware trilinear (K:601, 619,
+ * 635; texture set up K:1864-1869), the statistic decoded from the 8 corner
+ * records instead of a pre-baked float4 volume (algebraically identical). */
+static float sample_stat(const vol_t *v, f3 pos, int comp) {
+    float px = pos.x * 0.5f + 0.5f;
+    float py = pos.y * 0.5f + 0.5f;
+    float pz = pos.z * 0.5f + 0.5f;
+    int x0, x1, y0, y1, z0, z1;
+    float ax, ay, az;
+    lin_axis(px, v->nx, &x0, &x1, &ax);
+    lin_axis(py, v->ny, &y0, &y1, &ay);
+    lin_axis(pz, v->nz, &z0, &z1, &az);
+    if (v->mark) {
+        mark_voxel(v, x0, y0, z0); mark_voxel(v, x1, y0, z0);
+        mark_voxel(v, x0, y1, z0); mark_voxel(v, x1, y1, z0);
+        mark_voxel(v, x0, y0, z1); mark_voxel(v, x1, y0, z1);
+        mark_voxel(v, x0, y1, z1); mark_voxel(v, x1, y1, z1);
+    }
+    const int want = comp == 0 ? 1 : (comp == 1 ? 3 : 4);
+    float s[8][3];
+    stats3(rec_at(v, x0, y0, z0), v->nb, v->enorm, want, s[0]);
+    stats3(rec_at(v, x1, y0, z0), v->nb, v->enorm, want, s[1]);
+    stats3(rec_at(v, x0, y1, z0), v->nb, v->enorm, want, s[2]);
+    stats3(rec_at(v, x1, y1, z0), v->nb, v->enorm, want, s[3]);
+    stats3(rec_at(v, x0, y0, z1), v->nb, v->enorm, want, s[4]);
+    stats3(rec_at(v, x1, y0, z1), v->nb, v->enorm, want, s[5]);
+    stats3(rec_at(v, x0, y1, z1), v->nb, v->enorm, want, s[6]);
+    stats3(rec_at(v, x1, y1, z1), v->nb, v->enorm, want, s[7]);
+    float c00 = lerpq(s[0][comp], s[1][comp], ax);
+    float c10 = lerpq(s[2][comp], s[3][comp], ax);
+    float c01 = lerpq(s[4][comp], s[5][comp], ax);
+    float c11 = lerpq(s[6][comp], s[7][comp], ax);
+    float c0 = lerpq(c00, c10, ay);
+    float c1 = lerpq(c01, c11, ay);
+    return lerpq(c0, c1, az);
+}
+
+/* method 7 corner state, K:320-367 / K:398-463 */
+typedef struct {
+    f3 ip[8];
+    float mean[8];
+} m7_t;
+
+static void m7_refresh(const vol_t *v, const int N[3], f3 pos, m7_t *m) {
+    float qx = pos.x * 0.5f + 0.5f, qy = pos.y * 0.5f + 0.5f, qz = pos.z * 0.5f + 0.5f;
+    float fx = floorf(qx * (float)N[0]) / (float)N[0];
+    float cx = ceilf(qx * (float)N[0]) / (float)N[0];
+    float fy = floorf(qy * (float)N[1]) / (float)N[1];
+    float cy = ceilf(qy * (float)N[1]) / (float)N[1];
+    float fz = floorf(qz * (float)N[2]) / (float)N[2];
+    float cz = ceilf(qz * (float)N[2]) / (float)N[2];
+    for (int j = 0; j < 8; j++) {
+        m->ip[j].x = (j & 1) ? cx : fx;
+        m->ip[j].y = (j & 2) ? cy : fy;
+        m->ip[j].z = (j & 4) ? cz : fz;
+        int ix = point_axis(m->ip[j].x, v->nx);
+        int iy = point_axis(m->ip[j].y, v->ny);
+        int iz = point_axis(m->ip[j].z, v->nz);
+        m->mean[j] = raw_mean(rec_at(v, ix, iy, iz), v->nb);
+    }
+}
+
+/* inInterpolation, K:253-270 */
+static inline int m7_inside(f3 pos, const m7_t *m) {
+    float qx = pos.x * 0.5f + 0.5f, qy = pos.y * 0.5f + 0.5f, qz = pos.z * 0.5f + 0.5f;
+    if (qx < m->ip[0].x || qy < m->ip[0].y || qz < m->ip[0].z || qx > m->ip[7].x ||
+        qy > m->ip[7].y || qz > m->ip[7].z)
+        return 0;
+    return 1;
+}
+
+/* K:466-479 */
+static float m7_sample(f3 pos, const m7_t *m) {
+    float xd = (pos.x * 0.5f + 0.5f - m->ip[0].x) / (m->ip[1].x - m->ip[0].x);
+    float yd = (pos.y * 0.5f + 0.5f - m->ip[0].y) / (m->ip[2].y - m->ip[0].y);
+    float zd = (pos.z * 0.5f + 0.5f - m->ip[0].z) / (m->ip[4].z - m->ip[0].z);
+    const float *mn = m->mean;
+    float m00 = (float)((double)mn[0] * (1.0 - (double)xd) + (double)(mn[1] * xd));
+    float m10 = (float)((double)mn[2] * (1.0 - (double)xd) + (double)(mn[3] * xd));
+    float m01 = (float)((double)mn[4] * (1.0 - (double)xd) + (double)(mn[5] * xd));
+    float m11 = (float)((double)mn[6] * (1.0 - (double)xd) + (double)(mn[7] * xd));
+    float m0 = (float)((double)m00 * (1.0 - (double)yd) + (double)(m10 * yd));
+    float m1 = (float)((double)m01 * (1.0 - (double)yd) + (double)(m11 * yd));
+    float im = (float)((double)m0 * (1.0 - (double)zd) + (double)(m1 * zd));
+    return im * 50.0f; /* K:479 */
+}
+
+static inline float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+/* one pixel; returns samples taken, -1 on a miss */
+static int render_pixel(const vol_t *v, const orc_render_params *p, int x, int y,
+                        float rgba[4]) {
+    const int maxSteps = 500;          /* K:276 */
+    const float tstep = 0.01f;         /* K:277 */
+    const float opacityThreshold = 0.95f;
+    const float *M = p->inv_view;
+
+    float u = ((float)x / (float)p->width) * 2.0f - 1.0f;  /* K:288 */
+    float vv = ((float)y / (float)p->height) * 2.0f - 1.0f; /* K:289 */
+
+    /* K:293-296 */
+    f3 o;
+    o.x = 0.0f * M[0] + 0.0f * M[1] + 0.0f * M[2] + 1.0f * M[3];
+    o.y = 0.0f * M[4] + 0.0f * M[5] + 0.0f * M[6] + 1.0f * M[7];
+    o.z = 0.0f * M[8] + 0.0f * M[9] + 0.0f * M[10] + 1.0f * M[11];
+    f3 d0 = {u, vv, -2.0f};
+    float inv = 1.0f / sqrtf(dot3(d0, d0));
+    d0.x = d0.x * inv; d0.y = d0.y * inv; d0.z = d0.z * inv;
+    f3 d;
+    d.x = d0.x * M[0] + d0.y * M[1] + d0.z * M[2];
+    d.y = d0.x * M[4] + d0.y * M[5] + d0.z * M[6];
+    d.z = d0.x * M[8] + d0.y * M[9] + d0.z * M[10];
+
+    /* intersectBox, K:136-156 */
+    f3 invR = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    f3 tbot = {invR.x * (-1.0f - o.x), invR.y * (-1.0f - o.y), invR.z * (-1.0f - o.z)};
+    f3 ttop = {invR.x * (1.0f - o.x), invR.y * (1.0f - o.y), invR.z * (1.0f - o.z)};
+    f3 tmin = {fminf(ttop.x, tbot.x), fminf(ttop.y, tbot.y), fminf(ttop.z, tbot.z)};
+    f3 tmax = {fmaxf(ttop.x, tbot.x), fmaxf(ttop.y, tbot.y), fmaxf(ttop.z, tbot.z)};
+    float tnear = fmaxf(fmaxf(tmin.x, tmin.y), fmaxf(tmin.x, tmin.z));
+    float tfar = fminf(fminf(tmax.x, tmax.y), fminf(tmax.x, tmax.z));
+    if (!(tfar > tnear)) return -1; /* K:302-303: no write */
+    if (tnear < 0.0f) tnear = 0.0f;
+
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = tnear;
+    f3 pos = {o.x + d.x * tnear, o.y + d.y * tnear, o.z + d.z * tnear};
+    f3 step = {d.x * tstep, d.y * tstep, d.z * tstep};
+
+    m7_t m7;
+    const int method = p->query_method;
+    if (method == 7) m7_refresh(v, p->m7_dims, pos, &m7); /* K:320-367 */
+
+    int n = 0;
+    for (int i = 0; i < maxSteps; i++) {
+        float sample = 0.5f; /* K:383 */
+        if (method == 7) {
+            if (!m7_inside(pos, &m7)) m7_refresh(v, p->m7_dims, pos, &m7);
+            sample = m7_sample(pos, &m7);
+        } else if (method == 1) {
+            sample = sample_stat(v, pos, 0);
+        } else if (method == 2) {
+            sample = sample_stat(v, pos, 1);
+        } else if (method == 3) {
+            sample = sample_stat(v, pos, 2);
+        }
+        n = i + 1;
+        float col[4];
+        orc_transfer((sample - p->transfer_offset) * p->transfer_scale, col); /* K:683 */
+        col[3] = col[3] * p->density;   /* K:685 */
+        col[0] = col[0] * col[3];       /* K:691-693 */
+        col[1] = col[1] * col[3];
+        col[2] = col[2] * col[3];
+        float om = 1.0f - sw;           /* K:695 */
+        sx = sx + col[0] * om;
+        sy = sy + col[1] * om;
+        sz = sz + col[2] * om;
+        sw = sw + col[3] * om;
+        if (sw > opacityThreshold) break; /* K:698 */
+        t = t + tstep;                    /* K:701 */
+        if (t > tfar) break;              /* K:703 */
+        pos.x = pos.x + step.x;           /* K:706 */
+        pos.y = pos.y + step.y;
+        pos.z = pos.z + step.z;
+    }
+    rgba[0] = sx * p->brightness; /* K:713 */
+    rgba[1] = sy * p->brightness;
+    rgba[2] = sz * p->brightness;
+    rgba[3] = sw * p->brightness;
+    return n;
+}
+
+static void run_rows(const vol_t *v, const orc_render_params *p, uint32_t *out,
+                     float *out_f, int32_t *out_n, int row_start, int row_stride,
+                     int nthreads, int64_t *total) {
+    if (row_stride < 1) row_stride = 1;
+    int nrows = row_start < p->height ? (p->height - 1 - row_start) / row_stride + 1 : 0;
+    int64_t acc = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(+ : acc)
+#endif
+    for (int r = 0; r < nrows; r++) {
+        int y = row_start + r * row_stride;
+        for (int x = 0; x < p->width; x++) {
+            float rgba[4];
+            int n = render_pixel(v, p, x, y, rgba);
+            size_t pix = (size_t)y * (size_t)p->width + (size_t)x;
+            if (out_n) out_n[pix] = n;
+            if (n < 0) continue;
+            acc += n;
+            if (out) out[pix] = orc_pack(rgba);
+            if (out_f) {
+                out_f[pix * 4 + 0] = sat(rgba[0]);
+                out_f[pix * 4 + 1] = sat(rgba[1]);
+                out_f[pix * 4 + 2] = sat(rgba[2]);
+                out_f[pix * 4 + 3] = sat(rgba[3]);
+            }
+        }
+    }
+    (void)nthreads;
+    *total = acc;
+}
+
+int64_t orc_render(const float *vol, int nx, int ny, int nz, int nbins,
+                   const orc_render_params *p, uint32_t *out, float *out_f,
+                   int32_t *out_n, int row_start, int row_stride, int nthreads) {
+    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), NULL};
+    int64_t total = 0;
+    run_rows(&v, p, out, out_f, out_n, row_start, row_stride, nthreads, &total);
+    return total;
+}
+
+int64_t orc_count_footprint(const float *vol, int nx, int ny, int nz, int nbins,
+                            const orc_render_params *p, int nthreads) {
+    size_t nvox = (size_t)nx * (size_t)ny * (size_t)nz;
+    size_t nwords = (nvox + 63) / 64;
+    uint64_t *mark = (uint64_t *)calloc(nwords, sizeof(uint64_t));
+    if (!mark) return -1;
+    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), mark};
+    int64_t total = 0;
+    run_rows(&v, p, NULL, NULL, NULL, 0, 1, nthreads, &total);
+    int64_t u = 0;
+    for (size_t i = 0; i < nwords; i++) u += __builtin_popcountll(mark[i]);
+    free(mark);
+    return u;
+}
+
+/* ------------------------------------------------------------------------ */
+/* synthetic distribution volume                       */
+/* ------------------------------------------------------------------------ */
+
+uint64_t orc_splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static inline double u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+
+#define SYN_K 8
+#define SYN_G 16
+#define SYN_Q 4096
+
+static void axis_table(int n, double c, double s, float *out) {
+    for (int i = 0; i < n; i++) {
+        double q = ((double)i + 0.5) / (double)n;
+        out[i] = (float)exp(-(q - c) * (q - c) / (2.0 * s * s));
+    }
+}
+
+void orc_synth_fill(int nx, int ny, int nz, int nbins, uint64_t seed, float *vol,
+                    int nthreads) {
+    float amp[SYN_K];
+    float *gx = (float *)malloc(sizeof(float) * SYN_K * (size_t)nx);
+    float *gy = (float *)malloc(sizeof(float) * SYN_K * (size_t)ny);
+    float *gz = (float *)malloc(sizeof(float) * SYN_K * (size_t)nz);
+    for (int k = 0; k < SYN_K; k++) {
+        double r[5];
+        for (int j = 0; j < 5; j++) r[j] = u01(orc_splitmix64(seed + 0x100u + 8u * (uint64_t)k + (uint64_t)j));
+        amp[k] = (float)(0.3 + 0.7 * r[0]);
+        double s = 0.05 + 0.15 * r[4];
+        axis_table(nx, 0.2 + 0.6 * r[1], s, gx + (size_t)k * nx);
+        axis_table(ny, 0.2 + 0.6 * r[2], s, gy + (size_t)k * ny);
+        axis_table(nz, 0.2 + 0.6 * r[3], s, gz + (size_t)k * nz);
+    }
+    float *tab = NULL;
+    if (nbins > 1) {
+        tab = (float *)malloc(sizeof(float) * SYN_G * SYN_Q * (size_t)nbins);
+        double *e = (double *)malloc(sizeof(double) * (size_t)nbins);
+        for (int g = 0; g < SYN_G; g++) {
+            double sig = 0.02 + 0.1 * (double)g / 15.0;
+            for (int q = 0; q < SYN_Q; q++) {
+                double mu = ((double)q + 0.5) / (double)SYN_Q;
+                double sum = 0.0;
+                for (int b = 0; b < nbins; b++) {
+                    double dd = ((double)b + 0.5) / (double)nbins - mu;
+                    e[b] = exp(-dd * dd / (2.0 * sig * sig));
+                    sum += e[b];
+                }
+                float *row = tab + ((size_t)g * SYN_Q + (size_t)q) * (size_t)nbins;
+                for (int b = 0; b < nbins; b++) row[b] = (float)(e[b] / sum);
+            }
+        }
+        free(e);
+    }
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int z = 0; z < nz; z++) {
+        for (int y = 0; y < ny; y++) {
+            for (int x = 0; x < nx; x++) {
+                float f = 0.0f;
+                for (int k = 0; k < SYN_K; k++)
+                    f = f + ((amp[k] * gx[(size_t)k * nx + x]) * gy[(size_t)k * ny + y]) *
+                                gz[(size_t)k * nz + z];
+                if (f > 1.0f) f = 1.0f;
+                uint64_t vidx = ((uint64_t)z * (uint64_t)ny + (uint64_t)y) * (uint64_t)nx + (uint64_t)x;
+                float *rec = vol + vidx * (uint64_t)nbins;
+                if (nbins == 1) {
+                    rec[0] = f;
+                } else {
+                    int q = (int)(f * 4096.0f);
+                    if (q > SYN_Q - 1) q = SYN_Q - 1;
+                    int g = (int)(orc_splitmix64(seed ^ vidx) & (SYN_G - 1));
+                    memcpy(rec, tab + ((size_t)g * SYN_Q + (size_t)q) * (size_t)nbins,
+                           sizeof(float) * (size_t)nbins);
+                }
+            }
+        }
+    }
+    (void)nthreads;
+    free(tab);
+    free(gx);
+    free(gy);
+    free(gz);
+}

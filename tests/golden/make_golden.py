@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures from the CPU oracle.
+
+Each fixture holds the scene description (volume dims/bins/seed + a checksum of
+the generated volume, camera matrix, render parameters) and the expected
+outputs: packed RGBA8, samples per pixel and, for the small images, the float
+RGBA.  The reference itself ships no golden image, so these pin
+the oracle's restatement (cross-checked against tests/ref_numpy.py and the
+analytic KATs in tests/test_oracle.py) against accidental drift, and the GPU
+tests compare the HIP kernel with them too.
+
+  python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import __graft_entry__ as graft  # noqa: E402
+
+SEED = 20261015
+
+
+def scenes(cam):
+    c0, c1 = cam.single_test_inv_view(), cam.display_inv_view((30.0, 45.0))
+    out = []
+    for method in (1, 2, 3, 7):
+        out.append((f"vol16x4_c0_m{method}", (16, 16, 16, 4), (64, 64), c0, method, True))
+        out.append((f"vol16x4_c1_m{method}", (16, 16, 16, 4), (64, 64), c1, method, True))
+        # the reference's own data shape: Isabel 50x50x10 blocks x 32 bins (C:86-87)
+        out.append((f"isabel50x50x10x32_c0_m{method}", (50, 50, 10, 32), (128, 128), c0,
+                    method, False))
+    out.append(("vol24x20x16x8_c1_m1_256x160", (24, 20, 16, 8), (256, 160), c1, 1, False))
+    out.append(("vol32x1_c0_m1", (32, 32, 32, 1), (64, 64), c0, 1, True))
+    return out
+
+
+def main():
+    orc = graft.load_oracle()
+    cam = graft.load_package().camera
+    for name, (nx, ny, nz, nb), (W, H), m, method, keep_f in scenes(cam):
+        vol = orc.synth_volume(nx, ny, nz, nb, SEED)
+        p = orc.make_params(W, H, m, query_method=method, m7_dims=(nx, ny, nz))
+        out, f, n, _ = orc.render(vol, p)
+        arrays = dict(
+            dims=np.array([nx, ny, nz, nb]), seed=np.uint64(SEED),
+            vol_crc=np.uint32(np.bitwise_xor.reduce(vol.view(np.uint32).ravel())),
+            image=np.array([W, H]), inv_view=np.asarray(m, np.float32),
+            density=np.float32(0.05), brightness=np.float32(1.0), toff=np.float32(0.0),
+            tscale=np.float32(1.0), method=np.int32(method),
+            m7_dims=np.array([nx, ny, nz]), rgba8=out, steps=n.astype(np.int16))
+        if keep_f:
+            arrays["rgba_f"] = f
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
+        print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,211 @@
+"""Independent numpy restatement of d_render (methods 1/2/3/7) for small cases.
+
+Test infrastructure: a second, separately written reading of the reference
+(volumeRender_kernel.cu = K) used to cross-check the C oracle bit for bit.
+numpy float32 arithmetic is IEEE single precision without contraction, which is
+the canonical arithmetic of DESIGN.md section 3; float64 is used exactly where
+the reference source promotes to double.
+"""
+import numpy as np
+
+f32 = np.float32
+TF = np.array([[0, 0, 0, 0], [1, 0, 0, 1], [1, .5, 0, 1], [1, 1, 0, 1], [0, 1, 0, 1],
+               [0, 1, 1, 1], [0, 0, 1, 1], [1, 0, 1, 1], [0, 0, 0, 0]], dtype=np.float32)
+LN2 = np.float64(0.6931471805599453)
+
+
+def _clamp01(u):
+    return np.fmin(np.fmax(u, f32(0)), f32(1))
+
+
+def _lin(u, n):
+    u = _clamp01(u)
+    xb = u * f32(n) - f32(0.5)
+    fl = np.floor(xb)
+    a = np.rint((xb - fl) * f32(256)) * f32(1.0 / 256)
+    i = fl.astype(np.int64)
+    return np.clip(i, 0, n - 1), np.clip(i + 1, 0, n - 1), a.astype(np.float32)
+
+
+def _point(u, n):
+    u = _clamp01(u)
+    return np.minimum(np.floor(u * f32(n)).astype(np.int64), n - 1)
+
+
+def _lerp(a, b, t):
+    return (f32(1) - t) * a + t * b
+
+
+def transfer(x):
+    i0, i1, a = _lin(np.asarray(x, dtype=np.float32), 9)
+    return _lerp(TF[i0], TF[i1], a[..., None])
+
+
+def _bw(nb):
+    return (f32(0.0217) - f32(0)) / f32(nb)
+
+
+def raw_mean(p):
+    """p: (..., B) float32 records -> float32 (K:742-747)"""
+    nb = p.shape[-1]
+    bw = _bw(nb)
+    mean = np.zeros(p.shape[:-1], dtype=np.float32)
+    for i in range(nb):
+        c = np.float64(bw * f32(i)) + np.float64(bw) / 2.0
+        mean = (mean.astype(np.float64) + p[..., i].astype(np.float64) * c).astype(np.float32)
+    return mean
+
+
+def stat(p, comp):
+    nb = p.shape[-1]
+    mean = raw_mean(p)
+    if comp == 0:
+        return (mean.astype(np.float64) / 0.0217).astype(np.float32)
+    if comp == 1:
+        var = np.zeros_like(mean)
+        for i in range(nb):
+            d = (f32(i) / f32(nb)) * f32(0.0217) - mean
+            var = var + p[..., i] * d * d
+        return (var.astype(np.float64) / 0.000021).astype(np.float32)
+    ent = np.zeros_like(mean)
+    enorm = np.float32(np.log(np.float64(f32(nb)))) / np.float32(np.log(np.float64(f32(2))))
+    for i in range(nb):
+        pr = p[..., i]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            lg = np.log(pr.astype(np.float64)).astype(np.float32).astype(np.float64) / LN2
+        t = np.where(pr <= 0, 0.0, lg)
+        ent = (ent.astype(np.float64) + pr.astype(np.float64) * t).astype(np.float32)
+    return (-ent) / enorm
+
+
+def render(vol, W, H, m, method=1, density=0.05, brightness=1.0, toff=0.0, tscale=1.0,
+           m7_dims=None, footprint=None):
+    """Returns (rgba float32 (H,W,4) saturated, steps int (H,W), -1 = miss).
+    footprint: optional set, receives the flat indices of every voxel read by a
+    trilinear footprint of a sample taken (methods 1/2/3)."""
+    with np.errstate(all="ignore"):
+        return _render(vol, W, H, m, method, density, brightness, toff, tscale, m7_dims,
+                       footprint)
+
+
+def _render(vol, W, H, m, method, density, brightness, toff, tscale, m7_dims, footprint):
+    vol = np.asarray(vol, dtype=np.float32)
+    nz, ny, nx, nb = vol.shape
+    M = np.asarray(m, dtype=np.float32).reshape(12)
+    ys, xs = np.mgrid[0:H, 0:W]
+    u = (xs.astype(np.float32) / f32(W)) * f32(2) - f32(1)
+    v = (ys.astype(np.float32) / f32(H)) * f32(2) - f32(1)
+    o = np.array([f32(0) * M[4 * r] + f32(0) * M[4 * r + 1] + f32(0) * M[4 * r + 2]
+                  + f32(1) * M[4 * r + 3] for r in range(3)], dtype=np.float32)
+    inv = f32(1) / np.sqrt(u * u + v * v + f32(-2) * f32(-2))
+    d0 = [u * inv, v * inv, f32(-2) * inv]
+    d = [d0[0] * M[4 * r] + d0[1] * M[4 * r + 1] + d0[2] * M[4 * r + 2] for r in range(3)]
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        invR = [f32(1) / d[k] for k in range(3)]
+        tb = [invR[k] * (f32(-1) - o[k]) for k in range(3)]
+        tt = [invR[k] * (f32(1) - o[k]) for k in range(3)]
+    tmn = [np.fmin(tt[k], tb[k]) for k in range(3)]
+    tmx = [np.fmax(tt[k], tb[k]) for k in range(3)]
+    tnear = np.fmax(np.fmax(tmn[0], tmn[1]), np.fmax(tmn[0], tmn[2]))
+    tfar = np.fmin(np.fmin(tmx[0], tmx[1]), np.fmin(tmx[0], tmx[2]))
+    hit = tfar > tnear
+    tnear = np.where(tnear < 0, f32(0), tnear).astype(np.float32)
+    pos = [o[k] + d[k] * tnear for k in range(3)]
+    step = [d[k] * f32(0.01) for k in range(3)]
+    t = tnear.copy()
+    s = np.zeros((H, W, 4), dtype=np.float32)
+    n = np.where(hit, 0, -1)
+    active = hit.copy()
+    dims = (nx, ny, nz)
+    if method == 7:
+        N = m7_dims or dims
+        fpos, cpos, means = None, None, None
+
+    def m7_refresh(mask, pos, fpos, cpos, means):
+        q = [pos[k] * f32(0.5) + f32(0.5) for k in range(3)]
+        nf = [np.floor(q[k] * f32(N[k])) / f32(N[k]) for k in range(3)]
+        nc = [np.ceil(q[k] * f32(N[k])) / f32(N[k]) for k in range(3)]
+        nm = np.zeros((H, W, 8), dtype=np.float32)
+        for j in range(8):
+            cx = nc[0] if j & 1 else nf[0]
+            cy = nc[1] if j & 2 else nf[1]
+            cz = nc[2] if j & 4 else nf[2]
+            rec = vol[_point(cz, nz), _point(cy, ny), _point(cx, nx)]
+            nm[..., j] = raw_mean(rec)
+        if fpos is None:
+            return nf, nc, nm
+        for k in range(3):
+            fpos[k] = np.where(mask, nf[k], fpos[k])
+            cpos[k] = np.where(mask, nc[k], cpos[k])
+        means = np.where(mask[..., None], nm, means)
+        return fpos, cpos, means
+
+    if method == 7:
+        fpos, cpos, means = m7_refresh(hit, pos, None, None, None)
+    for i in range(500):
+        if not active.any():
+            break
+        if method == 7:
+            q = [pos[k] * f32(0.5) + f32(0.5) for k in range(3)]
+            out = np.zeros_like(active)
+            for k in range(3):
+                out |= (q[k] < fpos[k]) | (q[k] > cpos[k])
+            if (out & active).any():
+                fpos, cpos, means = m7_refresh(out & active, pos, fpos, cpos, means)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                xd = (pos[0] * f32(0.5) + f32(0.5) - fpos[0]) / (cpos[0] - fpos[0])
+                yd = (pos[1] * f32(0.5) + f32(0.5) - fpos[1]) / (cpos[1] - fpos[1])
+                zd = (pos[2] * f32(0.5) + f32(0.5) - fpos[2]) / (cpos[2] - fpos[2])
+            mn = means.astype(np.float64)
+
+            def bl(a, b, w):
+                with np.errstate(invalid="ignore"):
+                    return (a.astype(np.float64) * (1.0 - w.astype(np.float64))
+                            + (b * w).astype(np.float64)).astype(np.float32)
+            m00 = bl(mn[..., 0].astype(np.float32), mn[..., 1].astype(np.float32), xd)
+            m10 = bl(mn[..., 2].astype(np.float32), mn[..., 3].astype(np.float32), xd)
+            m01 = bl(mn[..., 4].astype(np.float32), mn[..., 5].astype(np.float32), xd)
+            m11 = bl(mn[..., 6].astype(np.float32), mn[..., 7].astype(np.float32), xd)
+            m0 = bl(m00, m10, yd)
+            m1 = bl(m01, m11, yd)
+            sample = bl(m0, m1, zd) * f32(50)
+        else:
+            comp = method - 1
+            ax = [_lin(pos[k] * f32(0.5) + f32(0.5), dims[k]) for k in range(3)]
+            vals = []
+            for j in range(8):
+                xi = ax[0][1] if j & 1 else ax[0][0]
+                yi = ax[1][1] if j & 2 else ax[1][0]
+                zi = ax[2][1] if j & 4 else ax[2][0]
+                vals.append(stat(vol[zi, yi, xi], comp))
+                if footprint is not None:
+                    flat = (zi * ny + yi) * nx + xi
+                    footprint.update(np.unique(flat[active]).tolist())
+            c00 = _lerp(vals[0], vals[1], ax[0][2])
+            c10 = _lerp(vals[2], vals[3], ax[0][2])
+            c01 = _lerp(vals[4], vals[5], ax[0][2])
+            c11 = _lerp(vals[6], vals[7], ax[0][2])
+            sample = _lerp(_lerp(c00, c10, ax[1][2]), _lerp(c01, c11, ax[1][2]), ax[2][2])
+        col = transfer((sample - f32(toff)) * f32(tscale))
+        cw = col[..., 3] * f32(density)
+        col = np.stack([col[..., 0] * cw, col[..., 1] * cw, col[..., 2] * cw, cw], -1)
+        om = f32(1) - s[..., 3]
+        ns = s + col * om[..., None]
+        s = np.where(active[..., None], ns, s)
+        n = np.where(active, i + 1, n)
+        done = s[..., 3] > f32(0.95)
+        t = np.where(active & ~done, t + f32(0.01), t).astype(np.float32)
+        done |= t > tfar
+        active &= ~done
+        pos = [np.where(active, pos[k] + step[k], pos[k]).astype(np.float32) for k in range(3)]
+    out = s * f32(brightness)
+    out = np.where(out > 0, np.where(out > 1, f32(1), out), f32(0))
+    out = np.where(hit[..., None], out, f32(0))
+    return out.astype(np.float32), n
+
+
+def pack(rgba):
+    r = np.asarray(rgba, dtype=np.float32)
+    c = np.where(r > 0, np.where(r > 1, f32(1), r), f32(0))
+    q = (c * f32(255)).astype(np.uint32)
+    return (q[..., 3] << 24) | (q[..., 2] << 16) | (q[..., 1] << 8) | q[..., 0]

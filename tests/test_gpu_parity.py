@@ -1,0 +1,220 @@
+"""GPU parity: the HIP march (through the C-ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): packed RGBA8 identical, float RGBA within
+1e-4 per channel, samples-per-pixel identical, on the same seeded inputs.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4  # max per-channel |RGBA - oracle| (north_star)
+
+
+def gpu_render(pkg, vol_or_none, W, H, m, method, torch, density=0.05, brightness=1.0,
+               toff=0.0, tscale=1.0, m7=None, tile_list=None):
+    if vol_or_none is not None:
+        pkg.init_distribution(vol_or_none)
+    dims = pkg.volume_info()[0]
+    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    out_f = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+    steps = torch.full((H * W,), -2, dtype=torch.int32, device="cuda")
+    d = pkg.make_desc(out, W, H, m, density=density, brightness=brightness,
+                      transfer_offset=toff, transfer_scale=tscale, query_method=method,
+                      volume_size=m7 or dims, d_output_f=out_f, d_steps=steps)
+    pkg.render(d)
+    torch.cuda.synchronize()
+    return (out.cpu().numpy().view(np.uint32).reshape(H, W),
+            out_f.cpu().numpy().reshape(H, W, 4), steps.cpu().numpy().reshape(H, W))
+
+
+def assert_parity(got, ref, what):
+    g8, gf, gn = got
+    r8, rf, rn = ref
+    hit = rn >= 0
+    assert np.array_equal(gn[hit], rn[hit]), f"{what}: samples per pixel differ"
+    assert np.all(gn[~hit] == -1), f"{what}: miss pixels must report -1"
+    assert np.array_equal(g8, r8), (
+        f"{what}: {int(np.sum(g8 != r8))} RGBA8 pixels differ from the oracle")
+    err = float(np.max(np.abs(gf - rf))) if gf.size else 0.0
+    assert err <= TOL, f"{what}: max |RGBA - oracle| = {err}"
+
+
+@pytest.mark.parametrize("method", [1, 2, 3, 7])
+@pytest.mark.parametrize("cam", ["C0", "C1"])
+@pytest.mark.parametrize("nb", [1, 4, 8])
+def test_small_scene(pkg, orc, gpu, method, cam, nb):
+    import torch
+    vol = orc.synth_volume(24, 20, 16, nb)
+    m = pkg.camera.single_test_inv_view() if cam == "C0" else pkg.camera.display_inv_view()
+    W, H = 96, 72
+    got = gpu_render(pkg, vol, W, H, m, method, torch)
+    p = orc.make_params(W, H, m, query_method=method, m7_dims=(24, 20, 16))
+    ref = orc.render(vol, p)[:3]
+    assert_parity(got, ref, f"24x20x16x{nb} {cam} m{method}")
+
+
+@pytest.mark.parametrize("nb", [2, 3, 5, 16, 32])
+def test_bin_counts(pkg, orc, gpu, nb):
+    """compiled specialisations (2, 16, 32) and the runtime-B path (3, 5)"""
+    import torch
+    vol = orc.synth_volume(12, 14, 10, nb)
+    m = pkg.camera.display_inv_view((20.0, -35.0))
+    for method in (1, 2, 3, 7):
+        got = gpu_render(pkg, vol, 48, 40, m, method, torch)
+        ref = orc.render(vol, orc.make_params(48, 40, m, query_method=method,
+                                              m7_dims=(12, 14, 10)))[:3]
+        assert_parity(got, ref, f"nb={nb} m{method}")
+
+
+def test_reference_isabel_shape_via_reference_api(pkg, orc, gpu):
+    """The reference's own shape: 50x50x10 blocks x 32 bins, initCuda + render_kernel at
+    512x512 with the runSingleTest camera (C:1016-1067)."""
+    import torch
+    vol = orc.synth_volume(50, 50, 10, 32)
+    W = H = 512
+    pkg.initCuda(vol.reshape(-1), (50, 50, 10), (32, 2500, 10))
+    m = pkg.camera.single_test_inv_view()
+    pkg.copyInvViewMatrix(m, 48)
+    pkg.basicDataProcessing()
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    for method in (1, 2, 3, 7):
+        out.zero_()  # C:208 / C:1022
+        pkg.render_kernel((32, 32, 1), (16, 16, 1), out, W, H, 0.05, 1.0, 0.0, 1.0, method,
+                          (50, 50, 10))
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32).reshape(H, W)
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=method,
+                                              m7_dims=(50, 50, 10)), want_float=False,
+                         want_steps=False)[0]
+        assert np.array_equal(got, ref), f"m{method}: {int(np.sum(got != ref))} pixels differ"
+    pkg.freeCudaBuffers()
+
+
+@pytest.mark.parametrize("params", [
+    dict(density=0.2, brightness=1.5, toff=0.1, tscale=1.3),
+    dict(density=1.0, brightness=0.7, toff=-0.2, tscale=0.5),
+    dict(density=0.01, brightness=2.0, toff=0.05, tscale=2.0),
+])
+def test_render_parameters(pkg, orc, gpu, params):
+    """density / brightness / transfer offset+scale (keyboard parameters, C:315-345)"""
+    import torch
+    vol = orc.synth_volume(20, 20, 20, 4)
+    m = pkg.camera.display_inv_view((10.0, 70.0))
+    for method in (1, 3):
+        got = gpu_render(pkg, vol, 64, 64, m, method, torch, **params)
+        ref = orc.render(vol, orc.make_params(
+            64, 64, m, density=params["density"], brightness=params["brightness"],
+            transfer_offset=params["toff"], transfer_scale=params["tscale"],
+            query_method=method))[:3]
+        assert_parity(got, ref, f"{params} m{method}")
+
+
+def test_method7_grid_differs_from_volume(pkg, orc, gpu):
+    """render_kernel's volumeSize drives only the method-7 corner grid (K:322-352)."""
+    import torch
+    vol = orc.synth_volume(16, 16, 16, 4)
+    m = pkg.camera.display_inv_view((25.0, 15.0))
+    got = gpu_render(pkg, vol, 64, 64, m, 7, torch, m7=(10, 12, 20))
+    ref = orc.render(vol, orc.make_params(64, 64, m, query_method=7, m7_dims=(10, 12, 20)))[:3]
+    assert_parity(got, ref, "m7 grid 10x12x20 over 16^3")
+
+
+def test_edge_images(pkg, orc, gpu):
+    """ragged image sizes: 1x1, odd sizes, partial tiles"""
+    import torch
+    vol = orc.synth_volume(16, 16, 16, 4)
+    pkg.init_distribution(vol)
+    m = pkg.camera.single_test_inv_view()
+    for W, H in [(1, 1), (17, 3), (33, 65), (250, 7)]:
+        got = gpu_render(pkg, None, W, H, m, 1, torch)
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=1))[:3]
+        assert_parity(got, ref, f"{W}x{H}")
+
+
+def test_camera_inside_volume(pkg, orc, gpu):
+    """eye inside the box: tnear < 0 is clamped to 0 (K:305-306)"""
+    import torch
+    vol = orc.synth_volume(16, 16, 16, 4)
+    m = pkg.camera.display_inv_view((0.0, 0.0), translation=(0.1, -0.2, -0.3))
+    got = gpu_render(pkg, vol, 64, 64, m, 1, torch)
+    ref = orc.render(vol, orc.make_params(64, 64, m, query_method=1))[:3]
+    assert_parity(got, ref, "eye inside")
+
+
+def test_synth_matches_oracle(pkg, orc, gpu):
+    """the on-device generator writes the same volume as the oracle generator"""
+    import torch
+    for dims, nb in [((16, 12, 10), 1), ((16, 12, 10), 4), ((9, 7, 5), 8), ((8, 8, 8), 3),
+                     ((8, 6, 4), 32)]:
+        pkg.synthesize(dims, nb, seed=20261015)
+        (nx, ny, nz), b, ptr = pkg.volume_info()
+        n = nx * ny * nz * b
+        t = torch.empty(n, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        # device-to-device copy of the library-owned volume into a torch tensor
+        hip = ctypes.CDLL("libamdhip64.so")
+        assert hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr),
+                             ctypes.c_size_t(n * 4), 3) == 0
+        got = t.cpu().numpy().reshape(nz, ny, nx, b)
+        ref = orc.synth_volume(nx, ny, nz, b)
+        assert np.array_equal(got, ref), f"synth {dims}x{nb} differs"
+
+
+def test_footprint_count(pkg, orc, gpu):
+    import torch
+    vol = orc.synth_volume(40, 36, 32, 4)
+    pkg.init_distribution(vol)
+    for cam, m in [("C0", pkg.camera.single_test_inv_view()),
+                   ("C1", pkg.camera.display_inv_view())]:
+        for method in (1, 2, 3):
+            out = torch.zeros(128 * 96, dtype=torch.int32, device="cuda")
+            d = pkg.make_desc(out, 128, 96, m, query_method=method)
+            u = pkg.count_footprint(d)
+            ref = orc.count_footprint(vol, orc.make_params(128, 96, m, query_method=method))
+            assert u == ref, f"{cam} m{method}: U {u} != oracle {ref}"
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tile_split_and_unscatter(pkg, orc, gpu, world):
+    """multi-GPU path on one device: each 'rank' renders its tile list into a packed
+    buffer, rank 0 unscatters -> identical to the full-frame render"""
+    import torch
+    vol = orc.synth_volume(32, 32, 32, 8)
+    pkg.init_distribution(vol)
+    W, H = 200, 136
+    m = pkg.camera.display_inv_view()
+    full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.render(pkg.make_desc(full, W, H, m, query_method=1))
+    lists = pkg.tiles.tile_lists(W, H, world)
+    n_slots = lists.shape[1]
+    packed = torch.zeros((world, n_slots * 256), dtype=torch.int32, device="cuda")
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    for r in range(world):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full)
+    ref = orc.render(vol, orc.make_params(W, H, m, query_method=1), want_float=False,
+                     want_steps=False)[0]
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref)
+
+
+def test_errors_do_not_exit(pkg, gpu):
+    import torch
+    vol = np.zeros((4, 4, 4, 2), np.float32)
+    pkg.init_distribution(vol)
+    out = torch.zeros(16, dtype=torch.int32, device="cuda")
+    for bad in (4, 5, 6, 8, 9, 0, 11):
+        with pytest.raises(pkg.VRError):
+            pkg.render_kernel((1, 1, 1), (16, 16, 1), out, 4, 4, 0.05, 1.0, 0.0, 1.0, bad,
+                              (4, 4, 4))
+    with pytest.raises(pkg.VRError):
+        pkg.dataProcessing()
+    pkg.freeCudaBuffers()
+    with pytest.raises(pkg.VRError):
+        pkg.render_kernel((1, 1, 1), (16, 16, 1), out, 4, 4, 0.05, 1.0, 0.0, 1.0, 1, (4, 4, 4))

@@ -1,0 +1,182 @@
+"""CPU oracle pins (no GPU): analytic known-answer tests, the independent numpy
+restatement, and the committed golden fixtures.
+
+The reference ships no golden image or test vectors, so the
+oracle is pinned by (1) KATs derived from the reference source, (2) bit-exact
+agreement with a second, independently written restatement (tests/ref_numpy.py),
+(3) fixtures committed under tests/golden/ (tests/golden/make_golden.py).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import ref_numpy as rn
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def cams(pkg):
+    return {"C0": pkg.camera.single_test_inv_view(), "C1": pkg.camera.display_inv_view()}
+
+
+def test_centre_ray_takes_200_samples(orc, cams):
+    """transparent volume: the centre ray enters at t=3, leaves at t=5 -> 200 steps of 0.01
+    in float32 (K:276-277, 701-704)"""
+    vol = np.zeros((8, 8, 8, 4), np.float32)
+    _, f, n, _ = orc.render(vol, orc.make_params(64, 64, cams["C0"]))
+    assert n[32, 32] == 200
+    assert np.all(f == 0)
+
+
+def test_constant_alpha_terminates_at_59(orc, cams):
+    """per-step alpha 0.05 (stat 0.5 -> TF entry 4, alpha 1, density 0.05):
+    sum.w = 1-(0.95)^n crosses 0.95 at n = 59 (K:685-699)"""
+    vol = np.ones((8, 8, 8, 1), np.float32)  # B=1: mean stat = 0.5
+    _, f, n, _ = orc.render(vol, orc.make_params(64, 64, cams["C0"]))
+    assert n[32, 32] == 59
+    assert abs(f[32, 32, 3] - 0.9515) < 1e-4
+    assert f[32, 32, 1] == f[32, 32, 3] and f[32, 32, 0] == 0 and f[32, 32, 2] == 0
+
+
+def test_misses_are_not_written(orc, cams):
+    """misses return before the store (K:302-303): the caller's zeroes stay"""
+    vol = np.full((8, 8, 8, 1), 1.0, np.float32)
+    out, f, n, _ = orc.render(vol, orc.make_params(512, 512, cams["C0"]))
+    miss = n < 0
+    assert np.all(out[miss] == 0) and np.all(f[miss] == 0)
+    assert abs(float(np.mean(~miss)) - 0.445) < 0.01
+
+
+def test_transfer_function(orc):
+    np.testing.assert_array_equal(orc.transfer(0.0), [0, 0, 0, 0])
+    np.testing.assert_array_equal(orc.transfer(1.0), [0, 0, 0, 0])
+    np.testing.assert_array_equal(orc.transfer(0.5), [0, 1, 0, 1])           # entry 4
+    np.testing.assert_array_equal(orc.transfer(2.5 / 9), [1, 0.5, 0, 1])    # entry 2
+    np.testing.assert_array_equal(orc.transfer(float("nan")), [0, 0, 0, 0])
+    np.testing.assert_array_equal(orc.transfer(-3.0), [0, 0, 0, 0])
+    # 8-bit fractional weight: xB = 1.3 -> alpha = round(0.3*256)/256 = 77/256
+    x = np.float32((np.float32(1.3) + np.float32(0.5)) / np.float32(9))
+    xb = np.float32(x * np.float32(9) - np.float32(0.5))
+    a = np.rint((xb - np.floor(xb)) * 256) / 256
+    got = orc.transfer(float(x))
+    np.testing.assert_allclose(got[1], 0.5 * a, rtol=0, atol=1e-7)          # G: 0 -> 0.5
+    assert a == 77 / 256
+    for x in np.linspace(-0.2, 1.2, 301, dtype=np.float32):
+        np.testing.assert_array_equal(orc.transfer(float(x)), rn.transfer(x))
+
+
+def test_pack_truncates(orc):
+    assert orc.pack([0.999, 0, 0, 0]) == 254
+    assert orc.pack([1.0, 0, 0, 0]) == 255
+    assert orc.pack([2.0, -1.0, float("nan"), 0.5]) == (127 << 24) | 255
+    assert orc.pack([0, 0, 1.0, 0]) == 255 << 16  # A<<24 | B<<16 | G<<8 | R (K:191-192)
+    assert orc.pack([0, 1.0, 0, 0]) == 255 << 8
+
+
+@pytest.mark.parametrize("nb", [1, 4, 8, 32])
+def test_record_stats(orc, nb):
+    bw = np.float32(0.0217) / np.float32(nb)
+    for i in range(nb):
+        rec = np.zeros(nb, np.float32)
+        rec[i] = 1.0
+        mean, var, ent = orc.record_stats(rec)
+        assert abs(mean - (i + 0.5) / nb) < 1e-6
+        # K:753: variance uses the bin *edge* i/B, the mean uses the centre: d = -bw/2
+        assert abs(var - (float(bw) / 2) ** 2 / 0.000021) < 1e-5
+        assert ent == 0.0 or (nb == 1 and np.isnan(ent))  # B=1: 0/log2(1)
+    if nb > 1:
+        mean, var, ent = orc.record_stats(np.full(nb, 1.0 / nb, np.float32))
+        assert abs(ent - 1.0) < 1e-6 and abs(mean - 0.5) < 1e-6
+    rng = np.random.default_rng(nb)
+    recs = rng.dirichlet(np.ones(nb), size=64).astype(np.float32)
+    for r in recs:
+        got = orc.record_stats(r)
+        for c in range(3):  # (B=1 entropy is 0/0 = NaN on both sides)
+            want = rn.stat(r[None], c)[0]
+            assert got[c] == want or (np.isnan(got[c]) and np.isnan(want))
+        assert orc.corner_mean(r) == rn.raw_mean(r[None])[0]
+
+
+@pytest.mark.parametrize("method", [1, 2, 3, 7])
+@pytest.mark.parametrize("cam", ["C0", "C1"])
+@pytest.mark.parametrize("nb", [1, 4, 8])
+def test_oracle_matches_numpy_restatement(orc, cams, method, cam, nb):
+    vol = orc.synth_volume(14, 12, 10, nb)
+    W, H = 48, 40
+    f, n = rn.render(vol, W, H, cams[cam], method, m7_dims=(14, 12, 10))
+    o8, of, on, _ = orc.render(vol, orc.make_params(W, H, cams[cam], query_method=method,
+                                                    m7_dims=(14, 12, 10)))
+    assert np.array_equal(n, on)
+    assert np.array_equal(f, of)
+    assert np.array_equal(np.where(n >= 0, rn.pack(f), 0), o8)
+
+
+def test_oracle_parameters_match_numpy(orc, cams):
+    vol = orc.synth_volume(10, 10, 10, 4)
+    for kw in [dict(density=0.3, brightness=1.7, toff=0.1, tscale=1.4),
+               dict(density=1.0, brightness=0.5, toff=-0.3, tscale=0.6)]:
+        for method in (1, 3, 7):
+            f, n = rn.render(vol, 32, 32, cams["C1"], method, **kw)
+            _, of, on, _ = orc.render(vol, orc.make_params(
+                32, 32, cams["C1"], kw["density"], kw["brightness"], kw["toff"], kw["tscale"],
+                method, m7_dims=(10, 10, 10)))
+            assert np.array_equal(n, on) and np.array_equal(f, of)
+
+
+def test_footprint_count_matches_numpy(orc, cams):
+    vol = orc.synth_volume(12, 10, 9, 4)
+    for cam in ("C0", "C1"):
+        fp = set()
+        rn.render(vol, 40, 32, cams[cam], 1, footprint=fp)
+        u = orc.count_footprint(vol, orc.make_params(40, 32, cams[cam], query_method=1))
+        assert u == len(fp)
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4, 8, 32])
+def test_synthetic_volume(orc, nb):
+    vol = orc.synth_volume(20, 18, 16, nb)
+    assert vol.shape == (16, 18, 20, nb)
+    assert np.all(vol >= 0) and np.all(vol <= 1)
+    if nb > 1:  # histograms sum to 1 (the loader check of C:940-942)
+        assert np.max(np.abs(vol.sum(-1, dtype=np.float64) - 1.0)) < 1e-6
+    assert np.array_equal(vol, orc.synth_volume(20, 18, 16, nb))
+    assert not np.array_equal(vol, orc.synth_volume(20, 18, 16, nb, seed=7))
+
+
+def test_rows_subset_equals_full(orc, cams):
+    """row-strided rendering (the CPU-baseline sample) renders the same pixels"""
+    vol = orc.synth_volume(16, 16, 16, 4)
+    p = orc.make_params(40, 30, cams["C1"])
+    full, _, _, _ = orc.render(vol, p)
+    part, _, _, _ = orc.render(vol, p, row_start=1, row_stride=3)
+    assert np.array_equal(part[1::3], full[1::3])
+    assert np.all(part[0::3] == 0) and np.all(part[2::3] == 0)
+
+
+def _golden_files():
+    return sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def test_golden_fixtures_present():
+    assert len(_golden_files()) >= 4
+
+
+@pytest.mark.parametrize("path", _golden_files(), ids=os.path.basename)
+def test_golden_fixture(orc, path):
+    """the oracle still produces the committed fixtures (tests/golden/make_golden.py)"""
+    z = np.load(path, allow_pickle=False)
+    nx, ny, nz, nb = (int(v) for v in z["dims"])
+    vol = orc.synth_volume(nx, ny, nz, nb, int(z["seed"]))
+    assert int(z["vol_crc"]) == int(np.bitwise_xor.reduce(vol.view(np.uint32).ravel()))
+    W, H = (int(v) for v in z["image"])
+    p = orc.make_params(W, H, z["inv_view"], float(z["density"]), float(z["brightness"]),
+                        float(z["toff"]), float(z["tscale"]), int(z["method"]),
+                        m7_dims=tuple(int(v) for v in z["m7_dims"]))
+    out, f, n, _ = orc.render(vol, p)
+    assert np.array_equal(out, z["rgba8"])
+    assert np.array_equal(n, z["steps"].astype(np.int32))
+    if "rgba_f" in z.files:
+        assert np.array_equal(f, z["rgba_f"])

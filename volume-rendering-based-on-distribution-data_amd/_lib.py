@@ -1,0 +1,147 @@
+"""ctypes binding of libvr.so (include/vr.h).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()``).
+There is no fallback: if the HIP library is missing or fails to load, every
+entry point raises, so nothing can silently run on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "build", "libvr.so")
+
+VR_OK = 0
+VR_ERR_ARG = -1
+VR_ERR_STATE = -2
+VR_ERR_HIP = -3
+VR_ERR_UNSUPPORTED = -4
+
+
+class VRError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"libvr status {status}: {message}")
+        self.status = status
+
+
+class Dim3(ctypes.Structure):
+    """Layout of dim3 (3 x uint32)."""
+    _fields_ = [("x", ctypes.c_uint32), ("y", ctypes.c_uint32), ("z", ctypes.c_uint32)]
+
+
+class Extent(ctypes.Structure):
+    """Layout of cudaExtent / hipExtent (3 x size_t)."""
+    _fields_ = [("width", ctypes.c_size_t), ("height", ctypes.c_size_t),
+                ("depth", ctypes.c_size_t)]
+
+
+class RenderDesc(ctypes.Structure):
+    """vr_render_desc of include/vr.h."""
+    _fields_ = [
+        ("d_output", ctypes.c_void_p),
+        ("d_output_f", ctypes.c_void_p),
+        ("d_steps", ctypes.c_void_p),
+        ("width", ctypes.c_uint32),
+        ("height", ctypes.c_uint32),
+        ("inv_view", ctypes.c_float * 12),
+        ("density", ctypes.c_float),
+        ("brightness", ctypes.c_float),
+        ("transfer_offset", ctypes.c_float),
+        ("transfer_scale", ctypes.c_float),
+        ("query_method", ctypes.c_int),
+        ("volume_size", Extent),
+        ("d_tile_list", ctypes.c_void_p),
+        ("n_tiles", ctypes.c_uint32),
+    ]
+
+
+# every symbol include/vr.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers",
+    "setTextureFilterMode", "basicDataProcessing", "dataProcessing",
+    "vr_last_error", "vr_last_status", "vr_clear_error", "vr_init_distribution",
+    "vr_synthesize", "vr_volume_info", "vr_set_stream", "vr_render", "vr_count_footprint",
+    "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version",
+]
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libvr.so (raises OSError / FileNotFoundError when absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(
+            f"{LIB_PATH} is missing: build the HIP library first (__graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, f32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float, ctypes.c_int
+    L.render_kernel.argtypes = [Dim3, Dim3, vp, u32, u32, f32, f32, f32, f32, i32, Extent]
+    L.render_kernel.restype = None
+    L.copyInvViewMatrix.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_size_t]
+    L.copyInvViewMatrix.restype = None
+    L.initCuda.argtypes = [vp, Extent, Extent, vp, Extent, vp, Extent, vp, Extent,
+                           vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.initCuda.restype = None
+    L.freeCudaBuffers.argtypes = []
+    L.freeCudaBuffers.restype = None
+    L.setTextureFilterMode.argtypes = [ctypes.c_bool]
+    L.setTextureFilterMode.restype = None
+    L.basicDataProcessing.argtypes = []
+    L.basicDataProcessing.restype = None
+    L.dataProcessing.argtypes = []
+    L.dataProcessing.restype = None
+    L.vr_last_error.argtypes = []
+    L.vr_last_error.restype = ctypes.c_char_p
+    L.vr_last_status.argtypes = []
+    L.vr_last_status.restype = i32
+    L.vr_clear_error.argtypes = []
+    L.vr_clear_error.restype = None
+    L.vr_init_distribution.argtypes = [vp, Extent, i32, i32]
+    L.vr_init_distribution.restype = i32
+    L.vr_synthesize.argtypes = [Extent, i32, ctypes.c_uint64]
+    L.vr_synthesize.restype = i32
+    L.vr_volume_info.argtypes = [ctypes.POINTER(Extent), ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(ctypes.c_void_p)]
+    L.vr_volume_info.restype = i32
+    L.vr_set_stream.argtypes = [vp]
+    L.vr_set_stream.restype = i32
+    L.vr_render.argtypes = [ctypes.POINTER(RenderDesc)]
+    L.vr_render.restype = i32
+    L.vr_count_footprint.argtypes = [ctypes.POINTER(RenderDesc)]
+    L.vr_count_footprint.restype = ctypes.c_int64
+    L.vr_unscatter_tiles.argtypes = [vp, vp, u32, u32, vp, u32, u32]
+    L.vr_unscatter_tiles.restype = i32
+    L.vr_tiles_x.argtypes = [u32]
+    L.vr_tiles_x.restype = u32
+    L.vr_tiles_y.argtypes = [u32]
+    L.vr_tiles_y.restype = u32
+    L.vr_version.argtypes = []
+    L.vr_version.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return load().vr_last_error().decode()
+
+
+def check(status: int) -> int:
+    """Raise VRError for a negative status (message from vr_last_error)."""
+    if status < 0:
+        msg = last_error()
+        load().vr_clear_error()
+        raise VRError(int(status), msg)
+    return status
+
+
+def check_last() -> None:
+    """Raise if a void reference entry point recorded an error."""
+    L = load()
+    st = L.vr_last_status()
+    if st != VR_OK:
+        msg = last_error()
+        L.vr_clear_error()
+        raise VRError(st, msg)

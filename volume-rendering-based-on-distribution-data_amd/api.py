@@ -1,0 +1,200 @@
+"""Python mirror of the reference's host/launch API (volumeRender.cpp:156-170).
+
+The functions keep the reference's names, argument order and meaning and call
+straight into libvr.so.  Device buffers are passed as torch CUDA tensors or as
+raw device addresses (int).  Where the reference's checkCudaErrors /
+getLastCudaError would have printed and exited (C:201-216, 1070), these
+functions raise VRError.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import Dim3, Extent, RenderDesc, VRError, check, check_last
+
+PAD = 0xFFFFFFFF
+
+
+def _ptr(buf) -> int:
+    if buf is None:
+        return 0
+    if isinstance(buf, int):
+        return buf
+    if hasattr(buf, "data_ptr"):
+        if not buf.is_cuda:
+            raise ValueError("device buffer expected (a CUDA/HIP tensor)")
+        if not buf.is_contiguous():
+            raise ValueError("device buffer must be contiguous")
+        return int(buf.data_ptr())
+    raise TypeError(f"cannot take a device pointer of {type(buf)!r}")
+
+
+def _extent(e) -> Extent:
+    if isinstance(e, Extent):
+        return e
+    w, h, d = (int(v) for v in e)
+    return Extent(w, h, d)
+
+
+def _dim3(d) -> Dim3:
+    if isinstance(d, Dim3):
+        return d
+    d = tuple(int(v) for v in d) + (1, 1, 1)
+    return Dim3(d[0], d[1], d[2])
+
+
+# ---------------------------------------------------------------- reference API
+
+def render_kernel(gridSize, blockSize, d_output, imageW: int, imageH: int, density: float,
+                  brightness: float, transferOffset: float, transferScale: float,
+                  queryMethod: int, volumeSize) -> None:
+    """render_kernel, K:2387-2401 (asynchronous; raises on a recorded error)."""
+    _lib.load().render_kernel(_dim3(gridSize), _dim3(blockSize), _ptr(d_output), int(imageW),
+                              int(imageH), float(density), float(brightness),
+                              float(transferOffset), float(transferScale), int(queryMethod),
+                              _extent(volumeSize))
+    check_last()
+
+
+def copyInvViewMatrix(invViewMatrix, sizeofMatrix: int = 48) -> None:
+    """copyInvViewMatrix, K:2403-2406."""
+    m = np.ascontiguousarray(np.asarray(invViewMatrix, dtype=np.float32).reshape(-1))
+    if m.nbytes < sizeofMatrix:
+        raise ValueError("matrix smaller than sizeofMatrix")
+    _lib.load().copyInvViewMatrix(m.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                  int(sizeofMatrix))
+    check_last()
+
+
+def initCuda(h_histogram, volumeSize, histogramSize, *codec_and_flexible_arrays) -> None:
+    """initCuda, K:1893-2358.  h_histogram: host fp32 array of B-bin records in
+    AoS order (record = x + X*(y + Y*z)); the remaining 15 reference arguments
+    (codebook/templates/flexible-block arrays) are accepted and ignored."""
+    h = np.ascontiguousarray(np.asarray(h_histogram, dtype=np.float32))
+    L = _lib.load()
+    z = Extent(0, 0, 0)
+    L.initCuda(h.ctypes.data, _extent(volumeSize), _extent(histogramSize), None, z, None, z,
+               None, z, None, None, None, None, None, None, None, None, None)
+    check_last()
+
+
+def freeCudaBuffers() -> None:
+    """freeCudaBuffers, K:2360-2385."""
+    _lib.load().freeCudaBuffers()
+    check_last()
+
+
+def setTextureFilterMode(bLinearFilter: bool) -> None:
+    """setTextureFilterMode, K:1889-1891 (no effect on methods 1/2/3/7)."""
+    _lib.load().setTextureFilterMode(bool(bLinearFilter))
+
+
+def basicDataProcessing() -> None:
+    """basicDataProcessing, K:1798-1887: nothing to pre-bake (decoded per step)."""
+    _lib.load().basicDataProcessing()
+    check_last()
+
+
+def dataProcessing() -> None:
+    """dataProcessing, K:1735-1796: flexible-block pre-pass, out of scope (raises)."""
+    _lib.load().dataProcessing()
+    check_last()
+
+
+# ---------------------------------------------------------------- extensions
+
+def init_distribution(bins, nbins: Optional[int] = None, dims=None, adopt: bool = False):
+    """Make a distribution volume resident.
+
+    bins: numpy array (nz, ny, nx, B) -> copied from host; or a torch CUDA tensor
+    of the same shape -> copied device-to-device (adopt=False) or used in place
+    (adopt=True, the caller keeps it alive)."""
+    L = _lib.load()
+    if hasattr(bins, "data_ptr") and getattr(bins, "is_cuda", False):
+        shp = tuple(bins.shape)
+        if dims is None:
+            nz, ny, nx, nb = shp
+            dims = (nx, ny, nz)
+        nb = nbins if nbins is not None else shp[-1]
+        check(L.vr_init_distribution(_ptr(bins), _extent(dims), int(nb), 2 if adopt else 1))
+        return
+    a = np.ascontiguousarray(np.asarray(bins, dtype=np.float32))
+    if dims is None:
+        nz, ny, nx, nb = a.shape
+        dims = (nx, ny, nz)
+    nb = nbins if nbins is not None else a.shape[-1]
+    check(L.vr_init_distribution(a.ctypes.data, _extent(dims), int(nb), 0))
+
+
+def synthesize(dims, nbins: int, seed: int = 20261015) -> None:
+    """Generate the seeded synthetic distribution volume directly in HBM."""
+    check(_lib.load().vr_synthesize(_extent(dims), int(nbins), int(seed)))
+
+
+def volume_info():
+    e = Extent()
+    nb = ctypes.c_int()
+    p = ctypes.c_void_p()
+    check(_lib.load().vr_volume_info(ctypes.byref(e), ctypes.byref(nb), ctypes.byref(p)))
+    return (e.width, e.height, e.depth), nb.value, p.value
+
+
+def set_stream(stream) -> None:
+    """Stream for subsequent launches: a torch.cuda.Stream, a raw hipStream_t, or None."""
+    raw = 0 if stream is None else (stream.cuda_stream if hasattr(stream, "cuda_stream")
+                                    else int(stream))
+    check(_lib.load().vr_set_stream(raw))
+
+
+def make_desc(d_output, width: int, height: int, inv_view, density=0.05, brightness=1.0,
+              transfer_offset=0.0, transfer_scale=1.0, query_method=1, volume_size=None,
+              d_output_f=None, d_steps=None, d_tile_list=None, n_tiles=0) -> RenderDesc:
+    d = RenderDesc()
+    d.d_output = _ptr(d_output)
+    d.d_output_f = _ptr(d_output_f)
+    d.d_steps = _ptr(d_steps)
+    d.width, d.height = int(width), int(height)
+    m = np.asarray(inv_view, dtype=np.float32).reshape(12)
+    for i in range(12):
+        d.inv_view[i] = float(m[i])
+    d.density, d.brightness = float(density), float(brightness)
+    d.transfer_offset, d.transfer_scale = float(transfer_offset), float(transfer_scale)
+    d.query_method = int(query_method)
+    if volume_size is None:
+        volume_size = volume_info()[0]
+    d.volume_size = _extent(volume_size)
+    d.d_tile_list = _ptr(d_tile_list)
+    d.n_tiles = int(n_tiles)
+    return d
+
+
+def render(desc: RenderDesc) -> None:
+    """Launch the march for an explicit descriptor (asynchronous)."""
+    check(_lib.load().vr_render(ctypes.byref(desc)))
+
+
+def count_footprint(desc: RenderDesc) -> int:
+    """U: distinct records under all trilinear footprints (synchronous)."""
+    return int(check(_lib.load().vr_count_footprint(ctypes.byref(desc))))
+
+
+def unscatter_tiles(d_packed, d_tile_lists, n_ranks: int, n_slots: int, d_frame, width: int,
+                    height: int) -> None:
+    check(_lib.load().vr_unscatter_tiles(_ptr(d_packed), _ptr(d_tile_lists), int(n_ranks),
+                                         int(n_slots), _ptr(d_frame), int(width), int(height)))
+
+
+def version() -> str:
+    return _lib.load().vr_version().decode()
+
+
+__all__ = [
+    "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers", "setTextureFilterMode",
+    "basicDataProcessing", "dataProcessing", "init_distribution", "synthesize", "volume_info",
+    "set_stream", "make_desc", "render", "count_footprint", "unscatter_tiles", "version",
+    "VRError", "PAD",
+]

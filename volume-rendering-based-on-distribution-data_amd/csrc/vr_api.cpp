@@ -1,0 +1,400 @@
+// vr_api.cpp -- host side of libvr.so: module-global device state and the
+// C-ABI of include/vr.h (the reference's extern "C" API, K:1889-2406, plus
+// the vr_* extensions).  Never exits; errors go to vr_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vr.h"
+#include "vr_internal.h"
+
+namespace {
+
+struct State {
+    float *vol = nullptr;
+    bool owned = false;
+    int nx = 0, ny = 0, nz = 0, nb = 0;
+    float inv_view[12] = {0};       // __constant__ c_invViewMatrix starts zeroed (K:116)
+    hipStream_t stream = nullptr;   // legacy default stream, like the reference
+    bool linear_filter = false;     // tex.filterMode = point after initCuda (K:2163)
+    std::string err;
+    int status = VR_OK;
+};
+
+State g;
+
+int fail(int status, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g.err = buf;
+    g.status = status;
+    return status;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(VR_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define VR_HIP(call)                                        \
+    do {                                                    \
+        hipError_t e_ = (call);                             \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);   \
+    } while (0)
+
+void release_volume() {
+    if (g.vol && g.owned) (void)hipFree(g.vol);
+    g.vol = nullptr;
+    g.owned = false;
+    g.nx = g.ny = g.nz = g.nb = 0;
+}
+
+float entropy_norm(int nb) {
+    // K:769: log((float)nBins) / log(2.0f) with the float overloads of log
+    const float a = (float)std::log((double)(float)nb);
+    const float b = (float)std::log((double)2.0f);
+    return a / b;
+}
+
+uint32_t tiles_x(uint32_t w) { return (w + vr::kTile - 1) / vr::kTile; }
+uint32_t tiles_y(uint32_t h) { return (h + vr::kTile - 1) / vr::kTile; }
+
+int check_method(int m) {
+    if (m == 1 || m == 2 || m == 3 || m == 7) return VR_OK;
+    if (m == 4 || m == 5 || m == 6)
+        return fail(VR_ERR_UNSUPPORTED,
+                    "queryMethod %d needs the fractal/template codec (out of scope)", m);
+    if (m == 8 || m == 9 || m == 0)
+        return fail(VR_ERR_UNSUPPORTED,
+                    "queryMethod %d needs the flexible-block pre-pass (out of scope)", m);
+    return fail(VR_ERR_ARG, "unknown queryMethod %d", m);
+}
+
+int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
+    if (!d) return fail(VR_ERR_ARG, "null render descriptor");
+    if (!g.vol) return fail(VR_ERR_STATE, "no volume resident (initCuda / vr_init_* first)");
+    if (!d->d_output) return fail(VR_ERR_ARG, "d_output is null");
+    if (d->width == 0 || d->height == 0) return fail(VR_ERR_ARG, "empty image");
+    int rc = check_method(d->query_method);
+    if (rc != VR_OK) return rc;
+    if (d->query_method == 7 &&
+        (d->volume_size.width == 0 || d->volume_size.height == 0 || d->volume_size.depth == 0))
+        return fail(VR_ERR_ARG, "method 7 needs a non-empty volumeSize");
+    std::memset(&P, 0, sizeof P);
+    std::memcpy(P.m, d->inv_view, sizeof P.m);
+    P.W = d->width;
+    P.H = d->height;
+    P.density = d->density;
+    P.brightness = d->brightness;
+    P.toff = d->transfer_offset;
+    P.tscale = d->transfer_scale;
+    P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
+    P.m7x = (int)d->volume_size.width;
+    P.m7y = (int)d->volume_size.height;
+    P.m7z = (int)d->volume_size.depth;
+    P.enorm = entropy_norm(g.nb);
+    P.nb = g.nb;
+    P.tiles_x = tiles_x(d->width);
+    P.tile_list = d->d_tile_list;
+    P.out = d->d_output;
+    P.out_f = d->d_output_f;
+    P.out_n = d->d_steps;
+    P.mark = nullptr;
+    const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
+    if (d->d_tile_list) {
+        nslots = d->n_tiles;
+    } else {
+        if (all > 0xFFFFFFFFull) return fail(VR_ERR_ARG, "image too large");
+        nslots = (uint32_t)all;
+    }
+    P.n_tiles = nslots;
+    return VR_OK;
+}
+
+// ---- synthetic volume tables ----
+uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+double u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+
+void blob_axis(int n, double c, double s, float *out) {
+    for (int i = 0; i < n; i++) {
+        const double q = ((double)i + 0.5) / (double)n;
+        out[i] = (float)std::exp(-(q - c) * (q - c) / (2.0 * s * s));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *vr_version(void) { return "vrdd-amd 0.1 (gfx950)"; }
+const char *vr_last_error(void) { return g.err.c_str(); }
+int vr_last_status(void) { return g.status; }
+void vr_clear_error(void) {
+    g.err.clear();
+    g.status = VR_OK;
+}
+
+uint32_t vr_tiles_x(uint32_t width) { return tiles_x(width); }
+uint32_t vr_tiles_y(uint32_t height) { return tiles_y(height); }
+
+int vr_set_stream(void *stream) {
+    g.stream = (hipStream_t)stream;
+    return VR_OK;
+}
+
+int vr_init_distribution(const float *bins, vr_extent dims, int nbins, int where) {
+    if (!bins) return fail(VR_ERR_ARG, "null distribution pointer");
+    if (nbins < 1) return fail(VR_ERR_ARG, "nbins must be >= 1 (got %d)", nbins);
+    if (dims.width == 0 || dims.height == 0 || dims.depth == 0)
+        return fail(VR_ERR_ARG, "empty volume");
+    if (dims.width > 65536 || dims.height > 65536 || dims.depth > 65536)
+        return fail(VR_ERR_ARG, "volume dimension > 65536");
+    const size_t nvox = dims.width * dims.height * dims.depth;
+    const size_t bytes = nvox * (size_t)nbins * sizeof(float);
+    release_volume();
+    if (where == 2) {
+        g.vol = const_cast<float *>(bins);
+        g.owned = false;
+    } else {
+        float *d = nullptr;
+        VR_HIP(hipMalloc(&d, bytes));
+        hipError_t e = hipMemcpy(d, bins, bytes,
+                                 where == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return hip_fail(e, "hipMemcpy(volume)");
+        }
+        g.vol = d;
+        g.owned = true;
+    }
+    g.nx = (int)dims.width;
+    g.ny = (int)dims.height;
+    g.nz = (int)dims.depth;
+    g.nb = nbins;
+    return VR_OK;
+}
+
+int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
+    if (nbins < 1) return fail(VR_ERR_ARG, "nbins must be >= 1 (got %d)", nbins);
+    if (dims.width == 0 || dims.height == 0 || dims.depth == 0)
+        return fail(VR_ERR_ARG, "empty volume");
+    if (dims.width > 65536 || dims.height > 65536 || dims.depth > 65536)
+        return fail(VR_ERR_ARG, "volume dimension > 65536");
+    const int nx = (int)dims.width, ny = (int)dims.height, nz = (int)dims.depth;
+    const size_t nvox = dims.width * dims.height * dims.depth;
+    vr::SynthArgs a{};
+    std::vector<float> gx((size_t)vr::kSynthBlobs * nx), gy((size_t)vr::kSynthBlobs * ny),
+        gz((size_t)vr::kSynthBlobs * nz);
+    for (int k = 0; k < vr::kSynthBlobs; k++) {
+        double r[5];
+        for (int j = 0; j < 5; j++)
+            r[j] = u01(splitmix64(seed + 0x100u + 8u * (uint64_t)k + (uint64_t)j));
+        a.amp[k] = (float)(0.3 + 0.7 * r[0]);
+        const double s = 0.05 + 0.15 * r[4];
+        blob_axis(nx, 0.2 + 0.6 * r[1], s, gx.data() + (size_t)k * nx);
+        blob_axis(ny, 0.2 + 0.6 * r[2], s, gy.data() + (size_t)k * ny);
+        blob_axis(nz, 0.2 + 0.6 * r[3], s, gz.data() + (size_t)k * nz);
+    }
+    std::vector<float> tab;
+    if (nbins > 1) {
+        tab.resize((size_t)vr::kSynthG * vr::kSynthQ * nbins);
+        std::vector<double> e(nbins);
+        for (int gi = 0; gi < vr::kSynthG; gi++) {
+            const double sig = 0.02 + 0.1 * (double)gi / 15.0;
+            for (int q = 0; q < vr::kSynthQ; q++) {
+                const double mu = ((double)q + 0.5) / (double)vr::kSynthQ;
+                double sum = 0.0;
+                for (int b = 0; b < nbins; b++) {
+                    const double dd = ((double)b + 0.5) / (double)nbins - mu;
+                    e[b] = std::exp(-dd * dd / (2.0 * sig * sig));
+                    sum += e[b];
+                }
+                float *row = tab.data() + ((size_t)gi * vr::kSynthQ + q) * nbins;
+                for (int b = 0; b < nbins; b++) row[b] = (float)(e[b] / sum);
+            }
+        }
+    }
+    release_volume();
+    float *vol = nullptr, *dgx = nullptr, *dgy = nullptr, *dgz = nullptr, *dtab = nullptr;
+    auto cleanup = [&]() {
+        if (dgx) (void)hipFree(dgx);
+        if (dgy) (void)hipFree(dgy);
+        if (dgz) (void)hipFree(dgz);
+        if (dtab) (void)hipFree(dtab);
+    };
+    hipError_t e = hipMalloc(&vol, nvox * (size_t)nbins * sizeof(float));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(volume)");
+    e = hipMalloc(&dgx, gx.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgy, gy.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgz, gz.size() * 4);
+    if (e == hipSuccess && !tab.empty()) e = hipMalloc(&dtab, tab.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(dgx, gx.data(), gx.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgy, gy.data(), gy.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgz, gz.data(), gz.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && dtab)
+        e = hipMemcpy(dtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        a.gx = dgx; a.gy = dgy; a.gz = dgz; a.table = dtab;
+        a.nx = nx; a.ny = ny; a.nz = nz; a.nb = nbins; a.seed = seed;
+        e = vr::launch_synth(vol, a, g.stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    cleanup();
+    if (e != hipSuccess) {
+        (void)hipFree(vol);
+        return hip_fail(e, "vr_synthesize");
+    }
+    g.vol = vol;
+    g.owned = true;
+    g.nx = nx; g.ny = ny; g.nz = nz; g.nb = nbins;
+    return VR_OK;
+}
+
+int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins) {
+    if (!g.vol) return fail(VR_ERR_STATE, "no volume resident");
+    if (dims) {
+        dims->width = (size_t)g.nx;
+        dims->height = (size_t)g.ny;
+        dims->depth = (size_t)g.nz;
+    }
+    if (nbins) *nbins = g.nb;
+    if (d_bins) *d_bins = g.vol;
+    return VR_OK;
+}
+
+int vr_render(const vr_render_desc *desc) {
+    vr::Params P;
+    uint32_t nslots = 0;
+    int rc = fill_params(desc, P, nslots);
+    if (rc != VR_OK) return rc;
+    hipError_t e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
+    if (e != hipSuccess) return hip_fail(e, "launch(k_march)");
+    return VR_OK;
+}
+
+int64_t vr_count_footprint(const vr_render_desc *desc) {
+    vr::Params P;
+    uint32_t nslots = 0;
+    int rc = fill_params(desc, P, nslots);
+    if (rc != VR_OK) return rc;
+    if (desc->query_method == 7)
+        return fail(VR_ERR_UNSUPPORTED, "footprint count is defined for methods 1/2/3");
+    const uint64_t nvox = (uint64_t)g.nx * g.ny * g.nz;
+    const uint64_t nwords = (nvox + 63) / 64;
+    unsigned long long *bits = nullptr, *total = nullptr;
+    VR_HIP(hipMalloc(&bits, nwords * 8 + 8));
+    total = bits + nwords;
+    hipError_t e = hipMemsetAsync(bits, 0, nwords * 8 + 8, g.stream);
+    P.mark = bits;
+    if (e == hipSuccess)
+        e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, true, g.stream);
+    if (e == hipSuccess) e = vr::launch_popcount(bits, nwords, total, g.stream);
+    unsigned long long u = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&u, total, 8, hipMemcpyDeviceToHost, g.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    (void)hipFree(bits);
+    if (e != hipSuccess) return hip_fail(e, "vr_count_footprint");
+    return (int64_t)u;
+}
+
+int vr_unscatter_tiles(const uint32_t *d_packed, const uint32_t *d_tile_lists, uint32_t n_ranks,
+                       uint32_t n_slots, uint32_t *d_frame, uint32_t width, uint32_t height) {
+    if (!d_packed || !d_tile_lists || !d_frame) return fail(VR_ERR_ARG, "null pointer");
+    const uint64_t n = (uint64_t)n_ranks * n_slots;
+    if (n > 0x7FFFFFFFull) return fail(VR_ERR_ARG, "too many tiles");
+    hipError_t e = vr::launch_unscatter(d_packed, d_tile_lists, (uint32_t)n, tiles_x(width),
+                                        d_frame, width, height, g.stream);
+    if (e != hipSuccess) return hip_fail(e, "launch(k_unscatter)");
+    return VR_OK;
+}
+
+// ---------------- reference entry points (K:1889-2406) ------------------
+
+void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output, uint32_t imageW,
+                   uint32_t imageH, float density, float brightness, float transferOffset,
+                   float transferScale, int queryMethod, vr_extent volumeSize) {
+    (void)gridSize;
+    (void)blockSize;
+    vr_render_desc d;
+    std::memset(&d, 0, sizeof d);
+    d.d_output = d_output;
+    d.width = imageW;
+    d.height = imageH;
+    std::memcpy(d.inv_view, g.inv_view, sizeof d.inv_view);
+    d.density = density;
+    d.brightness = brightness;
+    d.transfer_offset = transferOffset;
+    d.transfer_scale = transferScale;
+    d.query_method = queryMethod;
+    d.volume_size = volumeSize;
+    (void)vr_render(&d);
+}
+
+void copyInvViewMatrix(float *invViewMatrix, size_t sizeofMatrix) {
+    if (!invViewMatrix) {
+        fail(VR_ERR_ARG, "copyInvViewMatrix: null matrix");
+        return;
+    }
+    if (sizeofMatrix > sizeof g.inv_view) {
+        fail(VR_ERR_ARG, "copyInvViewMatrix: %zu bytes > 48", sizeofMatrix);
+        return;
+    }
+    std::memcpy(g.inv_view, invViewMatrix, sizeofMatrix);
+}
+
+void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
+              vr_int4 *h_codebook, vr_extent codebookSize, float *h_templates,
+              vr_extent templatesSize, vr_float2 *h_errorsbook, vr_extent errorsbookSize,
+              vr_int4 *h_codebookSpanLow, vr_int4 *h_codebookSpanHigh,
+              vr_int4 *h_flexibleCodebook, vr_float2 *h_flexibleErrorsbook,
+              vr_int4 *h_simpleLow, vr_int4 *h_simpleHigh, int *h_simpleCount,
+              vr_float2 *h_simpleHistogram, float *h_flexibleTemplates) {
+    // arrays 4-18 feed the codec / flexible-block methods only (out of scope)
+    (void)h_codebook; (void)codebookSize; (void)h_templates; (void)templatesSize;
+    (void)h_errorsbook; (void)errorsbookSize; (void)h_codebookSpanLow;
+    (void)h_codebookSpanHigh; (void)h_flexibleCodebook; (void)h_flexibleErrorsbook;
+    (void)h_simpleLow; (void)h_simpleHigh; (void)h_simpleCount; (void)h_simpleHistogram;
+    (void)h_flexibleTemplates;
+    const size_t nvox = volumeSize.width * volumeSize.height * volumeSize.depth;
+    if (histogramSize.width == 0 || histogramSize.height * histogramSize.depth != nvox) {
+        fail(VR_ERR_ARG,
+             "initCuda: histogramSize (%zu,%zu,%zu) does not hold one record per voxel of "
+             "(%zu,%zu,%zu)",
+             histogramSize.width, histogramSize.height, histogramSize.depth, volumeSize.width,
+             volumeSize.height, volumeSize.depth);
+        return;
+    }
+    if (vr_init_distribution((const float *)h_histogram, volumeSize, (int)histogramSize.width,
+                             0) == VR_OK)
+        g.linear_filter = false;
+}
+
+void freeCudaBuffers(void) {
+    release_volume();
+}
+
+void setTextureFilterMode(bool bLinearFilter) { g.linear_filter = bLinearFilter; }
+
+void basicDataProcessing(void) {
+    if (!g.vol) fail(VR_ERR_STATE, "basicDataProcessing: no volume resident");
+}
+
+void dataProcessing(void) {
+    fail(VR_ERR_UNSUPPORTED,
+         "dataProcessing: flexible-block pre-pass (methods 8/9/0) is out of scope");
+}
+
+}  // extern "C"

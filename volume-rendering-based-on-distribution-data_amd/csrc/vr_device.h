@@ -1,0 +1,217 @@
+// vr_device.h -- device-side arithmetic of the d_render path for gfx950.
+//
+// Every function evaluates the reference expression it cites with the
+// canonical arithmetic of DESIGN.md section 3: ISO C promotions as written in
+// the reference source, no FMA contraction (the library is compiled with
+// -ffp-contract=off), correctly rounded division/sqrt, CUDA texture-fetch
+// rules with 8-bit fractional filter weights.  K = volumeRender_kernel.cu.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vr {
+
+constexpr int kMaxSteps = 500;             // K:276
+constexpr float kTStep = 0.01f;            // K:277
+constexpr float kOpacityThreshold = 0.95f; // K:278
+constexpr int kTile = 16;                  // pixels per tile edge
+constexpr uint32_t kPad = 0xFFFFFFFFu;     // tile-list padding
+
+struct Params {
+    float m[12];                 // c_invViewMatrix (K:116), row-major 3x4
+    uint32_t W, H;
+    float density, brightness, toff, tscale;
+    int nx, ny, nz;              // resident volume dims
+    int m7x, m7y, m7z;           // render_kernel volumeSize (method 7)
+    float enorm;                 // log((float)B)/log(2.0f), K:769
+    int nb;                      // bins per record
+    uint32_t tiles_x;            // ceil(W/16)
+    uint32_t n_tiles;            // tiles in this launch
+    const uint32_t *tile_list;   // nullptr: tile = launch slot
+    uint32_t *out;
+    float *out_f;
+    int32_t *out_n;
+    unsigned long long *mark;    // footprint bitset (count mode only)
+};
+
+// log(2.0), correctly rounded (K:766)
+#define VR_LN2_D 0x1.62e42fefa39efp-1
+
+__device__ __forceinline__ float clamp01(float u) { return fminf(fmaxf(u, 0.0f), 1.0f); }
+
+// 9-bit fixed-point filter weight, 8 fractional bits
+__device__ __forceinline__ float q8(float a) { return rintf(a * 256.0f) * (1.0f / 256.0f); }
+
+__device__ __forceinline__ float lerpq(float a, float b, float t) {
+    return (1.0f - t) * a + t * b;
+}
+
+// linear filter, normalised coordinate, clamp addressing (K:1865-1869)
+__device__ __forceinline__ void lin_axis(float u, int n, int &i0, int &i1, float &a) {
+    u = clamp01(u);
+    float xb = u * (float)n - 0.5f;
+    float fl = floorf(xb);
+    float fr = xb - fl;
+    int i = (int)fl;
+    a = q8(fr);
+    i0 = max(0, min(n - 1, i));
+    i1 = max(0, min(n - 1, i + 1));
+}
+
+// point filter, normalised coordinate, clamp (index volume tex, K:2161-2165)
+__device__ __forceinline__ int point_axis(float u, int n) {
+    u = clamp01(u);
+    int i = (int)floorf(u * (float)n);
+    return min(i, n - 1);
+}
+
+// transfer function (K:2323-2326), linear / normalised / clamp (K:2337-2339)
+__device__ __forceinline__ float4 tf_entry(int i) {
+    // branch-free table: r,g,b,a of the 9 entries
+    const float r = (i == 1 || i == 2 || i == 3 || i == 7) ? 1.0f : 0.0f;
+    const float g = (i == 3 || i == 4 || i == 5) ? 1.0f : (i == 2 ? 0.5f : 0.0f);
+    const float b = (i == 5 || i == 6 || i == 7) ? 1.0f : 0.0f;
+    const float a = (i >= 1 && i <= 7) ? 1.0f : 0.0f;
+    return make_float4(r, g, b, a);
+}
+
+__device__ __forceinline__ float4 transfer(float x) {
+    int i0, i1;
+    float a;
+    lin_axis(x, 9, i0, i1, a);
+    const float4 t0 = tf_entry(i0), t1 = tf_entry(i1);
+    return make_float4(lerpq(t0.x, t1.x, a), lerpq(t0.y, t1.y, a), lerpq(t0.z, t1.z, a),
+                       lerpq(t0.w, t1.w, a));
+}
+
+__device__ __forceinline__ float sat(float x) {  // __saturatef, NaN -> 0
+    return (x > 0.0f) ? (x > 1.0f ? 1.0f : x) : 0.0f;
+}
+
+// rgbaFloatToInt, K:186-193
+__device__ __forceinline__ uint32_t pack_rgba(float r, float g, float b, float a) {
+    r = sat(r); g = sat(g); b = sat(b); a = sat(a);
+    return ((uint32_t)(a * 255.0f) << 24) | ((uint32_t)(b * 255.0f) << 16) |
+           ((uint32_t)(g * 255.0f) << 8) | (uint32_t)(r * 255.0f);
+}
+
+// binWidth, K:736-738
+__device__ __forceinline__ float bin_width(int nb) {
+    const float maxh = (float)0.0217;
+    return (maxh - 0.0f) / (float)nb;
+}
+
+// K:742-747: mean += p * (binWidth * i + binWidth / 2.0), float accumulator
+template <int B>
+__device__ __forceinline__ float raw_mean(const float (&p)[B]) {
+    const float bw = bin_width(B);
+    const double half = (double)bw / 2.0;
+    float mean = 0.0f;
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+        const double c = (double)(bw * (float)i) + half;
+        mean = (float)((double)mean + (double)p[i] * c);
+    }
+    return mean;
+}
+
+// K:749-755 (float arithmetic)
+template <int B>
+__device__ __forceinline__ float raw_variance(const float (&p)[B], float mean) {
+    const float maxh = (float)0.0217;
+    float var = 0.0f;
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+        const float d = ((float)i / (float)B) * maxh - mean;
+        var = var + p[i] * d * d;
+    }
+    return var;
+}
+
+// K:761-769
+template <int B>
+__device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
+    float ent = 0.0f;
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+        const float pr = p[i];
+        const double t = pr <= 0 ? 0.0 : ((double)(float)log((double)pr) / VR_LN2_D);
+        ent = (float)((double)ent + (double)pr * t);
+    }
+    ent = -ent;
+    return ent / enorm;
+}
+
+// the statistic a method samples, K:758-769 (M: 1 mean, 2 variance, 3 entropy)
+template <int B, int M>
+__device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
+    if constexpr (M == 1) {
+        return (float)((double)raw_mean<B>(p) / 0.0217);
+    } else if constexpr (M == 2) {
+        const float mean = raw_mean<B>(p);
+        return (float)((double)raw_variance<B>(p, mean) / 0.000021);
+    } else {
+        return entropy<B>(p, enorm);
+    }
+}
+
+// ---- runtime-B variants (bin counts without a compiled specialisation) ----
+__device__ __forceinline__ float raw_mean_rt(const float *__restrict__ p, int nb) {
+    const float bw = bin_width(nb);
+    const double half = (double)bw / 2.0;
+    float mean = 0.0f;
+    for (int i = 0; i < nb; i++) {
+        const double c = (double)(bw * (float)i) + half;
+        mean = (float)((double)mean + (double)p[i] * c);
+    }
+    return mean;
+}
+
+template <int M>
+__device__ __forceinline__ float record_stat_rt(const float *__restrict__ p, int nb,
+                                                float enorm) {
+    if constexpr (M == 1) {
+        return (float)((double)raw_mean_rt(p, nb) / 0.0217);
+    } else if constexpr (M == 2) {
+        const float mean = raw_mean_rt(p, nb);
+        const float maxh = (float)0.0217;
+        float var = 0.0f;
+        for (int i = 0; i < nb; i++) {
+            const float d = ((float)i / (float)nb) * maxh - mean;
+            var = var + p[i] * d * d;
+        }
+        return (float)((double)var / 0.000021);
+    } else {
+        float ent = 0.0f;
+        for (int i = 0; i < nb; i++) {
+            const float pr = p[i];
+            const double t = pr <= 0 ? 0.0 : ((double)(float)log((double)pr) / VR_LN2_D);
+            ent = (float)((double)ent + (double)pr * t);
+        }
+        ent = -ent;
+        return ent / enorm;
+    }
+}
+
+// load one B-float record (vectorised)
+template <int B>
+__device__ __forceinline__ void load_rec(const float *__restrict__ vol, uint64_t vidx,
+                                         float (&r)[B]) {
+    const float *src = vol + vidx * (uint64_t)B;
+    if constexpr (B % 4 == 0) {
+#pragma unroll
+        for (int i = 0; i < B / 4; i++) {
+            const float4 q = *reinterpret_cast<const float4 *>(src + 4 * i);
+            r[4 * i + 0] = q.x; r[4 * i + 1] = q.y; r[4 * i + 2] = q.z; r[4 * i + 3] = q.w;
+        }
+    } else if constexpr (B == 2) {
+        const float2 q = *reinterpret_cast<const float2 *>(src);
+        r[0] = q.x; r[1] = q.y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < B; i++) r[i] = src[i];
+    }
+}
+
+}  // namespace vr

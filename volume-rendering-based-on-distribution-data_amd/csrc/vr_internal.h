@@ -1,0 +1,33 @@
+// vr_internal.h -- declarations shared by the kernels (vr_kernels.hip) and the
+// host-side library state / C-ABI (vr_api.cpp).  Not a public header.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vr_device.h"
+
+namespace vr {
+
+constexpr int kSynthBlobs = 8;   // Gaussian blobs of the scalar field
+constexpr int kSynthG = 16;      // spread levels
+constexpr int kSynthQ = 4096;    // quantised field levels
+
+struct SynthArgs {
+    float amp[kSynthBlobs];
+    const float *gx, *gy, *gz;   // [k][n] separable blob factors
+    const float *table;          // [g][q][nb] normalised histograms
+    int nx, ny, nz, nb;
+    uint64_t seed;
+};
+
+hipError_t launch_march(int nb, int method, const float *vol, const Params &P,
+                        uint32_t nslots, bool count, hipStream_t s);
+hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
+hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,
+                            uint32_t tiles_x, uint32_t *frame, uint32_t W, uint32_t H,
+                            hipStream_t s);
+hipError_t launch_popcount(const unsigned long long *bits, uint64_t nwords,
+                           unsigned long long *total, hipStream_t s);
+
+}  // namespace vr
