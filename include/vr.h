@@ -113,6 +113,10 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed);
 /* dims, bin count and device pointer of the resident volume */
 int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins);
 
+/* Record pitch of a voxel row and of a slice of the resident volume in HBM
+ * (record (x,y,z) starts at d_bins + (z*slice_pitch + y*row_pitch + x)*nbins). */
+int vr_volume_layout(size_t *row_pitch, size_t *slice_pitch);
+
 /* Stream for all subsequent launches (hipStream_t; NULL = null stream). */
 int vr_set_stream(void *stream);
 

@@ -1,0 +1,69 @@
+"""C-ABI checks that need no GPU: libvr.so loads, exports every entry point that
+include/vr.h declares, and reports argument/state errors without exiting
+(no compute call is made)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vr.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src)
+    return sorted(set(n for n in names if n not in ("if", "sizeof")))
+
+
+def test_header_declares_reference_entry_points():
+    names = declared_functions()
+    for ref in ("render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers",
+                "setTextureFilterMode", "basicDataProcessing", "dataProcessing"):
+        assert ref in names
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = ctypes.CDLL(pkg.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, f"libvr.so lacks {missing}"
+    assert set(pkg._lib.EXPORTS) == set(declared_functions())
+
+
+def test_struct_layouts():
+    from ctypes import sizeof
+    import __graft_entry__ as g
+    L = g.load_package()._lib
+    assert sizeof(L.Dim3) == 12           # dim3
+    assert sizeof(L.Extent) == 24         # cudaExtent / hipExtent
+    # vr_render_desc: 3 pointers, 2 u32, 12 f32, 4 f32, int, (pad), extent, ptr, u32 (+pad)
+    assert sizeof(L.RenderDesc) == 8 * 3 + 4 * 2 + 4 * 12 + 4 * 4 + 4 + 4 + 24 + 8 + 8
+
+
+def test_errors_without_gpu(pkg):
+    L = pkg._lib.load()
+    L.vr_clear_error()
+    assert L.vr_render(None) == pkg._lib.VR_ERR_ARG
+    assert b"null" in L.vr_last_error()
+    L.vr_clear_error()
+    # no volume resident: render_kernel records a state error instead of exiting
+    pkg._lib.load().freeCudaBuffers()
+    with pytest.raises(pkg.VRError) as e:
+        pkg.render_kernel((1, 1, 1), (16, 16, 1), 0x1000, 4, 4, 0.05, 1.0, 0.0, 1.0, 1,
+                          (4, 4, 4))
+    assert e.value.status == pkg._lib.VR_ERR_STATE
+    with pytest.raises(pkg.VRError) as e:
+        pkg.dataProcessing()
+    assert e.value.status == pkg._lib.VR_ERR_UNSUPPORTED
+    with pytest.raises(pkg.VRError):
+        pkg.basicDataProcessing()
+    with pytest.raises(pkg.VRError):
+        pkg.initCuda(np.zeros(10, np.float32), (2, 2, 2), (4, 3, 1))  # 3 records != 8 voxels
+    with pytest.raises(pkg.VRError):
+        pkg.copyInvViewMatrix(np.zeros(16, np.float32), 64)            # > 48 bytes
+    pkg.setTextureFilterMode(True)  # stored only
+    assert pkg._lib.load().vr_tiles_x(1920) == 120 and pkg._lib.load().vr_tiles_y(1080) == 68
+    assert "gfx950" in pkg.version()

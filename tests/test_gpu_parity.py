@@ -151,14 +151,17 @@ def test_synth_matches_oracle(pkg, orc, gpu):
                      ((8, 6, 4), 32)]:
         pkg.synthesize(dims, nb, seed=20261015)
         (nx, ny, nz), b, ptr = pkg.volume_info()
-        n = nx * ny * nz * b
+        sy, sz = pkg.volume_layout()
+        n = sz * nz * b
         t = torch.empty(n, dtype=torch.float32, device="cuda")
         torch.cuda.synchronize()
-        # device-to-device copy of the library-owned volume into a torch tensor
+        # device-to-device copy of the library-owned (pitched) volume into a torch tensor
         hip = ctypes.CDLL("libamdhip64.so")
         assert hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr),
                              ctypes.c_size_t(n * 4), 3) == 0
-        got = t.cpu().numpy().reshape(nz, ny, nx, b)
+        flat = t.cpu().numpy()
+        got = np.stack([flat[z * sz * b:(z * sz + ny * sy) * b].reshape(ny, sy, b)[:, :nx]
+                        for z in range(nz)])
         ref = orc.synth_volume(nx, ny, nz, b)
         assert np.array_equal(got, ref), f"synth {dims}x{nb} differs"
 

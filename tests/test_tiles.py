@@ -1,0 +1,101 @@
+"""Multi-GPU image split, on CPU: tile partition properties, and the rank-0 gather
+of packed tile buffers over a world_size-2 gloo process group."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (512, 512), (256, 256), (33, 17), (16, 16)])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_partition_covers_each_tile_once(pkg, W, H, world):
+    T = pkg.tiles
+    lists = T.tile_lists(W, H, world)
+    assert lists.shape[0] == world
+    real = lists[lists != T.PAD]
+    ntiles = T.tiles_x(W) * T.tiles_y(H)
+    assert sorted(real.tolist()) == list(range(ntiles))
+    counts = (lists != T.PAD).sum(1)
+    assert counts.max() - counts.min() <= 4 + T.tiles_x(W) // 2  # +-1 block (+ ragged edge)
+
+
+def test_partition_spreads_the_hit_region(pkg):
+    """every rank gets ~1/8 of the tiles that intersect the box (C0 camera)"""
+    T = pkg.tiles
+    own = T.owner_of(1920, 1080, 8)
+    ty, tx = np.mgrid[0:own.shape[0], 0:own.shape[1]]
+    cx = (tx * 16 + 8) / 1920 * 2 - 1
+    cy = (ty * 16 + 8) / 1080 * 2 - 1
+    hit = (np.abs(cx) < 0.5) & (np.abs(cy) < 0.5)  # ~ the box's screen footprint
+    per_rank = np.bincount(own[hit], minlength=8)
+    assert per_rank.max() / per_rank.mean() < 1.1
+
+
+def _unscatter_np(gathered, lists, W, H, T):
+    frame = np.zeros(H * W, np.uint32)
+    tx = T.tiles_x(W)
+    for r in range(lists.shape[0]):
+        for s, tile in enumerate(lists[r]):
+            if tile == T.PAD:
+                continue
+            for i in range(256):
+                px = (tile % tx) * 16 + (i & 15)
+                py = (tile // tx) * 16 + (i >> 4)
+                if px < W and py < H:
+                    frame[py * W + px] = gathered[r, s * 256 + i]
+    return frame
+
+
+def _worker(rank, world, port, W, H, q):
+    import torch
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as g
+    T = g.load_package().tiles
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(7)
+    frame = rng.integers(0, 2**32, size=H * W, dtype=np.uint64).astype(np.uint32)
+    lists = T.tile_lists(W, H, world)
+    tx = T.tiles_x(W)
+    packed = np.zeros(lists.shape[1] * 256, np.uint32)
+    for s, tile in enumerate(lists[rank]):  # this rank's "render": copy its tiles
+        if tile == T.PAD:
+            continue
+        for i in range(256):
+            px, py = (tile % tx) * 16 + (i & 15), (tile // tx) * 16 + (i >> 4)
+            if px < W and py < H:
+                packed[s * 256 + i] = frame[py * W + px]
+    t = torch.from_numpy(packed.view(np.int32).copy())
+    got = T.gather_packed(t, world, rank)
+    if rank == 0:
+        g_np = got.numpy().view(np.uint32)
+        q.put(bool(np.array_equal(_unscatter_np(g_np, lists, W, H, T), frame)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,H", [(100, 52), (64, 64)])
+def test_gloo_gather_world2(pkg, W, H):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "build", "libvr.so")
+# VRDD_LIB overrides the library path (tools/bench_variants.py loads tuning builds)
+LIB_PATH = os.environ.get("VRDD_LIB") or os.path.join(_HERE, "csrc", "build", "libvr.so")
 
 VR_OK = 0
 VR_ERR_ARG = -1
@@ -61,7 +62,7 @@ EXPORTS = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers",
     "setTextureFilterMode", "basicDataProcessing", "dataProcessing",
     "vr_last_error", "vr_last_status", "vr_clear_error", "vr_init_distribution",
-    "vr_synthesize", "vr_volume_info", "vr_set_stream", "vr_render", "vr_count_footprint",
+    "vr_synthesize", "vr_volume_info", "vr_volume_layout", "vr_set_stream", "vr_render", "vr_count_footprint",
     "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version",
 ]
 
@@ -106,6 +107,9 @@ def load() -> ctypes.CDLL:
     L.vr_volume_info.argtypes = [ctypes.POINTER(Extent), ctypes.POINTER(ctypes.c_int),
                                  ctypes.POINTER(ctypes.c_void_p)]
     L.vr_volume_info.restype = i32
+    L.vr_volume_layout.argtypes = [ctypes.POINTER(ctypes.c_size_t),
+                                   ctypes.POINTER(ctypes.c_size_t)]
+    L.vr_volume_layout.restype = i32
     L.vr_set_stream.argtypes = [vp]
     L.vr_set_stream.restype = i32
     L.vr_render.argtypes = [ctypes.POINTER(RenderDesc)]

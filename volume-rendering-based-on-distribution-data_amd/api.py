@@ -143,6 +143,13 @@ def volume_info():
     return (e.width, e.height, e.depth), nb.value, p.value
 
 
+def volume_layout():
+    """(row_pitch, slice_pitch) of the resident volume, in records."""
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    check(_lib.load().vr_volume_layout(ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
+
+
 def set_stream(stream) -> None:
     """Stream for subsequent launches: a torch.cuda.Stream, a raw hipStream_t, or None."""
     raw = 0 if stream is None else (stream.cuda_stream if hasattr(stream, "cuda_stream")
@@ -195,6 +202,7 @@ def version() -> str:
 __all__ = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers", "setTextureFilterMode",
     "basicDataProcessing", "dataProcessing", "init_distribution", "synthesize", "volume_info",
+    "volume_layout",
     "set_stream", "make_desc", "render", "count_footprint", "unscatter_tiles", "version",
     "VRError", "PAD",
 ]

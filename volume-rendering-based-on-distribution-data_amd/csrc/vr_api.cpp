@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -19,6 +20,7 @@ struct State {
     float *vol = nullptr;
     bool owned = false;
     int nx = 0, ny = 0, nz = 0, nb = 0;
+    uint64_t sy = 0, sz = 0;        // record pitch of a voxel row / slice in HBM
     float inv_view[12] = {0};       // __constant__ c_invViewMatrix starts zeroed (K:116)
     hipStream_t stream = nullptr;   // legacy default stream, like the reference
     bool linear_filter = false;     // tex.filterMode = point after initCuda (K:2163)
@@ -54,6 +56,22 @@ void release_volume() {
     g.vol = nullptr;
     g.owned = false;
     g.nx = g.ny = g.nz = g.nb = 0;
+    g.sy = g.sz = 0;
+}
+
+// Row / slice pitch (in records) of the resident volume.  VR_PAD="px,pz" adds
+// px records to every row and pz records to every slice (layout experiments).
+void choose_pitch(int nx, int ny, uint64_t &sy, uint64_t &sz) {
+    long px = 0, pz = 0;
+    if (const char *e = std::getenv("VR_PAD")) {
+        char *end = nullptr;
+        px = std::strtol(e, &end, 10);
+        if (end && *end == ',') pz = std::strtol(end + 1, nullptr, 10);
+        if (px < 0 || px > 4096) px = 0;
+        if (pz < 0 || pz > (1 << 20)) pz = 0;
+    }
+    sy = (uint64_t)nx + (uint64_t)px;
+    sz = sy * (uint64_t)ny + (uint64_t)pz;
 }
 
 float entropy_norm(int nb) {
@@ -96,6 +114,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     P.toff = d->transfer_offset;
     P.tscale = d->transfer_scale;
     P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
+    P.sy = g.sy; P.sz = g.sz;
     P.m7x = (int)d->volume_size.width;
     P.m7y = (int)d->volume_size.height;
     P.m7z = (int)d->volume_size.depth;
@@ -107,6 +126,26 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     P.out_f = d->d_output_f;
     P.out_n = d->d_steps;
     P.mark = nullptr;
+    // VR_BOX_MAX: per-wave LDS box capacity (tuning / ablation knob; 0 disables staging)
+    P.box_max = vr::kBoxMax;
+    if (const char *e = std::getenv("VR_BOX_MAX")) {
+        const int v = std::atoi(e);
+        if (v >= 0 && v <= 2048) P.box_max = v;
+    }
+    // VR_WG_PER_CU: cap resident workgroups per CU through the LDS request (tuning knob)
+    P.wg_per_cu = 0;
+    if (const char *e = std::getenv("VR_WG_PER_CU")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= 32) P.wg_per_cu = v;
+    }
+    // VR_PATH: 0 = quad-cooperative pipelined gathers (default, B <= 8),
+    //          1 = k_march (LDS-staged box when it fits, else per-ray gathers),
+    //          2 = per-ray pipelined gathers
+    P.path = 0;
+    if (const char *e = std::getenv("VR_PATH")) {
+        const int v = std::atoi(e);
+        P.path = (v >= 0 && v <= 2) ? v : 0;
+    }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {
         nslots = d->n_tiles;
@@ -162,17 +201,29 @@ int vr_init_distribution(const float *bins, vr_extent dims, int nbins, int where
         return fail(VR_ERR_ARG, "empty volume");
     if (dims.width > 65536 || dims.height > 65536 || dims.depth > 65536)
         return fail(VR_ERR_ARG, "volume dimension > 65536");
-    const size_t nvox = dims.width * dims.height * dims.depth;
-    const size_t bytes = nvox * (size_t)nbins * sizeof(float);
     release_volume();
-    if (where == 2) {
+    const int nx = (int)dims.width, ny = (int)dims.height, nz = (int)dims.depth;
+    uint64_t sy, sz;
+    if (where == 2) {  // adopted buffer keeps its dense AoS layout
+        sy = (uint64_t)nx;
+        sz = sy * (uint64_t)ny;
         g.vol = const_cast<float *>(bins);
         g.owned = false;
     } else {
+        choose_pitch(nx, ny, sy, sz);
+        const size_t rec = (size_t)nbins * sizeof(float);
         float *d = nullptr;
-        VR_HIP(hipMalloc(&d, bytes));
-        hipError_t e = hipMemcpy(d, bins, bytes,
-                                 where == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice);
+        VR_HIP(hipMalloc(&d, sz * (size_t)nz * rec));
+        const hipMemcpyKind kind = where == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+        hipError_t e = hipSuccess;
+        if (sy == (uint64_t)nx && sz == sy * (uint64_t)ny) {
+            e = hipMemcpy(d, bins, sz * (size_t)nz * rec, kind);
+        } else {  // one pitched 2-D copy per slice
+            for (int z = 0; z < nz && e == hipSuccess; z++)
+                e = hipMemcpy2D(d + (size_t)z * sz * nbins, sy * rec,
+                                bins + (size_t)z * ny * nx * nbins, (size_t)nx * rec,
+                                (size_t)nx * rec, (size_t)ny, kind);
+        }
         if (e != hipSuccess) {
             (void)hipFree(d);
             return hip_fail(e, "hipMemcpy(volume)");
@@ -180,9 +231,11 @@ int vr_init_distribution(const float *bins, vr_extent dims, int nbins, int where
         g.vol = d;
         g.owned = true;
     }
-    g.nx = (int)dims.width;
-    g.ny = (int)dims.height;
-    g.nz = (int)dims.depth;
+    g.sy = sy;
+    g.sz = sz;
+    g.nx = nx;
+    g.ny = ny;
+    g.nz = nz;
     g.nb = nbins;
     return VR_OK;
 }
@@ -228,6 +281,8 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
         }
     }
     release_volume();
+    uint64_t sy, sz;
+    choose_pitch(nx, ny, sy, sz);
     float *vol = nullptr, *dgx = nullptr, *dgy = nullptr, *dgz = nullptr, *dtab = nullptr;
     auto cleanup = [&]() {
         if (dgx) (void)hipFree(dgx);
@@ -235,7 +290,8 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
         if (dgz) (void)hipFree(dgz);
         if (dtab) (void)hipFree(dtab);
     };
-    hipError_t e = hipMalloc(&vol, nvox * (size_t)nbins * sizeof(float));
+    (void)nvox;
+    hipError_t e = hipMalloc(&vol, sz * (size_t)nz * (size_t)nbins * sizeof(float));
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(volume)");
     e = hipMalloc(&dgx, gx.size() * 4);
     if (e == hipSuccess) e = hipMalloc(&dgy, gy.size() * 4);
@@ -249,6 +305,7 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
     if (e == hipSuccess) {
         a.gx = dgx; a.gy = dgy; a.gz = dgz; a.table = dtab;
         a.nx = nx; a.ny = ny; a.nz = nz; a.nb = nbins; a.seed = seed;
+        a.sy = sy; a.sz = sz;
         e = vr::launch_synth(vol, a, g.stream);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
@@ -260,6 +317,14 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
     g.vol = vol;
     g.owned = true;
     g.nx = nx; g.ny = ny; g.nz = nz; g.nb = nbins;
+    g.sy = sy; g.sz = sz;
+    return VR_OK;
+}
+
+int vr_volume_layout(size_t *row_pitch, size_t *slice_pitch) {
+    if (!g.vol) return fail(VR_ERR_STATE, "no volume resident");
+    if (row_pitch) *row_pitch = (size_t)g.sy;
+    if (slice_pitch) *slice_pitch = (size_t)g.sz;
     return VR_OK;
 }
 

@@ -10,6 +10,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// log(2.0), correctly rounded (K:766)
+#define VR_LN2_D 0x1.62e42fefa39efp-1
+
 namespace vr {
 
 constexpr int kMaxSteps = 500;             // K:276
@@ -23,6 +26,7 @@ struct Params {
     uint32_t W, H;
     float density, brightness, toff, tscale;
     int nx, ny, nz;              // resident volume dims
+    uint64_t sy, sz;             // record pitch of a voxel row / slice in HBM
     int m7x, m7y, m7z;           // render_kernel volumeSize (method 7)
     float enorm;                 // log((float)B)/log(2.0f), K:769
     int nb;                      // bins per record
@@ -33,10 +37,13 @@ struct Params {
     float *out_f;
     int32_t *out_n;
     unsigned long long *mark;    // footprint bitset (count mode only)
+    int box_max;                 // LDS-staged footprint box capacity (voxels per wave), 0 = off
+    int wg_per_cu;               // occupancy cap through the LDS request (0 = none)
+    int path;                    // 0 quad pipelined, 1 k_march, 2 per-ray pipelined
 };
 
-// log(2.0), correctly rounded (K:766)
-#define VR_LN2_D 0x1.62e42fefa39efp-1
+constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)
+
 
 __device__ __forceinline__ float clamp01(float u) { return fminf(fmaxf(u, 0.0f), 1.0f); }
 
@@ -96,6 +103,21 @@ __device__ __forceinline__ uint32_t pack_rgba(float r, float g, float b, float a
            ((uint32_t)(g * 255.0f) << 8) | (uint32_t)(r * 255.0f);
 }
 
+// Division by a constant with the reference's double rounding: q0 = m*R,
+// corrected once with an exact FMA residual (Markstein), R = RN(1/D).
+// tests/c/divcheck.c proves it bit-identical to `m / D` for every float m
+// and each of the three divisors below (~16 cycles instead of ~58 for the
+// full IEEE double-division sequence on gfx950).
+__device__ __forceinline__ double div_const(double m, double D, double R) {
+    const double q0 = m * R;
+    const double e = __builtin_fma(-q0, D, m);
+    const double q = __builtin_fma(e, R, q0);
+    return (q0 == 0.0 || __builtin_isinf(q0)) ? q0 : q;
+}
+constexpr double kMeanD = 0.0217, kMeanR = 1.0 / 0.0217;          // K:758
+constexpr double kVarD = 0.000021, kVarR = 1.0 / 0.000021;        // K:759
+constexpr double kLn2R = 1.0 / VR_LN2_D;                          // K:766
+
 // binWidth, K:736-738
 __device__ __forceinline__ float bin_width(int nb) {
     const float maxh = (float)0.0217;
@@ -136,7 +158,8 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
 #pragma unroll
     for (int i = 0; i < B; i++) {
         const float pr = p[i];
-        const double t = pr <= 0 ? 0.0 : ((double)(float)log((double)pr) / VR_LN2_D);
+        const double t =
+            pr <= 0 ? 0.0 : div_const((double)(float)log((double)pr), VR_LN2_D, kLn2R);
         ent = (float)((double)ent + (double)pr * t);
     }
     ent = -ent;
@@ -147,10 +170,10 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
 template <int B, int M>
 __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
     if constexpr (M == 1) {
-        return (float)((double)raw_mean<B>(p) / 0.0217);
+        return (float)div_const((double)raw_mean<B>(p), kMeanD, kMeanR);
     } else if constexpr (M == 2) {
         const float mean = raw_mean<B>(p);
-        return (float)((double)raw_variance<B>(p, mean) / 0.000021);
+        return (float)div_const((double)raw_variance<B>(p, mean), kVarD, kVarR);
     } else {
         return entropy<B>(p, enorm);
     }
@@ -172,7 +195,7 @@ template <int M>
 __device__ __forceinline__ float record_stat_rt(const float *__restrict__ p, int nb,
                                                 float enorm) {
     if constexpr (M == 1) {
-        return (float)((double)raw_mean_rt(p, nb) / 0.0217);
+        return (float)div_const((double)raw_mean_rt(p, nb), kMeanD, kMeanR);
     } else if constexpr (M == 2) {
         const float mean = raw_mean_rt(p, nb);
         const float maxh = (float)0.0217;
@@ -181,12 +204,13 @@ __device__ __forceinline__ float record_stat_rt(const float *__restrict__ p, int
             const float d = ((float)i / (float)nb) * maxh - mean;
             var = var + p[i] * d * d;
         }
-        return (float)((double)var / 0.000021);
+        return (float)div_const((double)var, kVarD, kVarR);
     } else {
         float ent = 0.0f;
         for (int i = 0; i < nb; i++) {
             const float pr = p[i];
-            const double t = pr <= 0 ? 0.0 : ((double)(float)log((double)pr) / VR_LN2_D);
+            const double t =
+                pr <= 0 ? 0.0 : div_const((double)(float)log((double)pr), VR_LN2_D, kLn2R);
             ent = (float)((double)ent + (double)pr * t);
         }
         ent = -ent;

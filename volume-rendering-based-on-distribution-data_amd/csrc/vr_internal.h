@@ -18,6 +18,7 @@ struct SynthArgs {
     const float *gx, *gy, *gz;   // [k][n] separable blob factors
     const float *table;          // [g][q][nb] normalised histograms
     int nx, ny, nz, nb;
+    uint64_t sy, sz;             // record pitch of a row / slice
     uint64_t seed;
 };
 

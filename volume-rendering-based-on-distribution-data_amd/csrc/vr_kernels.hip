@@ -5,7 +5,10 @@
 //                        one 16x16-pixel tile per 256-thread workgroup,
 //                        XCD-aware tile order.  Per step the statistic is
 //                        decoded from the 8 corner distribution records and
-//                        blended with 8-bit filter weights.
+//                        blended with 8-bit filter weights; when the wave's
+//                        footprint box fits its LDS slice the box is loaded
+//                        coalesced and every voxel decoded once (staged path),
+//                        otherwise each lane gathers its own corners.
 //  k_march_m7<B>         method 7, software-interpolated corner means
 //                        (K:320-367, 395-480), stateful along the ray.
 //  k_synth               the synthetic distribution volume, written in HBM.
@@ -15,6 +18,8 @@
 // K = volumeRender_kernel.cu of the reference.
 #include "vr_device.h"
 #include "vr_internal.h"
+
+#include <algorithm>
 
 namespace vr {
 
@@ -61,52 +66,6 @@ __device__ __forceinline__ void mark_voxel(unsigned long long *mark, uint64_t id
     atomicOr(mark + (idx >> 6), 1ull << (idx & 63));
 }
 
-// tex3D(originalQueryTex, p) of the method's statistic, K:601/619/635
-template <int B, int M, bool COUNT>
-__device__ __forceinline__ float sample_tri(const float *__restrict__ vol, const Params &P,
-                                            float px, float py, float pz) {
-    int x0, x1, y0, y1, z0, z1;
-    float ax, ay, az;
-    lin_axis(px * 0.5f + 0.5f, P.nx, x0, x1, ax);
-    lin_axis(py * 0.5f + 0.5f, P.ny, y0, y1, ay);
-    lin_axis(pz * 0.5f + 0.5f, P.nz, z0, z1, az);
-    const uint64_t nx = (uint64_t)P.nx, ny = (uint64_t)P.ny;
-    const uint64_t r00 = ((uint64_t)z0 * ny + (uint64_t)y0) * nx;
-    const uint64_t r10 = ((uint64_t)z0 * ny + (uint64_t)y1) * nx;
-    const uint64_t r01 = ((uint64_t)z1 * ny + (uint64_t)y0) * nx;
-    const uint64_t r11 = ((uint64_t)z1 * ny + (uint64_t)y1) * nx;
-    const uint64_t vidx[8] = {r00 + x0, r00 + x1, r10 + x0, r10 + x1,
-                              r01 + x0, r01 + x1, r11 + x0, r11 + x1};
-    if constexpr (COUNT) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) mark_voxel(P.mark, vidx[j]);
-    }
-    float s[8];
-    if constexpr (B > 0) {
-        // corners per load group: keep <= 64 record floats live
-        constexpr int CG = (B >= 64) ? 1 : ((64 / B) > 8 ? 8 : (64 / B));
-#pragma unroll
-        for (int g = 0; g < 8; g += CG) {
-            float rec[CG][B];
-#pragma unroll
-            for (int j = 0; j < CG; j++) load_rec<B>(vol, vidx[g + j], rec[j]);
-#pragma unroll
-            for (int j = 0; j < CG; j++) s[g + j] = record_stat<B, M>(rec[j], P.enorm);
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < 8; j++)
-            s[j] = record_stat_rt<M>(vol + vidx[j] * (uint64_t)P.nb, P.nb, P.enorm);
-    }
-    const float c00 = lerpq(s[0], s[1], ax);
-    const float c10 = lerpq(s[2], s[3], ax);
-    const float c01 = lerpq(s[4], s[5], ax);
-    const float c11 = lerpq(s[6], s[7], ax);
-    const float c0 = lerpq(c00, c10, ay);
-    const float c1 = lerpq(c01, c11, ay);
-    return lerpq(c0, c1, az);
-}
-
 // pixel of this thread inside its tile: wave w covers the 8x8 quadrant w
 __device__ __forceinline__ void tile_pixel(uint32_t t, uint32_t &lx, uint32_t &ly) {
     const uint32_t wave = t >> 6, lane = t & 63;
@@ -140,8 +99,265 @@ __device__ __forceinline__ bool composite(const Params &P, float sample, float &
     return sw > kOpacityThreshold;
 }
 
+// ---- wave-level helpers (64 lanes, DPP) ----
+// min over the 64 lanes: row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast 15 / 31 across rows; lane 63 holds the result.
+__device__ __forceinline__ int dpp_min(int v, int ident) {
+    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x111, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x112, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x114, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x118, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xC, 0xF, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int wave_min(int v) { return dpp_min(v, 0x7FFFFFFF); }
+__device__ __forceinline__ int wave_max(int v) { return -dpp_min(-v, 0x7FFFFFFF); }
+
+__device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0; }
+
+// Corners of one sample (K:601 texture footprint): texel indices + 8-bit weights.
+struct Foot {
+    int x0, x1, y0, y1, z0, z1;
+    float ax, ay, az;
+};
+
+__device__ __forceinline__ Foot footprint(const Params &P, float px, float py, float pz) {
+    Foot f;
+    lin_axis(px * 0.5f + 0.5f, P.nx, f.x0, f.x1, f.ax);
+    lin_axis(py * 0.5f + 0.5f, P.ny, f.y0, f.y1, f.ay);
+    lin_axis(pz * 0.5f + 0.5f, P.nz, f.z0, f.z1, f.az);
+    return f;
+}
+
+__device__ __forceinline__ float blend8(const float (&s)[8], const Foot &f) {
+    const float c00 = lerpq(s[0], s[1], f.ax);
+    const float c10 = lerpq(s[2], s[3], f.ax);
+    const float c01 = lerpq(s[4], s[5], f.ax);
+    const float c11 = lerpq(s[6], s[7], f.ax);
+    const float c0 = lerpq(c00, c10, f.ay);
+    const float c1 = lerpq(c01, c11, f.ay);
+    return lerpq(c0, c1, f.az);
+}
+
+// Compile-time tuning knobs (tools/build_variants.sh builds sweeps of them).
+#ifndef VR_DIRECT_CG
+#define VR_DIRECT_CG 8      // corners gathered before decoding, direct path
+#endif
+#ifndef VR_BOX_G
+#define VR_BOX_G 4          // box voxels per lane in flight, staged path
+#endif
+
+// Direct path: each lane gathers and decodes its own 8 corner records.
+template <int B, int M>
+__device__ __forceinline__ float sample_direct(const float *__restrict__ vol, const Params &P,
+                                               const Foot &f) {
+    const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
+    const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
+    const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
+    const uint64_t r11 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y1 * P.sy;
+    const uint64_t vidx[8] = {r00 + f.x0, r00 + f.x1, r10 + f.x0, r10 + f.x1,
+                              r01 + f.x0, r01 + f.x1, r11 + f.x0, r11 + f.x1};
+    float s[8];
+    if constexpr (B > 0) {
+        constexpr int CG0 = (B >= 64) ? 1 : ((64 / B) > 8 ? 8 : (64 / B));
+        constexpr int CG = CG0 < VR_DIRECT_CG ? CG0 : VR_DIRECT_CG;
+#pragma unroll
+        for (int g = 0; g < 8; g += CG) {
+            float rec[CG][B];
+#pragma unroll
+            for (int j = 0; j < CG; j++) load_rec<B>(vol, vidx[g + j], rec[j]);
+#pragma unroll
+            for (int j = 0; j < CG; j++) s[g + j] = record_stat<B, M>(rec[j], P.enorm);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            s[j] = record_stat_rt<M>(vol + vidx[j] * (uint64_t)P.nb, P.nb, P.enorm);
+    }
+    return blend8(s, f);
+}
+
+__device__ __forceinline__ void mark_foot(const Params &P, const Foot &f) {
+    const uint64_t nx = (uint64_t)P.nx, ny = (uint64_t)P.ny;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint64_t z = (j & 4) ? f.z1 : f.z0, y = (j & 2) ? f.y1 : f.y0;
+        const uint64_t x = (j & 1) ? f.x1 : f.x0;
+        mark_voxel(P.mark, (z * ny + y) * nx + x);
+    }
+}
+
+// Staged path: the wave's footprint box for this step (every voxel any active
+// lane's 8 corners touch) is loaded with consecutive lanes on consecutive
+// voxels of a box row (coalesced), each voxel's statistic is decoded ONCE and
+// parked in the wave's LDS slice, then every lane blends its 8 corners from
+// LDS.  Position p -> (x,y,z) in the box uses float reciprocals, exact for
+// p < 2^11 (box_max <= 1024).  Positions past the box end are clamped to its
+// last voxel so every load is unconditional: all G slots' loads issue
+// back-to-back before the first decode waits on them.
+template <int B, int M>
+__device__ __forceinline__ void decode_box(const float *__restrict__ vbase, const Params &P,
+                                           float *box, int dx, int dxy, int V, uint32_t lane) {
+    constexpr int G0 = B >= 32 ? 1 : (B >= 16 ? 2 : 4);
+    constexpr int G = G0 < VR_BOX_G ? G0 : VR_BOX_G;  // voxels per lane in flight
+    const float rdx = 1.0f / (float)dx, rdxy = 1.0f / (float)dxy;
+    const uint32_t sy = (uint32_t)P.sy;
+    for (int p0 = 0; p0 < V; p0 += 64 * G) {
+        float rec[G][B];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int p = min(p0 + g * 64 + (int)lane, V - 1);
+            const int z = (int)(((float)p + 0.5f) * rdxy);
+            const int r = p - z * dxy;
+            const int y = (int)(((float)r + 0.5f) * rdx);
+            const int x = r - y * dx;
+            const uint64_t off = (uint64_t)(uint32_t)z * P.sz + (uint32_t)(y * sy + x);
+            load_rec<B>(vbase, off, rec[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int p = p0 + g * 64 + (int)lane;
+            if (p < V) box[p] = record_stat<B, M>(rec[g], P.enorm);
+        }
+    }
+}
+
 template <int B, int M, bool COUNT>
 __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Params P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const uint32_t slot = xcd_slot(blockIdx.x, gridDim.x);
+    const uint32_t tile = P.tile_list ? P.tile_list[slot] : slot;
+    if (tile == kPad) return;  // whole workgroup uniform
+    const uint32_t lane = threadIdx.x & 63u;
+    float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
+    uint32_t lx, ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+                                   : (uint64_t)y * P.W + x;
+    // every lane stays to the end: the staged decode needs all 64 lanes
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    for (int i = 0; i < kMaxSteps; i++) {
+        if (!wave_any(alive)) break;
+        const Foot f = footprint(P, px, py, pz);
+        if constexpr (COUNT) {
+            if (alive) mark_foot(P, f);
+        }
+        float sample = 0.0f;
+        bool staged = false;
+        if constexpr (B > 0) {
+            if (P.box_max > 0) {
+                const int bx0 = wave_min(alive ? f.x0 : 0x7FFFFFFF);
+                const int by0 = wave_min(alive ? f.y0 : 0x7FFFFFFF);
+                const int bz0 = wave_min(alive ? f.z0 : 0x7FFFFFFF);
+                // x1 = min(x0 + 1, n - 1) except at the low clamp, so this is a
+                // (tight or one-voxel-larger) superset of the upper corners
+                const int bx1 = min(wave_max(alive ? f.x0 : -1) + 1, P.nx - 1);
+                const int by1 = min(wave_max(alive ? f.y0 : -1) + 1, P.ny - 1);
+                const int bz1 = min(wave_max(alive ? f.z0 : -1) + 1, P.nz - 1);
+                const int dx = bx1 - bx0 + 1, dy = by1 - by0 + 1, dz = bz1 - bz0 + 1;
+                if (dx * dy * dz <= P.box_max) {  // wave-uniform
+                    staged = true;
+                    const int dxy = dx * dy;
+                    const float *vbase =
+                        vol + ((uint64_t)bz0 * P.sz + (uint64_t)by0 * P.sy + (uint64_t)bx0) *
+                                  (uint64_t)B;
+                    decode_box<B, M>(vbase, P, box, dx, dxy, dxy * dz, lane);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (alive) {
+                        const int b0 = ((f.z0 - bz0) * dy + (f.y0 - by0)) * dx + (f.x0 - bx0);
+                        const int ox = f.x1 - f.x0, oy = (f.y1 - f.y0) * dx;
+                        const int oz = (f.z1 - f.z0) * dxy;
+                        float s[8];
+                        s[0] = box[b0];
+                        s[1] = box[b0 + ox];
+                        s[2] = box[b0 + oy];
+                        s[3] = box[b0 + oy + ox];
+                        s[4] = box[b0 + oz];
+                        s[5] = box[b0 + oz + ox];
+                        s[6] = box[b0 + oz + oy];
+                        s[7] = box[b0 + oz + oy + ox];
+                        sample = blend8(s, f);
+                    }
+                    // the slice is rewritten next step: keep these reads ahead of it
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+            }
+        }
+        if (alive) {
+            if (!staged) sample = sample_direct<B, M>(vol, P, f);
+            n = i + 1;
+            if (composite(P, sample, sx, sy, sz, sw)) {
+                alive = false;
+            } else {
+                t = t + kTStep;
+                if (t > r.tfar) {
+                    alive = false;
+                } else {
+                    px = px + stx;
+                    py = py + sty;
+                    pz = pz + stz;
+                }
+            }
+        }
+    }
+    if (!valid) return;
+    if (n == 0) {  // miss (K:302-303): nothing written
+        if (P.out_n) P.out_n[o] = -1;
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
+// ---- software-pipelined march (B <= 8) ----
+// Same arithmetic as k_march's direct path, but the 8 corner records of step
+// i+1 are gathered into a second register set BEFORE step i is decoded, so
+// every wave always has a step's gathers in flight while its f64 decode runs.
+// The prefetch assumes the ray continues; a ray that terminates early
+// (sum.w > 0.95) wastes one step of gathers.  The loop is unrolled by two so
+// the two register sets swap roles without copies.
+template <int B>
+__device__ __forceinline__ void gather8(const float *__restrict__ vol, const Params &P,
+                                        const Foot &f, float (&rec)[8][B]) {
+    const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
+    const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
+    const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
+    const uint64_t r11 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y1 * P.sy;
+    load_rec<B>(vol, r00 + f.x0, rec[0]);
+    load_rec<B>(vol, r00 + f.x1, rec[1]);
+    load_rec<B>(vol, r10 + f.x0, rec[2]);
+    load_rec<B>(vol, r10 + f.x1, rec[3]);
+    load_rec<B>(vol, r01 + f.x0, rec[4]);
+    load_rec<B>(vol, r01 + f.x1, rec[5]);
+    load_rec<B>(vol, r11 + f.x0, rec[6]);
+    load_rec<B>(vol, r11 + f.x1, rec[7]);
+}
+
+template <int B, int M>
+__device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][B],
+                                         const Foot &f) {
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) s[j] = record_stat<B, M>(rec[j], P.enorm);
+    return blend8(s, f);
+}
+
+template <int B, int M>
+__global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vol, Params P) {
     const uint32_t slot = xcd_slot(blockIdx.x, gridDim.x);
     const uint32_t tile = P.tile_list ? P.tile_list[slot] : slot;
     if (tile == kPad) return;
@@ -149,7 +365,7 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTile + lx;
     const uint32_t y = (tile / P.tiles_x) * kTile + ly;
-    if (x >= P.W || y >= P.H) return;
+    if (x >= P.W || y >= P.H) return;  // no cross-lane work in this kernel
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -162,15 +378,228 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
     float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
     const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
     int n = 0;
-    for (int i = 0; i < kMaxSteps; i++) {
-        const float sample = sample_tri<B, M, COUNT>(vol, P, px, py, pz);
+    bool alive = true;
+    Foot fa = footprint(P, px, py, pz), fb;
+    float ra[8][B], rb[8][B];
+    gather8<B>(vol, P, fa, ra);
+    // one step: decode (fc, rc) while the gathers of the next step go to (fn, rn)
+    auto step = [&](int i, const Foot &fc, const float (&rc)[8][B], Foot &fn,
+                    float (&rn)[8][B]) {
+        const float tn = t + kTStep;                               // K:701
+        const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, K:381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;   // K:706
+        if (cont) {
+            fn = footprint(P, nx, ny, nz);
+            gather8<B>(vol, P, fn, rn);
+        }
+        const float sample = decode8<B, M>(P, rc, fc);
         n = i + 1;
-        if (composite(P, sample, sx, sy, sz, sw)) break;
-        t = t + kTStep;
-        if (t > r.tfar) break;
-        px = px + stx;
-        py = py + sty;
-        pz = pz + stz;
+        if (composite(P, sample, sx, sy, sz, sw) || !cont) {
+            alive = false;
+        } else {
+            t = tn;
+            px = nx;
+            py = ny;
+            pz = nz;
+        }
+    };
+    for (int i = 0; i < kMaxSteps; i += 2) {
+        step(i, fa, ra, fb, rb);
+        if (!alive) break;
+        step(i + 1, fb, rb, fa, ra);
+        if (!alive) break;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
+// ---- quad-cooperative pipelined march (B == 8) ----
+// Lane l = 4q + g of a wave is the home of the ray at pixel (q, g) of the
+// wave's 16x4 pixel block (the 4 waves of a workgroup stack to 16x16).  For
+// the gathers the four lanes of quad q work for ray (G, q), G = 0..3 in turn:
+// per (y,z) corner combo they read that ray's x0/x1 record pair as ONE
+// contiguous 64-byte run (lane g takes 16-byte chunk g), so every 4-lane group
+// of a gather instruction is one contiguous request.  This is the cheapest
+// pattern for the texture-address path, which bounds per-ray 16-byte gathers
+// at 32-byte strides (tools/ta_rates.hip, tools/replay_loads.hip, PMC
+// TA_TA_BUSY ~90 %).  A pair swap with the xor-1 neighbour then gives each
+// lane two complete records -- corner (x = g>>1, y = g&1) at z0 and z1 -- so
+// every corner is still decoded exactly once, and the blend runs inside the
+// quad in the reference's lerp order (x, then y, then z).  Next-step gathers
+// are issued group by group into the registers the current group has just
+// released (rolling prefetch).
+
+// quad_perm DPP: lane g of each quad reads lane sel[g] of its quad
+template <int CTRL>
+__device__ __forceinline__ float qperm(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int qpermi(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+constexpr int kQ0 = 0x00, kQ1 = 0x55, kQ2 = 0xAA, kQ3 = 0xFF;  // broadcast lane 0/1/2/3
+constexpr int kQx1 = 0xB1;   // [1,0,3,2]
+constexpr int kQ0101 = 0x44; // [0,1,0,1]
+constexpr int kQ2323 = 0xEE; // [2,3,2,3]
+
+template <int G>
+__device__ __forceinline__ int bcast_g(int v) {
+    if constexpr (G == 0) return qpermi<kQ0>(v);
+    else if constexpr (G == 1) return qpermi<kQ1>(v);
+    else if constexpr (G == 2) return qpermi<kQ2>(v);
+    else return qpermi<kQ3>(v);
+}
+
+// footprint packed for the quad broadcast:
+//   w0 = x0 | y0 << 16,  w1 = z0 | dx << 16 | dy << 17 | dz << 18 | live << 19,
+//   w2 = filter weights in 9-bit fixed point (exact: q8 gives k/256, k <= 256)
+struct FootPacked {
+    int w0, w1, w2;
+};
+
+__device__ __forceinline__ FootPacked pack_foot(const Foot &f, bool live) {
+    FootPacked p;
+    p.w0 = f.x0 | (f.y0 << 16);
+    p.w1 = f.z0 | ((f.x1 - f.x0) << 16) | ((f.y1 - f.y0) << 17) | ((f.z1 - f.z0) << 18) |
+           ((live ? 1 : 0) << 19);
+    p.w2 = (int)(f.ax * 256.0f) | ((int)(f.ay * 256.0f) << 9) | ((int)(f.az * 256.0f) << 18);
+    return p;
+}
+
+// Gather ray (G, q)'s four x-pairs: L[c] = chunk g of the pair at combo c =
+// (y = c & 1, z = c >> 1).  A pair clamped at the x edge (x1 == x0) repeats x0.
+template <int G>
+__device__ __forceinline__ bool qc_gather(const float *__restrict__ vol, const Params &P,
+                                          const FootPacked &fp, uint32_t g, float4 (&L)[4]) {
+    const int w0 = bcast_g<G>(fp.w0), w1 = bcast_g<G>(fp.w1);
+    const bool live = (w1 >> 19) & 1;
+    if (live) {
+        const uint64_t x0 = (uint32_t)w0 & 0xFFFFu, y0 = (uint32_t)w0 >> 16;
+        const uint64_t z0 = (uint32_t)w1 & 0xFFFFu;
+        const uint64_t ddy = (w1 >> 17) & 1, ddz = (w1 >> 18) & 1;
+        const uint32_t chunk = ((w1 >> 16) & 1) ? g : (g & 1u);
+        const uint64_t r00 = z0 * P.sz + y0 * P.sy + x0;
+        const uint64_t r10 = r00 + ddy * P.sy, r01 = r00 + ddz * P.sz, r11 = r10 + ddz * P.sz;
+        L[0] = reinterpret_cast<const float4 *>(vol + r00 * 8)[chunk];
+        L[1] = reinterpret_cast<const float4 *>(vol + r10 * 8)[chunk];
+        L[2] = reinterpret_cast<const float4 *>(vol + r01 * 8)[chunk];
+        L[3] = reinterpret_cast<const float4 *>(vol + r11 * 8)[chunk];
+    }
+    return live;
+}
+
+// pair swap: from the chunks of combos (c, c') build lane g's full record of
+// corner (x = g >> 1, combo = g & 1 ? c' : c)
+__device__ __forceinline__ float swp(float i1, float i2, bool odd, bool hi) {
+    const float recv = qperm<kQx1>(odd ? i1 : i2);
+    return hi ? (odd ? i2 : recv) : (odd ? recv : i1);
+}
+__device__ __forceinline__ void pair_swap(const float4 &i1, const float4 &i2, bool odd,
+                                          float (&rec)[8]) {
+    rec[0] = swp(i1.x, i2.x, odd, false); rec[1] = swp(i1.y, i2.y, odd, false);
+    rec[2] = swp(i1.z, i2.z, odd, false); rec[3] = swp(i1.w, i2.w, odd, false);
+    rec[4] = swp(i1.x, i2.x, odd, true);  rec[5] = swp(i1.y, i2.y, odd, true);
+    rec[6] = swp(i1.z, i2.z, odd, true);  rec[7] = swp(i1.w, i2.w, odd, true);
+}
+
+// in-quad trilinear blend of ray (G, q): lane g holds corner (x = g>>1, y = g&1)
+// at z0 (s0) and z1 (s1).  Same lerp order as blend8 (x, then y, then z).
+template <int G>
+__device__ __forceinline__ float qc_blend(const FootPacked &fp, float s0, float s1) {
+    const int w2 = bcast_g<G>(fp.w2);
+    const float ax = (float)(w2 & 0x1FF) * (1.0f / 256.0f);
+    const float ay = (float)((w2 >> 9) & 0x1FF) * (1.0f / 256.0f);
+    const float az = (float)((w2 >> 18) & 0x1FF) * (1.0f / 256.0f);
+    // x: lane g gets c(y = g&1, z) = lerp(s(x0,y), s(x1,y), ax)
+    const float cz0 = lerpq(qperm<kQ0101>(s0), qperm<kQ2323>(s0), ax);
+    const float cz1 = lerpq(qperm<kQ0101>(s1), qperm<kQ2323>(s1), ax);
+    // y: c(z) = lerp(c(y0,z), c(y1,z), ay), identical in all four lanes
+    const float c0 = lerpq(qperm<kQ0>(cz0), qperm<kQ1>(cz0), ay);
+    const float c1 = lerpq(qperm<kQ0>(cz1), qperm<kQ1>(cz1), ay);
+    return lerpq(c0, c1, az);
+}
+
+template <int G, int M>
+__device__ __forceinline__ float qc_group(const float *__restrict__ vol, const Params &P,
+                                          const FootPacked &fc, bool lc, const FootPacked &fn,
+                                          bool &ln, uint32_t g, float4 (&L)[4]) {
+    // this step's records of ray (G, q) out of the chunk registers ...
+    const bool odd = g & 1u;
+    float r0[8], r1[8];
+    pair_swap(L[0], L[1], odd, r0);  // combo (y = g&1, z0)
+    pair_swap(L[2], L[3], odd, r1);  // combo (y = g&1, z1)
+    // ... which frees them for the next step's gathers of the same group
+    ln = qc_gather<G>(vol, P, fn, g, L);
+    float s0 = 0.0f, s1 = 0.0f;
+    if (lc) {
+        s0 = record_stat<8, M>(r0, P.enorm);
+        s1 = record_stat<8, M>(r1, P.enorm);
+    }
+    return qc_blend<G>(fc, s0, s1);
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void k_march_quad(const float *__restrict__ vol, Params P) {
+    const uint32_t slot = xcd_slot(blockIdx.x, gridDim.x);
+    const uint32_t tile = P.tile_list ? P.tile_list[slot] : slot;
+    if (tile == kPad) return;  // uniform per workgroup
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t q = lane >> 2, g = lane & 3u;
+    const uint32_t lx = q, ly = wave * 4u + g;  // 16x4 block per wave
+    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+                                   : (uint64_t)y * P.W + x;
+    // every lane stays to the end: quads cooperate on each other's rays
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    const bool hit = alive;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    float4 L0[4], L1[4], L2[4], L3[4];  // chunk registers of groups 0..3
+    FootPacked fc = pack_foot(footprint(P, px, py, pz), alive);
+    bool lc[4];
+    lc[0] = qc_gather<0>(vol, P, fc, g, L0);
+    lc[1] = qc_gather<1>(vol, P, fc, g, L1);
+    lc[2] = qc_gather<2>(vol, P, fc, g, L2);
+    lc[3] = qc_gather<3>(vol, P, fc, g, L3);
+    for (int i = 0; i < kMaxSteps; i++) {
+        if (!wave_any(alive)) break;
+        // next step of this lane's own ray (speculative: assumes no early exit)
+        const float tn = t + kTStep;                                        // K:701
+        const bool cont = alive && !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, 381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
+        const FootPacked fn = pack_foot(footprint(P, nx, ny, nz), cont);
+        bool ln[4];
+        const float b0 = qc_group<0, M>(vol, P, fc, lc[0], fn, ln[0], g, L0);
+        const float b1 = qc_group<1, M>(vol, P, fc, lc[1], fn, ln[1], g, L1);
+        const float b2 = qc_group<2, M>(vol, P, fc, lc[2], fn, ln[2], g, L2);
+        const float b3 = qc_group<3, M>(vol, P, fc, lc[3], fn, ln[3], g, L3);
+        const float sample = g == 0 ? b0 : (g == 1 ? b1 : (g == 2 ? b2 : b3));
+        if (alive) {
+            n = i + 1;
+            if (composite(P, sample, sx, sy, sz, sw) || !cont) {
+                alive = false;
+            } else {
+                t = tn;
+                px = nx;
+                py = ny;
+                pz = nz;
+            }
+        }
+        fc = fn;
+#pragma unroll
+        for (int k = 0; k < 4; k++) lc[k] = ln[k];
+    }
+    if (!valid) return;
+    if (!hit) {
+        if (P.out_n) P.out_n[o] = -1;
+        return;
     }
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
                 sw * P.brightness);
@@ -186,7 +615,7 @@ template <int B>
 __device__ __forceinline__ float corner_mean(const float *__restrict__ vol, const Params &P,
                                              float ux, float uy, float uz) {
     const int ix = point_axis(ux, P.nx), iy = point_axis(uy, P.ny), iz = point_axis(uz, P.nz);
-    const uint64_t vidx = ((uint64_t)iz * (uint64_t)P.ny + (uint64_t)iy) * (uint64_t)P.nx + ix;
+    const uint64_t vidx = (uint64_t)iz * P.sz + (uint64_t)iy * P.sy + (uint64_t)ix;
     if constexpr (B > 0) {
         float rec[B];
         load_rec<B>(vol, vidx, rec);
@@ -287,7 +716,7 @@ __global__ __launch_bounds__(256) void k_synth(float *__restrict__ vol, SynthArg
             f = f + ((a.amp[k] * a.gx[k * a.nx + x]) * a.gy[k * a.ny + y]) * a.gz[k * a.nz + z];
         if (f > 1.0f) f = 1.0f;
         const int nb = B > 0 ? B : a.nb;
-        float *dst = vol + v * (uint64_t)nb;
+        float *dst = vol + ((uint64_t)z * a.sz + (uint64_t)y * a.sy + x) * (uint64_t)nb;
         if (nb == 1) {
             dst[0] = f;
             continue;
@@ -333,13 +762,36 @@ __global__ __launch_bounds__(256) void k_popcount(const unsigned long long *__re
 // ------------------------------ launchers ---------------------------------
 
 template <int B, bool COUNT>
-static hipError_t march_b(int method, const float *vol, const Params &P, uint32_t nslots,
+static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslots,
                           hipStream_t s) {
     const dim3 grid(nslots), block(256);
+    // one f32 box slice of box_max voxels per wave (4 waves); a larger request
+    // caps the workgroups resident per CU (160 KiB of LDS per CU)
+    size_t lds = B > 0 ? (size_t)P.box_max * 4u * sizeof(float) : 0;
+    if (P.wg_per_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / P.wg_per_cu) & ~(size_t)255);
+    if constexpr (!COUNT && B > 0 && B <= 8) {
+        if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {
+            switch (method) {
+            case 1: hipLaunchKernelGGL((k_march_quad<1>), grid, block, 0, s, vol, P); break;
+            case 2: hipLaunchKernelGGL((k_march_quad<2>), grid, block, 0, s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_quad<3>), grid, block, 0, s, vol, P); break;
+            }
+            return hipGetLastError();
+        }
+        if (B < 8 && P.path == 0) P.path = 2;  // per-ray pipelined for narrow records
+        if (P.path == 2 && method >= 1 && method <= 3) {
+            switch (method) {
+            case 1: hipLaunchKernelGGL((k_march_pipe<B, 1>), grid, block, 0, s, vol, P); break;
+            case 2: hipLaunchKernelGGL((k_march_pipe<B, 2>), grid, block, 0, s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3>), grid, block, 0, s, vol, P); break;
+            }
+            return hipGetLastError();
+        }
+    }
     switch (method) {
-    case 1: hipLaunchKernelGGL((k_march<B, 1, COUNT>), grid, block, 0, s, vol, P); break;
-    case 2: hipLaunchKernelGGL((k_march<B, 2, COUNT>), grid, block, 0, s, vol, P); break;
-    case 3: hipLaunchKernelGGL((k_march<B, 3, COUNT>), grid, block, 0, s, vol, P); break;
+    case 1: hipLaunchKernelGGL((k_march<B, 1, COUNT>), grid, block, lds, s, vol, P); break;
+    case 2: hipLaunchKernelGGL((k_march<B, 2, COUNT>), grid, block, lds, s, vol, P); break;
+    case 3: hipLaunchKernelGGL((k_march<B, 3, COUNT>), grid, block, lds, s, vol, P); break;
     case 7:
         if (COUNT) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_march_m7<B>), grid, block, 0, s, vol, P);

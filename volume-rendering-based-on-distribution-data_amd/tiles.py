@@ -6,11 +6,12 @@ inside 288 GB of HBM) and ray-casts only its own tiles.  Rays are independent
 volume), so the one exchange per frame is gathering the finished tiles to
 rank 0 (an RCCL gather over xGMI when the process group is NCCL/RCCL).
 
-Tiles are the 16x16-pixel tiles of the march kernel.  They are dealt to ranks
-in 2x2-tile blocks (32x32 px) on a diagonal pattern, so every rank gets an
-equal share of tiles spread over the whole image: only ~45 % of the pixels hit
-the volume at the reference camera, so contiguous bands would be badly
-unbalanced.
+Tiles are the 16x16-pixel tiles of the march kernel.  They are grouped in
+2x2-tile blocks (32x32 px); the blocks are enumerated along a serpentine
+(boustrophedon) path over the image and dealt round-robin, so every rank gets
+the same number of blocks (+-1) spread over the whole image: only ~45 % of the
+pixels hit the volume at the reference camera, so contiguous bands would be
+badly unbalanced.
 """
 from __future__ import annotations
 
@@ -32,9 +33,11 @@ def tiles_y(height: int) -> int:
 def owner_of(width: int, height: int, world_size: int) -> np.ndarray:
     """rank owning each tile, shape (tiles_y, tiles_x)."""
     tx, ty = tiles_x(width), tiles_y(height)
-    bx = np.arange(tx) // BLOCK
-    by = np.arange(ty) // BLOCK
-    return ((bx[None, :] + 3 * by[:, None]) % world_size).astype(np.int64)
+    nbx, nby = (tx + BLOCK - 1) // BLOCK, (ty + BLOCK - 1) // BLOCK
+    by, bx = np.mgrid[0:nby, 0:nbx]
+    snake = np.where(by % 2 == 0, bx, nbx - 1 - bx)
+    block_rank = (by * nbx + snake) % world_size
+    return np.repeat(np.repeat(block_rank, BLOCK, 0), BLOCK, 1)[:ty, :tx].astype(np.int64)
 
 
 def tile_lists(width: int, height: int, world_size: int) -> np.ndarray:
