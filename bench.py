@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=0,
                     help="CPU baseline renders every k-th row (0 = auto)")
-    ap.add_argument("--traffic-json", default="",
-                    help="rocprofv3 PMC summary (tools/pmc_traffic.py) for roofline.traffic")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for "
+                         "roofline.traffic; used only when the kernel matches")
     return ap.parse_args()
 
 
@@ -59,20 +60,26 @@ def cpu_baseline(pkg, cfg_name, m, method, row_stride):
     n, nb, W, H = CONFIGS[cfg_name]
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     if row_stride <= 0:
-        row_stride = {128: 1, 256: 2, 512: 8, 1024: 8}[n]
+        row_stride = 1  # the whole frame
     vol = orc.synth_volume(n, n, n, nb, SEED, threads)
     p = orc.make_params(W, H, m, query_method=method, m7_dims=(n, n, n))
-    t0 = time.perf_counter()
-    _, _, _, samples = orc.render(vol, p, row_start=0, row_stride=row_stride, nthreads=threads,
-                                  want_float=False, want_steps=False)
-    dt = time.perf_counter() - t0
+    # repeat the frame until ~24 core-seconds of work have been timed
+    frames, samples, dt = 0, 0, 0.0
+    while frames == 0 or dt * threads < 24.0 and frames < 16:
+        t0 = time.perf_counter()
+        _, _, _, s = orc.render(vol, p, row_start=0, row_stride=row_stride, nthreads=threads,
+                                want_float=False, want_steps=False)
+        dt += time.perf_counter() - t0
+        samples += s
+        frames += 1
     rows = len(range(0, H, row_stride))
-    rays = rows * W
+    rays = rows * W * frames
     del vol
     return {
         "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
         "sample": (f"oracle/vr_oracle.c (-O3, OpenMP) on every {row_stride}th row of the "
-                   f"{W}x{H} frame ({rays} rays, {samples} samples, {dt:.2f} s), "
+                   f"{W}x{H} frame, {frames} frame(s) ({rays} rays, {samples} samples, "
+                   f"{dt:.2f} s on {threads} threads), "
                    f"full {n}^3x{nb} volume in host RAM"),
     }
 
@@ -158,6 +165,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kernel = pkg.last_kernel()
 
     # algorithmic bytes of one launch on this rank: U*S_rec + pixels*4
     u = pkg.count_footprint(desc)
@@ -165,12 +173,15 @@ def main():
     alg_bytes = u * nb * 4 + pixels * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
+    # HBM bytes per launch from the committed PMC passes of this same workload
+    # (tools/pmc_traffic.py; FETCH_SIZE x 2 + WRITE_SIZE), only if measured on
+    # the kernel variant that ran here
     traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
+    if world == 1 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if tj.get("config") == args.config and tj.get("n_gpus", 1) == world:
-            traffic = tj.get("hbm_bytes_per_launch")
+            entry = json.load(f).get(f"{args.config}|{args.camera}|m{args.method}")
+        if entry and entry.get("kernel") == kernel:
+            traffic = entry.get("hbm_bytes_per_launch")
 
     ms_per_step = elapsed / args.steps * 1e3
     value = W * H / (elapsed / args.steps) / 1e6
@@ -180,7 +191,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(pkg, args.config, m, args.method, args.cpu_row_stride)
         out = {
-            "metric": f"Mrays/s at {n}^3 x {nb}-bin volume, {W}x{H}",
+            "metric": f"Mrays/s + fps at {n}^3 x {nb}-bin volume, {W}x{H}; % HBM roofline",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -204,8 +215,7 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": (f"k_march<{nb},{args.method},false>" if args.method != 7
-                           else f"k_march_m7<{nb}>"),
+                "kernel": kernel,
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes), "U_records": int(u),
             },

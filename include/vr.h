@@ -161,6 +161,10 @@ int vr_unscatter_tiles(const uint32_t *d_packed, const uint32_t *d_tile_lists,
 uint32_t vr_tiles_x(uint32_t width);
 uint32_t vr_tiles_y(uint32_t height);
 
+/* name and template arguments of the march kernel the last vr_render /
+ * render_kernel call launched (e.g. "k_march_quad<B=8,M=1>"), "" before any */
+const char *vr_last_kernel(void);
+
 /* library version string */
 const char *vr_version(void);
 

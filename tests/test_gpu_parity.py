@@ -221,3 +221,39 @@ def test_errors_do_not_exit(pkg, gpu):
     pkg.freeCudaBuffers()
     with pytest.raises(pkg.VRError):
         pkg.render_kernel((1, 1, 1), (16, 16, 1), out, 4, 4, 0.05, 1.0, 0.0, 1.0, 1, (4, 4, 4))
+
+
+@pytest.mark.parametrize("path,env", [
+    ("0", {}), ("1", {}), ("2", {}),
+    ("1", {"VR_BOX_MAX": "0"}), ("1", {"VR_BOX_MAX": "64"}), ("0", {"VR_WG_PER_CU": "1"}),
+])
+@pytest.mark.parametrize("nb", [4, 8])
+def test_every_kernel_path(pkg, orc, gpu, path, env, nb, monkeypatch):
+    """each march variant (quad / LDS-staged box with fallback / per-ray pipelined) is
+    bit-identical to the oracle on both cameras and all three statistics"""
+    import torch
+    monkeypatch.setenv("VR_PATH", path)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    vol = orc.synth_volume(26, 22, 18, nb)
+    pkg.init_distribution(vol)
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),
+                pkg.camera.display_inv_view((-60.0, 110.0))):
+        for method in (1, 2, 3):
+            got = gpu_render(pkg, None, 80, 64, cam, method, torch)
+            ref = orc.render(vol, orc.make_params(80, 64, cam, query_method=method))[:3]
+            assert_parity(got, ref, f"path {path} {env} nb={nb} m{method}")
+
+
+def test_padded_layout(pkg, orc, gpu, monkeypatch):
+    """pitched rows / slices (VR_PAD) change only addresses, never results"""
+    import torch
+    vol = orc.synth_volume(20, 18, 16, 8)
+    ref = orc.render(vol, orc.make_params(64, 48, pkg.camera.display_inv_view(), query_method=1))[:3]
+    for pad in ("4,0", "3,77"):
+        monkeypatch.setenv("VR_PAD", pad)
+        got = gpu_render(pkg, vol, 64, 48, pkg.camera.display_inv_view(), 1, torch)
+        assert_parity(got, ref, f"pad {pad}")
+        pkg.synthesize((20, 18, 16), 8)
+        got = gpu_render(pkg, None, 64, 48, pkg.camera.display_inv_view(), 1, torch)
+        assert_parity(got, ref, f"synth pad {pad}")

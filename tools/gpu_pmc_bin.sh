@@ -8,4 +8,4 @@ while read -r CTRS; do
   [ -z "$CTRS" ] && continue
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $CTRS --output-format csv -d gpurun_out/pmc/$TAG/p$i -o $TAG -- "$@" > gpurun_out/pmc/$TAG.p$i.log 2>&1; rc=$?; echo "$TAG pass $i rc=$rc"; guard $rc
-done < tools/pmc_sets_mem.txt
+done < ${SETS:-tools/pmc_sets_mem.txt}

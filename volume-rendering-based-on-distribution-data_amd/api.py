@@ -195,6 +195,11 @@ def unscatter_tiles(d_packed, d_tile_lists, n_ranks: int, n_slots: int, d_frame,
                                          int(n_slots), _ptr(d_frame), int(width), int(height)))
 
 
+def last_kernel() -> str:
+    """The march kernel (and its template arguments) the last render launched."""
+    return _lib.load().vr_last_kernel().decode()
+
+
 def version() -> str:
     return _lib.load().vr_version().decode()
 
@@ -203,6 +208,6 @@ __all__ = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers", "setTextureFilterMode",
     "basicDataProcessing", "dataProcessing", "init_distribution", "synthesize", "volume_info",
     "volume_layout",
-    "set_stream", "make_desc", "render", "count_footprint", "unscatter_tiles", "version",
+    "set_stream", "make_desc", "render", "count_footprint", "unscatter_tiles", "last_kernel", "version",
     "VRError", "PAD",
 ]

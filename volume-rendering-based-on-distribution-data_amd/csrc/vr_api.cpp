@@ -138,13 +138,16 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
         const int v = std::atoi(e);
         if (v >= 1 && v <= 32) P.wg_per_cu = v;
     }
-    // VR_PATH: 0 = quad-cooperative pipelined gathers (default, B <= 8),
-    //          1 = k_march (LDS-staged box when it fits, else per-ray gathers),
-    //          2 = per-ray pipelined gathers
-    P.path = 0;
+    // Kernel choice.  Per-ray lanes (path 2) coalesce when the screen x axis
+    // runs along the volume's voxel rows (|m[0]| ~ 1, e.g. the runSingleTest
+    // view): consecutive lanes then read consecutive records.  Otherwise the
+    // quad-cooperative gathers (path 0, B == 8) keep every 4-lane group on one
+    // contiguous 64-byte run.  VR_PATH overrides: 0 quad, 1 k_march (LDS-staged
+    // box / per-ray), 2 per-ray pipelined.
+    P.path = std::fabs(d->inv_view[0]) >= 0.95f ? 2 : 0;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
-        P.path = (v >= 0 && v <= 2) ? v : 0;
+        if (v >= 0 && v <= 2) P.path = v;
     }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {
@@ -179,6 +182,8 @@ void blob_axis(int n, double c, double s, float *out) {
 extern "C" {
 
 const char *vr_version(void) { return "vrdd-amd 0.1 (gfx950)"; }
+
+const char *vr_last_kernel(void) { return vr::last_march_kernel(); }
 const char *vr_last_error(void) { return g.err.c_str(); }
 int vr_last_status(void) { return g.status; }
 void vr_clear_error(void) {

@@ -24,6 +24,8 @@ struct SynthArgs {
 
 hipError_t launch_march(int nb, int method, const float *vol, const Params &P,
                         uint32_t nslots, bool count, hipStream_t s);
+// name of the march kernel the last non-counting launch_march() chose
+const char *last_march_kernel();
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,
                             uint32_t tiles_x, uint32_t *frame, uint32_t W, uint32_t H,

@@ -20,6 +20,7 @@
 #include "vr_internal.h"
 
 #include <algorithm>
+#include <cstdio>
 
 namespace vr {
 
@@ -761,6 +762,14 @@ __global__ __launch_bounds__(256) void k_popcount(const unsigned long long *__re
 
 // ------------------------------ launchers ---------------------------------
 
+static char g_last_kernel[64] = "";
+
+static void note_kernel(const char *kind, int B, int method) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "%s<B=%d,M=%d>", kind, B, method);
+}
+
+const char *last_march_kernel() { return g_last_kernel; }
+
 template <int B, bool COUNT>
 static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslots,
                           hipStream_t s) {
@@ -771,6 +780,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     if (P.wg_per_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / P.wg_per_cu) & ~(size_t)255);
     if constexpr (!COUNT && B > 0 && B <= 8) {
         if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {
+            note_kernel("k_march_quad", B, method);
             switch (method) {
             case 1: hipLaunchKernelGGL((k_march_quad<1>), grid, block, 0, s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_quad<2>), grid, block, 0, s, vol, P); break;
@@ -780,6 +790,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         }
         if (B < 8 && P.path == 0) P.path = 2;  // per-ray pipelined for narrow records
         if (P.path == 2 && method >= 1 && method <= 3) {
+            note_kernel("k_march_pipe", B, method);
             switch (method) {
             case 1: hipLaunchKernelGGL((k_march_pipe<B, 1>), grid, block, 0, s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_pipe<B, 2>), grid, block, 0, s, vol, P); break;
@@ -788,6 +799,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             return hipGetLastError();
         }
     }
+    if (!COUNT) note_kernel(method == 7 ? "k_march_m7" : "k_march", B, method);
     switch (method) {
     case 1: hipLaunchKernelGGL((k_march<B, 1, COUNT>), grid, block, lds, s, vol, P); break;
     case 2: hipLaunchKernelGGL((k_march<B, 2, COUNT>), grid, block, lds, s, vol, P); break;
