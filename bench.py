@@ -45,6 +45,11 @@ def parse():
     ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 7])
     ap.add_argument("--camera", default="C0", choices=["C0", "C1"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-frame", default="",
+                    help="rank 0 saves the last assembled frame (.npy) for checks")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo stages the tile gather through host memory (multi-rank "
+                         "rehearsal on a single GPU; never for measurement)")
     ap.add_argument("--cpu-row-stride", type=int, default=0,
                     help="CPU baseline renders every k-th row (0 = auto)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -97,10 +102,16 @@ def main():
         if rank == 0:
             print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
                   file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks need {world} GPUs, {ndev} visible")
+    dev = torch.device("cuda", local_rank % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     pkg = graft.load_package()
     n, nb, W, H = CONFIGS[args.config]
@@ -161,10 +172,13 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if args.dump_frame and rank == 0:
+        np.save(args.dump_frame, frame.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
 
     # algorithmic bytes of one launch on this rank: U*S_rec + pixels*4
@@ -209,7 +223,9 @@ def main():
                             f"{args.camera}, queryMethod {args.method}",
                 "volume": [n, n, n], "bins": nb, "image": [W, H], "camera": args.camera,
                 "query_method": args.method, "density": 0.05,
-                "parallelism": f"image tiles x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": f"image tiles x{world}" + (
+                (" + RCCL gather" if args.dist_backend == "nccl" else " + gloo host gather")
+                if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -125,7 +125,11 @@ int vr_set_stream(void *stream);
  * tiles named by d_tile_list (tile id = ty*ceil(width/16) + tx, device array)
  * are rendered into a packed buffer: tile slot s occupies
  * d_output[s*256 .. s*256+255] in row-major 16x16 order.  Entries of
- * 0xFFFFFFFF in the tile list are padding and are skipped.
+ * 0xFFFFFFFF in the tile list are padding and are skipped.  Entry s is
+ * rendered by workgroup s, which runs on XCD s % 8 (each XCD has its own L2):
+ * order the list so every 8th entry forms an equally loaded, spatially
+ * compact set (tiles.py tile_lists does).  Full frames use the library's own
+ * XCD-balanced order.
  * d_output_f (optional) receives the saturated float RGBA of every written
  * pixel, d_steps (optional) the samples taken (-1 for a miss; written for
  * every pixel inside the image). */

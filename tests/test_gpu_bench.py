@@ -1,0 +1,45 @@
+"""bench.py end to end on the GPU: the JSON contract at N = 1, and the N > 1 tile
+path (2 ranks sharing the one GPU, tile gather staged through gloo) assembling
+exactly the single-rank frame."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--config", "256x4", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+
+
+def _run(cmd, tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_single_and_two_rank_frames_agree(gpu, tmp_path):
+    f1 = str(tmp_path / "f1.npy")
+    out1 = _run([sys.executable, "bench.py", *ARGS, "--dump-frame", f1], tmp_path)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in out1, k
+    assert out1["n_gpus"] == 1 and out1["value"] > 0
+    rf = out1["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"].startswith("k_march")
+    f2 = str(tmp_path / "f2.npy")
+    out2 = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                 "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", "29533",
+                 "bench.py", "--gpus", "2", *ARGS, "--dist-backend", "gloo",
+                 "--dump-frame", f2], tmp_path)
+    assert out2["n_gpus"] == 2
+    a, b = np.load(f1), np.load(f2)
+    assert a.shape == (512, 512) and np.count_nonzero(a) > 0
+    assert np.array_equal(a, b), f"{int(np.sum(a != b))} pixels differ between N=1 and N=2"

@@ -99,3 +99,24 @@ def test_gloo_gather_world2(pkg, W, H):
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_lists_match_owner_and_balance_xcds(pkg, world):
+    """list entry s runs on XCD s % 8: every (rank, XCD) pair gets an equal share of
+    the tiles that hit the box at the C0 camera, and lists agree with owner_of"""
+    T = pkg.tiles
+    W, H = 1920, 1080
+    lists = T.tile_lists(W, H, world)
+    own = T.owner_of(W, H, world).reshape(-1)
+    tx = T.tiles_x(W)
+    share = np.zeros((world, T.XCDS))
+    for r in range(world):
+        for s, tile in enumerate(lists[r]):
+            if tile == T.PAD:
+                continue
+            assert own[tile] == r
+            cx = (tile % tx * 16 + 8) / W * 2 - 1
+            cy = (tile // tx * 16 + 8) / H * 2 - 1
+            share[r, s % T.XCDS] += (abs(cx) < 0.6) and (abs(cy) < 0.6)
+    assert share.max() / share.mean() < 1.2, share

@@ -11,6 +11,7 @@ import argparse
 import ctypes
 import glob
 import itertools
+import re
 import os
 import sys
 
@@ -81,7 +82,7 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
     envs = []
     for e in args.env:
         d = {}
-        for kv in filter(None, e.split(",")):
+        for kv in filter(None, re.split(r",(?=[A-Z_]+=)", e)):
             k, v = kv.split("=")
             d[k] = v
         envs.append(d)

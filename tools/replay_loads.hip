@@ -45,19 +45,24 @@ template <int PAT>
 __global__ __launch_bounds__(256) void k_replay(const float *__restrict__ vol, Params P) {
     const uint32_t tile = blockIdx.x;
     const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    uint32_t lx, ly;
+    uint32_t lx, ly, TW = 16, TH = 16;
     if (PAT == 0) { lx = ((wave & 1u) << 3) | (lane & 7u); ly = ((wave >> 1) << 3) | (lane >> 3); }
+    else if (PAT == 3) { lx = lane; ly = wave; TW = 64; TH = 4; }
+    else if (PAT == 4) { lx = lane & 31u; ly = wave * 2 + (lane >> 5); TW = 32; TH = 8; }
+    else if (PAT == 5) { lx = lane & 15u; ly = wave * 4 + (lane >> 4); }
+    else if (PAT == 6) { lx = lane & 31u; ly = wave * 2 + (lane >> 5); TW = 32; TH = 8; }
     else { lx = lane >> 2; ly = wave * 4 + (lane & 3); }
-    const uint32_t x = (tile % P.tiles_x) * 16 + lx, y = (tile / P.tiles_x) * 16 + ly;
+    const uint32_t ntx = (P.W + TW - 1) / TW;
+    const uint32_t x = (tile % ntx) * TW + lx, y = (tile / ntx) * TH + ly;
     float px = 0, py = 0, pz = 0, dx = 0, dy = 0, dz = 0;
     int nsteps = 0;
     const bool hit = x < P.W && y < P.H && ray_of(P, x, y, px, py, pz, dx, dy, dz, nsteps);
-    if (PAT == 0 && !hit) return;
+    if ((PAT == 0 || PAT >= 3) && !hit) return;
     float acc = 0.0f;
     int i = 0;
     while (true) {
         const bool alive = hit && i < nsteps;
-        if (PAT == 0) { if (!alive) break; }
+        if (PAT == 0 || PAT >= 3) { if (!alive) break; }
         else if (__ballot(alive) == 0) break;
         int x0, x1, y0, y1, z0, z1;
         float a;
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(256) void k_replay(const float *__restrict__ vol, P
         lin_axis(qy * 0.5f + 0.5f, P.ny, y0, y1, a);
         lin_axis(qz * 0.5f + 0.5f, P.nz, z0, z1, a);
         float4 r[16];
-        if constexpr (PAT == 0) {
+        if constexpr (PAT == 0 || PAT >= 3) {
             const uint64_t rows[4] = {z0 * P.sz + y0 * P.sy, z0 * P.sz + y1 * P.sy,
                                       z1 * P.sz + y0 * P.sy, z1 * P.sz + y1 * P.sy};
 #pragma unroll
@@ -139,16 +144,19 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char *names[] = {"per-ray", "quad", "quad-contig"};
+    const char *names[] = {"per-ray", "quad", "quad-contig", "per-ray 64x1", "per-ray 32x2", "per-ray 16x4", "32x2 pipelined"};
     for (int cam = 0; cam < 2; cam++) {
         memcpy(P.m, cam ? c1 : c0, sizeof c0);
-        for (int pat = 0; pat < 3; pat++) {
+        for (int pat = 0; pat < 6; pat++) {
             float best = 1e30f;
             for (int rep = 0; rep < 3; rep++) {
                 auto go = [&]() {
                     if (pat == 0) hipLaunchKernelGGL(k_replay<0>, dim3(ntiles), dim3(256), 0, 0, vol, P);
                     if (pat == 1) hipLaunchKernelGGL(k_replay<1>, dim3(ntiles), dim3(256), 0, 0, vol, P);
                     if (pat == 2) hipLaunchKernelGGL(k_replay<2>, dim3(ntiles), dim3(256), 0, 0, vol, P);
+                    if (pat == 3) hipLaunchKernelGGL(k_replay<3>, dim3(30 * 270), dim3(256), 0, 0, vol, P);
+                    if (pat == 4) hipLaunchKernelGGL(k_replay<4>, dim3(60 * 135), dim3(256), 0, 0, vol, P);
+                    if (pat == 5) hipLaunchKernelGGL(k_replay<5>, dim3(ntiles), dim3(256), 0, 0, vol, P);
                 };
                 go();
                 hipEventRecord(e0);

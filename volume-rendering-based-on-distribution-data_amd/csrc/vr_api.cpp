@@ -3,6 +3,7 @@
 // the vr_* extensions).  Never exits; errors go to vr_last_error().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -26,6 +27,10 @@ struct State {
     bool linear_filter = false;     // tex.filterMode = point after initCuda (K:2163)
     std::string err;
     int status = VR_OK;
+    // full-frame workgroup -> tile order (frame_order), cached per frame shape
+    uint32_t *perm = nullptr;
+    uint32_t perm_key[4] = {0, 0, 0, 0};
+    std::vector<uint32_t> perm_host;
 };
 
 State g;
@@ -95,6 +100,58 @@ int check_method(int m) {
     return fail(VR_ERR_ARG, "unknown queryMethod %d", m);
 }
 
+// Full-frame tile order.  Workgroup b runs on XCD b % 8, and each XCD has its
+// own L2.  Tiles are grouped in bx x by blocks (neighbouring tiles share the
+// records along their common edges, so a block keeps that sharing inside one
+// L2); blocks are dealt round-robin to the XCDs along a serpentine walk, which
+// spreads the hit region -- and with it the ray-marching work -- evenly over
+// all eight (a raster split hands the frame's empty top and bottom strips to
+// whole XCDs).  VR_XBLOCK="bx,by" (default 4,4; "0" = plain raster order).
+int frame_order(uint32_t tx, uint32_t ty, const uint32_t *&perm) {
+    uint32_t bx = 4, by = 4;
+    if (const char *e = std::getenv("VR_XBLOCK")) {
+        char *end = nullptr;
+        const long a = std::strtol(e, &end, 10);
+        long b = a;
+        if (end && *end == ',') b = std::strtol(end + 1, nullptr, 10);
+        if (a <= 0 || b <= 0) { perm = nullptr; return VR_OK; }
+        bx = (uint32_t)std::min(a, 64L);
+        by = (uint32_t)std::min(b, 64L);
+    }
+    const uint32_t key[4] = {tx, ty, bx, by};
+    if (g.perm && std::memcmp(key, g.perm_key, sizeof key) == 0) {
+        perm = g.perm;
+        return VR_OK;
+    }
+    const uint32_t nbx = (tx + bx - 1) / bx, nby = (ty + by - 1) / by;
+    std::vector<std::vector<uint32_t>> lists(8);
+    uint32_t j = 0;
+    for (uint32_t byi = 0; byi < nby; byi++) {
+        for (uint32_t k = 0; k < nbx; k++, j++) {
+            const uint32_t bxi = (byi & 1) ? nbx - 1 - k : k;
+            std::vector<uint32_t> &l = lists[j & 7];
+            for (uint32_t y = byi * by; y < std::min(ty, byi * by + by); y++)
+                for (uint32_t x = bxi * bx; x < std::min(tx, bxi * bx + bx); x++)
+                    l.push_back(y * tx + x);
+        }
+    }
+    std::vector<uint32_t> &h = g.perm_host;
+    h.clear();
+    size_t longest = 0;
+    for (auto &l : lists) longest = std::max(longest, l.size());
+    for (size_t i = 0; i < longest; i++)
+        for (auto &l : lists)
+            if (i < l.size()) h.push_back(l[i]);
+    if (g.perm) (void)hipFree(g.perm);
+    g.perm = nullptr;
+    VR_HIP(hipMalloc(&g.perm, h.size() * sizeof(uint32_t)));
+    VR_HIP(hipMemcpyAsync(g.perm, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          g.stream));
+    std::memcpy(g.perm_key, key, sizeof key);
+    perm = g.perm;
+    return VR_OK;
+}
+
 int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     if (!d) return fail(VR_ERR_ARG, "null render descriptor");
     if (!g.vol) return fail(VR_ERR_STATE, "no volume resident (initCuda / vr_init_* first)");
@@ -122,6 +179,11 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     P.nb = g.nb;
     P.tiles_x = tiles_x(d->width);
     P.tile_list = d->d_tile_list;
+    P.perm = nullptr;
+    if (!d->d_tile_list) {
+        int rc = frame_order(tiles_x(d->width), tiles_y(d->height), P.perm);
+        if (rc != VR_OK) return rc;
+    }
     P.out = d->d_output;
     P.out_f = d->d_output_f;
     P.out_n = d->d_steps;
@@ -143,11 +205,11 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     // view): consecutive lanes then read consecutive records.  Otherwise the
     // quad-cooperative gathers (path 0, B == 8) keep every 4-lane group on one
     // contiguous 64-byte run.  VR_PATH overrides: 0 quad, 1 k_march (LDS-staged
-    // box / per-ray), 2 per-ray pipelined.
+    // box / per-ray), 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows.
     P.path = std::fabs(d->inv_view[0]) >= 0.95f ? 2 : 0;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
-        if (v >= 0 && v <= 2) P.path = v;
+        if (v >= 0 && v <= 4) P.path = v;
     }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {
@@ -184,6 +246,13 @@ extern "C" {
 const char *vr_version(void) { return "vrdd-amd 0.1 (gfx950)"; }
 
 const char *vr_last_kernel(void) { return vr::last_march_kernel(); }
+
+#ifdef VR_WG_PROF
+// tooling build only (tools/wg_prof.py): read and reset the phase counters
+int vr_wg_prof_read(unsigned long long *host16) {
+    return vr::wg_prof_read(host16) == hipSuccess ? VR_OK : VR_ERR_HIP;
+}
+#endif
 const char *vr_last_error(void) { return g.err.c_str(); }
 int vr_last_status(void) { return g.status; }
 void vr_clear_error(void) {

@@ -31,6 +31,7 @@ struct Params {
     float enorm;                 // log((float)B)/log(2.0f), K:769
     int nb;                      // bins per record
     uint32_t tiles_x;            // ceil(W/16)
+    const uint32_t *perm;        // full frame: tile of workgroup b (nullptr: xcd_slot order)
     uint32_t n_tiles;            // tiles in this launch
     const uint32_t *tile_list;   // nullptr: tile = launch slot
     uint32_t *out;

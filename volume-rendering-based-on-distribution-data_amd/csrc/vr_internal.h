@@ -26,6 +26,9 @@ hipError_t launch_march(int nb, int method, const float *vol, const Params &P,
                         uint32_t nslots, bool count, hipStream_t s);
 // name of the march kernel the last non-counting launch_march() chose
 const char *last_march_kernel();
+#ifdef VR_WG_PROF
+hipError_t wg_prof_read(unsigned long long *host);   // tooling build only
+#endif
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,
                             uint32_t tiles_x, uint32_t *frame, uint32_t W, uint32_t H,

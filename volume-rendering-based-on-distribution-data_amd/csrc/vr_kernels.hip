@@ -34,6 +34,19 @@ __device__ __forceinline__ uint32_t xcd_slot(uint32_t bid, uint32_t n) {
     return base + i;
 }
 
+// Workgroup b runs on XCD b % 8.  Tile lists (multi-GPU) and the host-built
+// full-frame order P.perm are already XCD-interleaved by their producers
+// (tiles.py / frame_order), so workgroup b takes entry b; without either, the
+// raster order is split into one contiguous run per XCD (xcd_slot).
+__device__ __forceinline__ uint32_t launch_slot(const Params &P) {
+    return (P.tile_list || P.perm) ? blockIdx.x : xcd_slot(blockIdx.x, gridDim.x);
+}
+__device__ __forceinline__ uint32_t tile_of(const Params &P, uint32_t slot) {
+    if (P.tile_list) return P.tile_list[slot];
+    if (P.perm) return P.perm[slot];
+    return slot;
+}
+
 struct Ray {
     float ox, oy, oz, dx, dy, dz, tnear, tfar;
 };
@@ -73,6 +86,16 @@ __device__ __forceinline__ void tile_pixel(uint32_t t, uint32_t &lx, uint32_t &l
     lx = ((wave & 1u) << 3) | (lane & 7u);
     ly = ((wave >> 1) << 3) | (lane >> 3);
 }
+
+// pixel of this thread inside its tile: wave w covers rows 4w .. 4w+3 (16x4)
+__device__ __forceinline__ void tile_pixel_rows(uint32_t t, uint32_t &lx, uint32_t &ly) {
+    lx = t & 15u;
+    ly = t >> 4;
+}
+
+#ifndef VR_PIPE_MAP
+#define VR_PIPE_MAP 1       // k_march_pipe lane->ray map: 0 8x8 blocks, 1 16x4 rows
+#endif
 
 __device__ __forceinline__ void write_pixel(const Params &P, uint64_t o, int n, float r,
                                             float g, float b, float a) {
@@ -149,10 +172,11 @@ __device__ __forceinline__ float blend8(const float (&s)[8], const Foot &f) {
 #define VR_BOX_G 4          // box voxels per lane in flight, staged path
 #endif
 
-// Direct path: each lane gathers and decodes its own 8 corner records.
-template <int B, int M>
-__device__ __forceinline__ float sample_direct(const float *__restrict__ vol, const Params &P,
-                                               const Foot &f) {
+// Direct path: each lane gathers and decodes its own 8 corner records, CGMAX
+// corners in flight.
+template <int B, int M, int CGMAX = VR_DIRECT_CG>
+__device__ __forceinline__ float sample_direct_cg(const float *__restrict__ vol, const Params &P,
+                                                  const Foot &f) {
     const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
     const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
     const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
@@ -162,7 +186,7 @@ __device__ __forceinline__ float sample_direct(const float *__restrict__ vol, co
     float s[8];
     if constexpr (B > 0) {
         constexpr int CG0 = (B >= 64) ? 1 : ((64 / B) > 8 ? 8 : (64 / B));
-        constexpr int CG = CG0 < VR_DIRECT_CG ? CG0 : VR_DIRECT_CG;
+        constexpr int CG = CG0 < CGMAX ? CG0 : CGMAX;
 #pragma unroll
         for (int g = 0; g < 8; g += CG) {
             float rec[CG][B];
@@ -177,6 +201,12 @@ __device__ __forceinline__ float sample_direct(const float *__restrict__ vol, co
             s[j] = record_stat_rt<M>(vol + vidx[j] * (uint64_t)P.nb, P.nb, P.enorm);
     }
     return blend8(s, f);
+}
+
+template <int B, int M>
+__device__ __forceinline__ float sample_direct(const float *__restrict__ vol, const Params &P,
+                                               const Foot &f) {
+    return sample_direct_cg<B, M, VR_DIRECT_CG>(vol, P, f);
 }
 
 __device__ __forceinline__ void mark_foot(const Params &P, const Foot &f) {
@@ -227,8 +257,8 @@ __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, cons
 template <int B, int M, bool COUNT>
 __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Params P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const uint32_t slot = xcd_slot(blockIdx.x, gridDim.x);
-    const uint32_t tile = P.tile_list ? P.tile_list[slot] : slot;
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // whole workgroup uniform
     const uint32_t lane = threadIdx.x & 63u;
     float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
@@ -324,6 +354,481 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
                 sw * P.brightness);
 }
 
+// ---- workgroup-staged march (B <= 8) ----
+// The 256 rays of a tile march in lockstep.  Each step the workgroup builds the
+// exact set of voxel records its live rays' trilinear footprints touch, as
+// x-spans of (y,z) voxel rows: every lane min/max-es its x0/x1 into a row
+// table in LDS (4 rows per lane), the non-empty rows are compacted with a
+// workgroup scan, then 8-lane groups stream the rows from HBM (consecutive
+// lanes on consecutive records), decode each record's statistic ONCE and park
+// it in LDS.  Finally every lane blends its 8 corners from LDS.  Compared with
+// per-lane gathers this loads each record once per tile-step instead of once
+// per touching ray, and keeps the texture-address unit on a few lines per
+// instruction.  A step whose row table or record set does not fit falls back to
+// per-lane gathers (workgroup-uniform).
+constexpr int kWgTbl = 1024;   // (y,z) row-table entries (Y*Z <= kWgTbl)
+#ifdef VR_WG_PROF   // tooling build: per-phase cycle totals of thread 0 (tools/wg_prof.py)
+__device__ unsigned long long g_wg_prof[16];
+#define WG_PROF_T(k) if (tid == 0) { const uint64_t now_ = clock64(); prof_[k] += now_ - tlast_; tlast_ = now_; }
+#define WG_PROF_C(k, v) if (tid == 0) prof_[k] += (uint64_t)(v);
+#else
+#define WG_PROF_T(k)
+#define WG_PROF_C(k, v)
+#endif
+constexpr int kWgRec = 4096;   // staged record statistics per step (< 2^12)
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
+template <int B, int M>
+__global__ __launch_bounds__(256) void k_march_wg(const float *__restrict__ vol, Params P) {
+    __shared__ int s_xmn[kWgTbl], s_xmx[kWgTbl], s_toff[kWgTbl];
+    __shared__ uint2 s_rows[kWgTbl];   // x: ry | rz << 10 | loff << 20,  y: xmin | len << 16
+    __shared__ float s_stat[kWgRec];
+    __shared__ int s_red[4][6];
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;  // whole workgroup uniform
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    for (uint32_t e = tid; e < (uint32_t)kWgTbl; e += 256) {
+        s_xmn[e] = 0x7FFFFFFF;
+        s_xmx[e] = -1;
+    }
+    uint32_t lx, ly;
+    tile_pixel(tid, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    const uint32_t grp = tid >> 3, gl = tid & 7u;
+#ifdef VR_WG_PROF
+    uint64_t prof_[16] = {0};
+    uint64_t tlast_ = clock64();
+#endif
+    for (int i = 0; i < kMaxSteps; i++) {
+        Foot f = {0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0.0f};
+        if (alive) f = footprint(P, px, py, pz);
+        {   // workgroup extent of the live footprints in y and z
+            const int a = wave_min(alive ? f.y0 : 0x7FFFFFFF);
+            const int b = wave_max(alive ? f.y1 : -1);
+            const int c = wave_min(alive ? f.z0 : 0x7FFFFFFF);
+            const int d = wave_max(alive ? f.z1 : -1);
+            if (lane == 0) {
+                s_red[wave][0] = a; s_red[wave][1] = b; s_red[wave][2] = c; s_red[wave][3] = d;
+            }
+        }
+        WG_PROF_T(0)
+        __syncthreads();
+        WG_PROF_T(1)
+        int ymn = s_red[0][0], ymx = s_red[0][1], zmn = s_red[0][2], zmx = s_red[0][3];
+#pragma unroll
+        for (int w = 1; w < 4; w++) {
+            ymn = min(ymn, s_red[w][0]); ymx = max(ymx, s_red[w][1]);
+            zmn = min(zmn, s_red[w][2]); zmx = max(zmx, s_red[w][3]);
+        }
+        if (ymx < 0) break;  // no live ray in the tile
+        const int Y = ymx - ymn + 1, E = Y * (zmx - zmn + 1);
+        bool staged = E <= kWgTbl;
+        float sample = 0.0f;
+        WG_PROF_C(11, 1)
+        if (staged) {
+            const int e00 = (f.y0 - ymn) + Y * (f.z0 - zmn);
+            const int e10 = e00 + (f.y1 - f.y0), e01 = e00 + Y * (f.z1 - f.z0);
+            const int e11 = e01 + (f.y1 - f.y0);
+            if (alive) {
+                atomicMin(&s_xmn[e00], f.x0); atomicMax(&s_xmx[e00], f.x1);
+                atomicMin(&s_xmn[e10], f.x0); atomicMax(&s_xmx[e10], f.x1);
+                atomicMin(&s_xmn[e01], f.x0); atomicMax(&s_xmx[e01], f.x1);
+                atomicMin(&s_xmn[e11], f.x0); atomicMax(&s_xmx[e11], f.x1);
+            }
+            WG_PROF_T(2)
+            __syncthreads();
+            WG_PROF_T(3)
+            // compaction: thread t owns table entries 4t .. 4t+3
+            int mn[4], ln[4], cnt = 0, rec = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int e = 4 * (int)tid + j;
+                ln[j] = 0;
+                mn[j] = 0;
+                if (e < E) {
+                    const int a = s_xmn[e], b = s_xmx[e];
+                    if (b >= a) { mn[j] = a; ln[j] = b - a + 1; cnt++; rec += ln[j]; }
+                    s_xmn[e] = 0x7FFFFFFF;
+                    s_xmx[e] = -1;
+                }
+            }
+            const int icnt = wave_incl_scan(cnt), irec = wave_incl_scan(rec);
+            if (lane == 63) { s_red[wave][4] = icnt; s_red[wave][5] = irec; }
+            WG_PROF_T(4)
+            __syncthreads();
+            WG_PROF_T(5)
+            int rows = 0, recs = 0, rbase = icnt - cnt, obase = irec - rec;
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const int c = s_red[w][4], d = s_red[w][5];
+                if (w < (int)wave) { rbase += c; obase += d; }
+                rows += c;
+                recs += d;
+            }
+            staged = recs <= kWgRec;
+            if (staged) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (ln[j] > 0) {
+                        const int e = 4 * (int)tid + j;
+                        const int rz = e / Y, ry = e - rz * Y;
+                        s_rows[rbase] = make_uint2((uint32_t)ry | ((uint32_t)rz << 10) |
+                                                       ((uint32_t)obase << 20),
+                                                   (uint32_t)mn[j] | ((uint32_t)ln[j] << 16));
+                        s_toff[e] = obase - mn[j];
+                        rbase++;
+                        obase += ln[j];
+                    }
+                }
+                WG_PROF_C(12, 1)
+                WG_PROF_C(13, rows)
+                WG_PROF_C(14, recs)
+            }
+            WG_PROF_T(6)
+            __syncthreads();
+            WG_PROF_T(7)
+            if (staged) {
+                // 8-lane group grp streams rows grp, grp+32, ...; lane gl takes
+                // records gl, gl+8, ... of each row.  4 records in flight per lane.
+                int k = (int)grp, nn = (int)gl;
+                uint64_t gb = 0;
+                int lo = 0, len = 0;
+                if (k < rows) {
+                    const uint2 rw = s_rows[k];
+                    gb = (uint64_t)(zmn + (int)((rw.x >> 10) & 1023u)) * P.sz +
+                         (uint64_t)(ymn + (int)(rw.x & 1023u)) * P.sy + (rw.y & 0xFFFFu);
+                    lo = (int)(rw.x >> 20);
+                    len = (int)(rw.y >> 16);
+                }
+                while (k < rows) {
+                    uint64_t ga[4];
+                    int li[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        while (k < rows && nn >= len) {
+                            k += 32;
+                            nn = (int)gl;
+                            if (k < rows) {
+                                const uint2 rw = s_rows[k];
+                                gb = (uint64_t)(zmn + (int)((rw.x >> 10) & 1023u)) * P.sz +
+                                     (uint64_t)(ymn + (int)(rw.x & 1023u)) * P.sy +
+                                     (rw.y & 0xFFFFu);
+                                lo = (int)(rw.x >> 20);
+                                len = (int)(rw.y >> 16);
+                            }
+                        }
+                        if (k < rows) {
+                            ga[u] = gb + (uint64_t)nn;
+                            li[u] = lo + nn;
+                            nn += 8;
+                        } else {
+                            ga[u] = 0;
+                            li[u] = -1;
+                        }
+                    }
+                    float rr[4][B];
+                    WG_PROF_C(15, 1)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) load_rec<B>(vol, ga[u], rr[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (li[u] >= 0) s_stat[li[u]] = record_stat<B, M>(rr[u], P.enorm);
+                }
+            }
+            WG_PROF_T(8)
+            __syncthreads();
+            WG_PROF_T(9)
+            if (staged && alive) {
+                const int t00 = s_toff[e00], t10 = s_toff[e10];
+                const int t01 = s_toff[e01], t11 = s_toff[e11];
+                float sv[8];
+                sv[0] = s_stat[t00 + f.x0]; sv[1] = s_stat[t00 + f.x1];
+                sv[2] = s_stat[t10 + f.x0]; sv[3] = s_stat[t10 + f.x1];
+                sv[4] = s_stat[t01 + f.x0]; sv[5] = s_stat[t01 + f.x1];
+                sv[6] = s_stat[t11 + f.x0]; sv[7] = s_stat[t11 + f.x1];
+                sample = blend8(sv, f);
+            }
+        }
+        if (alive) {
+            if (!staged) sample = sample_direct<B, M>(vol, P, f);
+            n = i + 1;
+            if (composite(P, sample, sx, sy, sz, sw)) {
+                alive = false;
+            } else {
+                t = t + kTStep;
+                if (t > r.tfar) {
+                    alive = false;
+                } else {
+                    px = px + stx;
+                    py = py + sty;
+                    pz = pz + stz;
+                }
+            }
+        }
+        WG_PROF_T(10)
+    }
+#ifdef VR_WG_PROF
+    if (tid == 0)
+        for (int k = 0; k < 16; k++) atomicAdd(&g_wg_prof[k], prof_[k]);
+#endif
+    if (!valid) return;
+    if (n == 0) {  // miss (K:302-303): nothing written
+        if (P.out_n) P.out_n[o] = -1;
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
+#ifdef VR_WG_PROF
+hipError_t wg_prof_read(unsigned long long *host) {
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_prof), sizeof(g_wg_prof));
+    if (e != hipSuccess) return e;
+    static const unsigned long long zero[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wg_prof), zero, sizeof(zero));
+}
+#endif
+
+// ---- wave-staged march (B <= 8) ----
+// The same exact-footprint staging as k_march_wg, but per wave (8x8 rays) and
+// wave-synchronous: no workgroup barriers, so the 16-20 resident waves of a CU
+// hide each other's HBM latency.  Per step: (y,z) row table by LDS atomics,
+// compaction by DPP scans, row-start marks + a max-scan give every lane its
+// (row, x) for consecutive records, so consecutive lanes load consecutive
+// records (coalesced), each record's statistic is decoded once and parked in
+// LDS, and every lane blends its 8 corners from there.
+constexpr int kWsTbl = 256;   // (y,z) row-table entries per wave (4 per lane)
+constexpr int kWsRows = 128;  // compacted rows per wave-step
+constexpr int kWsRec = 512;   // staged record statistics per wave-step
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int wave_incl_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xA, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+
+#ifndef VR_WS_WAVES
+#define VR_WS_WAVES 4       // waves per SIMD the wave-staged kernel is register-capped for
+#endif
+
+template <int B, int M>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES, 8))) void k_march_ws(const float *__restrict__ vol, Params P) {
+    __shared__ int s_xmn[4][kWsTbl], s_xmx[4][kWsTbl], s_toff[4][kWsTbl];
+    __shared__ uint2 s_rows[4][kWsRows];  // x: ry | rz << 10 | loff << 20,  y: xmin
+    __shared__ int s_mark[4][kWsRec];
+    __shared__ float s_stat[4][kWsRec];
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;  // whole workgroup uniform
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    int *xmn = s_xmn[wave], *xmx = s_xmx[wave], *toff = s_toff[wave], *mark = s_mark[wave];
+    uint2 *rowv = s_rows[wave];
+    float *stat = s_stat[wave];
+    for (uint32_t e = lane; e < (uint32_t)kWsTbl; e += 64) {
+        xmn[e] = 0x7FFFFFFF;
+        xmx[e] = -1;
+    }
+    for (uint32_t q = lane; q < (uint32_t)kWsRec; q += 64) mark[q] = -1;
+    wave_sync();
+    uint32_t lx, ly;
+    tile_pixel(tid, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+#ifdef VR_WG_PROF
+    uint64_t prof_[16] = {0};
+    uint64_t tlast_ = clock64();
+#endif
+    for (int i = 0; i < kMaxSteps; i++) {
+        if (!wave_any(alive)) break;
+        Foot f = {0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0.0f};
+        if (alive) f = footprint(P, px, py, pz);
+        const int ymn = wave_min(alive ? f.y0 : 0x7FFFFFFF);
+        const int ymx = wave_max(alive ? f.y1 : -1);
+        const int zmn = wave_min(alive ? f.z0 : 0x7FFFFFFF);
+        const int zmx = wave_max(alive ? f.z1 : -1);
+        const int Y = ymx - ymn + 1, E = Y * (zmx - zmn + 1);
+        bool staged = E <= kWsTbl;
+        float sample = 0.0f;
+        WG_PROF_C(11, 1)
+        WG_PROF_C(6, E > kWsTbl)
+        WG_PROF_T(0)
+        if (staged) {
+            const int e00 = (f.y0 - ymn) + Y * (f.z0 - zmn);
+            const int e10 = e00 + (f.y1 - f.y0), e01 = e00 + Y * (f.z1 - f.z0);
+            const int e11 = e01 + (f.y1 - f.y0);
+            if (alive) {
+                atomicMin(&xmn[e00], f.x0); atomicMax(&xmx[e00], f.x1);
+                atomicMin(&xmn[e10], f.x0); atomicMax(&xmx[e10], f.x1);
+                atomicMin(&xmn[e01], f.x0); atomicMax(&xmx[e01], f.x1);
+                atomicMin(&xmn[e11], f.x0); atomicMax(&xmx[e11], f.x1);
+            }
+            wave_sync();
+            WG_PROF_T(2)
+            // compaction: lane owns table entries 4*lane .. 4*lane+3 (and resets them)
+            int mn[4], ln[4], cnt = 0, rec = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int e = 4 * (int)lane + j;
+                ln[j] = 0;
+                mn[j] = 0;
+                if (e < E) {
+                    const int a = xmn[e], b = xmx[e];
+                    if (b >= a) { mn[j] = a; ln[j] = b - a + 1; cnt++; rec += ln[j]; }
+                    xmn[e] = 0x7FFFFFFF;
+                    xmx[e] = -1;
+                }
+            }
+            const int icnt = wave_incl_scan(cnt), irec = wave_incl_scan(rec);
+            const int rows = __builtin_amdgcn_readlane(icnt, 63);
+            const int R = __builtin_amdgcn_readlane(irec, 63);
+            staged = rows <= kWsRows && R <= kWsRec;
+            WG_PROF_C(7, rows > kWsRows)
+            WG_PROF_C(8, R > kWsRec)
+            WG_PROF_T(4)
+            if (staged) {
+                WG_PROF_C(12, 1)
+                WG_PROF_C(13, rows)
+                WG_PROF_C(14, R)
+                // row-start marks carry the step as a tag: stale marks never match
+                const float rY = 1.0f / (float)Y;
+                int rb = icnt - cnt, ob = irec - rec;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (ln[j] > 0) {
+                        const int e = 4 * (int)lane + j;
+                        const int rz = (int)(((float)e + 0.5f) * rY), ry = e - rz * Y;
+                        rowv[rb] = make_uint2((uint32_t)ry | ((uint32_t)rz << 10) |
+                                                  ((uint32_t)ob << 20),
+                                              (uint32_t)mn[j]);
+                        toff[e] = ob - mn[j];
+                        mark[ob] = (i << 8) | rb;
+                        rb++;
+                        ob += ln[j];
+                    }
+                }
+                wave_sync();
+                WG_PROF_T(5)
+                // consecutive lanes on consecutive records; 4 x 64 records in flight
+                int carry = -1;
+                for (int q0 = 0; q0 < R; q0 += 256) {
+                    float rr[4][B];
+                    int li[4];
+                    WG_PROF_C(15, 1)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int q = q0 + 64 * u + (int)lane;
+                        uint64_t ga = 0;
+                        li[u] = -1;
+                        if (q0 + 64 * u < R) {  // wave-uniform
+                            int m = -1;
+                            if (q < R) {
+                                const int v = mark[q];
+                                if ((v >> 8) == i) m = v & 255;
+                            }
+                            m = max(wave_incl_max(m), carry);
+                            carry = __builtin_amdgcn_readlane(m, 63);
+                            if (q < R) {
+                                const uint2 rw = rowv[m];
+                                const int lo = (int)(rw.x >> 20);
+                                ga = (uint64_t)(zmn + (int)((rw.x >> 10) & 1023u)) * P.sz +
+                                     (uint64_t)(ymn + (int)(rw.x & 1023u)) * P.sy +
+                                     (uint64_t)(rw.y + (uint32_t)(q - lo));
+                                li[u] = q;
+                            }
+                        }
+                        load_rec<B>(vol, ga, rr[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (li[u] >= 0) stat[li[u]] = record_stat<B, M>(rr[u], P.enorm);
+                }
+                wave_sync();
+                WG_PROF_T(9)
+                if (alive) {
+                    const int t00 = toff[e00], t10 = toff[e10];
+                    const int t01 = toff[e01], t11 = toff[e11];
+                    float sv[8];
+                    sv[0] = stat[t00 + f.x0]; sv[1] = stat[t00 + f.x1];
+                    sv[2] = stat[t10 + f.x0]; sv[3] = stat[t10 + f.x1];
+                    sv[4] = stat[t01 + f.x0]; sv[5] = stat[t01 + f.x1];
+                    sv[6] = stat[t11 + f.x0]; sv[7] = stat[t11 + f.x1];
+                    sample = blend8(sv, f);
+                }
+                wave_sync();
+            }
+        }
+        if (alive) {
+            if (!staged) sample = sample_direct_cg<B, M, 2>(vol, P, f);
+            n = i + 1;
+            if (composite(P, sample, sx, sy, sz, sw)) {
+                alive = false;
+            } else {
+                t = t + kTStep;
+                if (t > r.tfar) {
+                    alive = false;
+                } else {
+                    px = px + stx;
+                    py = py + sty;
+                    pz = pz + stz;
+                }
+            }
+        }
+        WG_PROF_T(10)
+    }
+#ifdef VR_WG_PROF
+    if (tid == 0)
+        for (int k = 0; k < 16; k++) atomicAdd(&g_wg_prof[k], prof_[k]);
+#endif
+    if (!valid) return;
+    if (n == 0) {  // miss (K:302-303): nothing written
+        if (P.out_n) P.out_n[o] = -1;
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 // ---- software-pipelined march (B <= 8) ----
 // Same arithmetic as k_march's direct path, but the 8 corner records of step
 // i+1 are gathered into a second register set BEFORE step i is decoded, so
@@ -359,11 +864,12 @@ __device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][
 
 template <int B, int M>
 __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vol, Params P) {
-    const uint32_t slot = xcd_slot(blockIdx.x, gridDim.x);
-    const uint32_t tile = P.tile_list ? P.tile_list[slot] : slot;
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
     uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
+    if (VR_PIPE_MAP == 1) tile_pixel_rows(threadIdx.x, lx, ly);
+    else tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTile + lx;
     const uint32_t y = (tile / P.tiles_x) * kTile + ly;
     if (x >= P.W || y >= P.H) return;  // no cross-lane work in this kernel
@@ -542,8 +1048,8 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
 
 template <int M>
 __global__ __launch_bounds__(256) void k_march_quad(const float *__restrict__ vol, Params P) {
-    const uint32_t slot = xcd_slot(blockIdx.x, gridDim.x);
-    const uint32_t tile = P.tile_list ? P.tile_list[slot] : slot;
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // uniform per workgroup
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 2, g = lane & 3u;
@@ -644,8 +1150,8 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
 
 template <int B>
 __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol, Params P) {
-    const uint32_t slot = xcd_slot(blockIdx.x, gridDim.x);
-    const uint32_t tile = P.tile_list ? P.tile_list[slot] : slot;
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
     uint32_t lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
@@ -785,6 +1291,24 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             case 1: hipLaunchKernelGGL((k_march_quad<1>), grid, block, 0, s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_quad<2>), grid, block, 0, s, vol, P); break;
             case 3: hipLaunchKernelGGL((k_march_quad<3>), grid, block, 0, s, vol, P); break;
+            }
+            return hipGetLastError();
+        }
+        if (P.path == 3 && method >= 1 && method <= 3) {
+            note_kernel("k_march_wg", B, method);
+            switch (method) {
+            case 1: hipLaunchKernelGGL((k_march_wg<B, 1>), grid, block, 0, s, vol, P); break;
+            case 2: hipLaunchKernelGGL((k_march_wg<B, 2>), grid, block, 0, s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_wg<B, 3>), grid, block, 0, s, vol, P); break;
+            }
+            return hipGetLastError();
+        }
+        if (P.path == 4 && method >= 1 && method <= 3) {
+            note_kernel("k_march_ws", B, method);
+            switch (method) {
+            case 1: hipLaunchKernelGGL((k_march_ws<B, 1>), grid, block, 0, s, vol, P); break;
+            case 2: hipLaunchKernelGGL((k_march_ws<B, 2>), grid, block, 0, s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_ws<B, 3>), grid, block, 0, s, vol, P); break;
             }
             return hipGetLastError();
         }

@@ -12,6 +12,13 @@ Tiles are the 16x16-pixel tiles of the march kernel.  They are grouped in
 the same number of blocks (+-1) spread over the whole image: only ~45 % of the
 pixels hit the volume at the reference camera, so contiguous bands would be
 badly unbalanced.
+
+Inside a rank the list order matters too: workgroup s of the launch renders
+list entry s and runs on XCD s % 8, each XCD with its own L2.  The rank's
+blocks are therefore dealt round-robin to the 8 XCDs along its serpentine
+order and the list interleaves them (entry 8*i + g = i-th tile of XCD g), so
+every XCD gets an equal, frame-wide share of the work while the 4 tiles of a
+block -- which share footprint records -- stay in one L2.
 """
 from __future__ import annotations
 
@@ -20,6 +27,7 @@ import numpy as np
 TILE = 16
 PAD = 0xFFFFFFFF
 BLOCK = 2  # tiles per block edge
+XCDS = 8   # MI355X accelerator complex dies (workgroup b runs on XCD b % 8)
 
 
 def tiles_x(width: int) -> int:
@@ -41,10 +49,27 @@ def owner_of(width: int, height: int, world_size: int) -> np.ndarray:
 
 
 def tile_lists(width: int, height: int, world_size: int) -> np.ndarray:
-    """(world_size, n_slots) uint32 tile ids (row-major order per rank), PAD-padded
-    to the longest list so every rank gathers the same number of bytes."""
-    own = owner_of(width, height, world_size).reshape(-1)
-    ids = [np.nonzero(own == r)[0].astype(np.uint32) for r in range(world_size)]
+    """(world_size, n_slots) uint32 tile ids, XCD-interleaved per rank (module
+    docstring), PAD-padded to the longest list so every rank gathers the same
+    number of bytes."""
+    tx, ty = tiles_x(width), tiles_y(height)
+    nbx, nby = (tx + BLOCK - 1) // BLOCK, (ty + BLOCK - 1) // BLOCK
+    per_rank = [[[] for _ in range(XCDS)] for _ in range(world_size)]
+    j = 0
+    for by in range(nby):
+        for k in range(nbx):
+            bx = k if by % 2 == 0 else nbx - 1 - k
+            r, q = j % world_size, j // world_size   # q-th block of rank r
+            j += 1
+            lst = per_rank[r][q % XCDS]
+            for y in range(by * BLOCK, min(ty, by * BLOCK + BLOCK)):
+                for x in range(bx * BLOCK, min(tx, bx * BLOCK + BLOCK)):
+                    lst.append(y * tx + x)
+    ids = []
+    for subs in per_rank:
+        longest = max((len(l) for l in subs), default=0)
+        ids.append(np.array([l[i] for i in range(longest) for l in subs if i < len(l)],
+                            dtype=np.uint32))
     n_slots = max((len(i) for i in ids), default=0)
     out = np.full((world_size, n_slots), PAD, dtype=np.uint32)
     for r, i in enumerate(ids):
@@ -64,6 +89,10 @@ def gather_packed(packed, world_size: int, rank: int, group=None):
 
     if world_size == 1:
         return packed.view(1, -1)
+    if packed.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device gather: stage through host memory (tests only)
+        host = gather_packed(packed.cpu(), world_size, rank, group)
+        return None if host is None else host.to(packed.device)
     recv = None
     if rank == 0:
         recv = torch.empty((world_size,) + tuple(packed.shape), dtype=packed.dtype,
