@@ -40,7 +40,7 @@ typedef struct { float x, y; } vr_float2;                     /* == float2     *
  * caller-owned device buffer d_output (imageW*imageH packed RGBA8, row-major,
  * A<<24|B<<16|G<<8|R).  Miss pixels are not written (caller zeroes, C:208).
  * gridSize/blockSize are accepted for ABI compatibility; the library picks its
- * own gfx950 launch geometry (16x16-pixel tiles, one 8x8 ray block per wave).
+ * own gfx950 launch geometry (64x4-pixel tiles, one 64-pixel row per wave).
  * volumeSize is used exactly where the reference uses it: the method-7 corner
  * grid (K:322-352).  queryMethod: 1 mean, 2 variance, 3 entropy,
  * 7 software-interpolated mean.  4/5/6 and 8/9/0 need the fractal codec and
@@ -121,10 +121,10 @@ int vr_volume_layout(size_t *row_pitch, size_t *slice_pitch);
 int vr_set_stream(void *stream);
 
 /* Explicit-parameter render.  With d_tile_list == NULL the whole frame is
- * rendered into d_output[y*width + x].  Otherwise the n_tiles 16x16-pixel
- * tiles named by d_tile_list (tile id = ty*ceil(width/16) + tx, device array)
+ * rendered into d_output[y*width + x].  Otherwise the n_tiles 64x4-pixel
+ * tiles named by d_tile_list (tile id = ty*ceil(width/64) + tx, device array)
  * are rendered into a packed buffer: tile slot s occupies
- * d_output[s*256 .. s*256+255] in row-major 16x16 order.  Entries of
+ * d_output[s*256 .. s*256+255] in row-major 64x4 order.  Entries of
  * 0xFFFFFFFF in the tile list are padding and are skipped.  Entry s is
  * rendered by workgroup s, which runs on XCD s % 8 (each XCD has its own L2):
  * order the list so every 8th entry forms an equally loaded, spatially
@@ -161,7 +161,7 @@ int vr_unscatter_tiles(const uint32_t *d_packed, const uint32_t *d_tile_lists,
                        uint32_t n_ranks, uint32_t n_slots, uint32_t *d_frame,
                        uint32_t width, uint32_t height);
 
-/* number of 16x16 tiles of a width x height frame */
+/* tiles (64 wide, 4 high) across / down a width x height frame */
 uint32_t vr_tiles_x(uint32_t width);
 uint32_t vr_tiles_y(uint32_t height);
 

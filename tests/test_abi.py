@@ -65,5 +65,6 @@ def test_errors_without_gpu(pkg):
     with pytest.raises(pkg.VRError):
         pkg.copyInvViewMatrix(np.zeros(16, np.float32), 64)            # > 48 bytes
     pkg.setTextureFilterMode(True)  # stored only
-    assert pkg._lib.load().vr_tiles_x(1920) == 120 and pkg._lib.load().vr_tiles_y(1080) == 68
+    assert pkg._lib.load().vr_tiles_x(1920) == pkg.tiles.tiles_x(1920) == 30
+    assert pkg._lib.load().vr_tiles_y(1080) == pkg.tiles.tiles_y(1080) == 270
     assert "gfx950" in pkg.version()

@@ -26,7 +26,8 @@ def test_partition_covers_each_tile_once(pkg, W, H, world):
     ntiles = T.tiles_x(W) * T.tiles_y(H)
     assert sorted(real.tolist()) == list(range(ntiles))
     counts = (lists != T.PAD).sum(1)
-    assert counts.max() - counts.min() <= 4 + T.tiles_x(W) // 2  # +-1 block (+ ragged edge)
+    # +-1 block (+ ragged edge)
+    assert counts.max() - counts.min() <= T.BLOCK_X * T.BLOCK_Y + T.tiles_x(W) * T.BLOCK_Y // 2
 
 
 def test_partition_spreads_the_hit_region(pkg):
@@ -34,8 +35,8 @@ def test_partition_spreads_the_hit_region(pkg):
     T = pkg.tiles
     own = T.owner_of(1920, 1080, 8)
     ty, tx = np.mgrid[0:own.shape[0], 0:own.shape[1]]
-    cx = (tx * 16 + 8) / 1920 * 2 - 1
-    cy = (ty * 16 + 8) / 1080 * 2 - 1
+    cx = (tx * T.TILE_W + T.TILE_W / 2) / 1920 * 2 - 1
+    cy = (ty * T.TILE_H + T.TILE_H / 2) / 1080 * 2 - 1
     hit = (np.abs(cx) < 0.5) & (np.abs(cy) < 0.5)  # ~ the box's screen footprint
     per_rank = np.bincount(own[hit], minlength=8)
     assert per_rank.max() / per_rank.mean() < 1.1
@@ -49,8 +50,8 @@ def _unscatter_np(gathered, lists, W, H, T):
             if tile == T.PAD:
                 continue
             for i in range(256):
-                px = (tile % tx) * 16 + (i & 15)
-                py = (tile // tx) * 16 + (i >> 4)
+                px = (tile % tx) * T.TILE_W + i % T.TILE_W
+                py = (tile // tx) * T.TILE_H + i // T.TILE_W
                 if px < W and py < H:
                     frame[py * W + px] = gathered[r, s * 256 + i]
     return frame
@@ -75,7 +76,8 @@ def _worker(rank, world, port, W, H, q):
         if tile == T.PAD:
             continue
         for i in range(256):
-            px, py = (tile % tx) * 16 + (i & 15), (tile // tx) * 16 + (i >> 4)
+            px = (tile % tx) * T.TILE_W + i % T.TILE_W
+            py = (tile // tx) * T.TILE_H + i // T.TILE_W
             if px < W and py < H:
                 packed[s * 256 + i] = frame[py * W + px]
     t = torch.from_numpy(packed.view(np.int32).copy())
@@ -116,7 +118,7 @@ def test_lists_match_owner_and_balance_xcds(pkg, world):
             if tile == T.PAD:
                 continue
             assert own[tile] == r
-            cx = (tile % tx * 16 + 8) / W * 2 - 1
-            cy = (tile // tx * 16 + 8) / H * 2 - 1
+            cx = (tile % tx * T.TILE_W + T.TILE_W / 2) / W * 2 - 1
+            cy = (tile // tx * T.TILE_H + T.TILE_H / 2) / H * 2 - 1
             share[r, s % T.XCDS] += (abs(cx) < 0.6) and (abs(cy) < 0.6)
     assert share.max() / share.mean() < 1.2, share

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Copy a gpu_round.sh run (gpurun_out/<TAG>) into profiles/<DEST> and refresh
+# profiles/traffic.json.  usage: tools/collect_profiles.sh TAG DEST
+set -e
+cd "$(dirname "$0")/.."
+R=gpurun_out/$1; D=profiles/$2
+mkdir -p $D/pmc
+for c in C0 C1; do
+  cp $R/ktrace/${c}_kernel_stats.csv $D/kernel_stats_1024x8_$c.csv
+  grep '^{' $R/bench_1024x8_$c.log > $D/bench_1024x8_$c.json
+  for p in 1 2 3; do cp $R/pmc_$c/p$p/p${p}_counter_collection.csv $D/pmc/${c}_p$p.csv; done
+done
+[ -f $R/pytest_gpu.log ] && cp $R/pytest_gpu.log $D/pytest_gpu.log
+cp $R/traffic.json profiles/traffic.json
+ls $D

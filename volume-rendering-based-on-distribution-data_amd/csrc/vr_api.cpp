@@ -86,8 +86,8 @@ float entropy_norm(int nb) {
     return a / b;
 }
 
-uint32_t tiles_x(uint32_t w) { return (w + vr::kTile - 1) / vr::kTile; }
-uint32_t tiles_y(uint32_t h) { return (h + vr::kTile - 1) / vr::kTile; }
+uint32_t tiles_x(uint32_t w) { return (w + vr::kTileW - 1) / vr::kTileW; }
+uint32_t tiles_y(uint32_t h) { return (h + vr::kTileH - 1) / vr::kTileH; }
 
 int check_method(int m) {
     if (m == 1 || m == 2 || m == 3 || m == 7) return VR_OK;
@@ -103,12 +103,14 @@ int check_method(int m) {
 // Full-frame tile order.  Workgroup b runs on XCD b % 8, and each XCD has its
 // own L2.  Tiles are grouped in bx x by blocks (neighbouring tiles share the
 // records along their common edges, so a block keeps that sharing inside one
-// L2); blocks are dealt round-robin to the XCDs along a serpentine walk, which
-// spreads the hit region -- and with it the ray-marching work -- evenly over
-// all eight (a raster split hands the frame's empty top and bottom strips to
-// whole XCDs).  VR_XBLOCK="bx,by" (default 4,4; "0" = plain raster order).
+// L2); block (i, j) goes to XCD (i + 3 j) % 8, a diagonal lattice that gives
+// every XCD an evenly spread eighth of any region spanning a few blocks -- so
+// the hit region, and with it the ray-marching work, is split evenly (a raster
+// split hands the frame's empty top and bottom strips to whole XCDs).  Each
+// XCD walks its blocks row by row.  VR_XBLOCK="bx,by" (default 1,4 = 64x16
+// pixels; "0" = plain raster order).
 int frame_order(uint32_t tx, uint32_t ty, const uint32_t *&perm) {
-    uint32_t bx = 4, by = 4;
+    uint32_t bx = 1, by = 4;
     if (const char *e = std::getenv("VR_XBLOCK")) {
         char *end = nullptr;
         const long a = std::strtol(e, &end, 10);
@@ -125,11 +127,9 @@ int frame_order(uint32_t tx, uint32_t ty, const uint32_t *&perm) {
     }
     const uint32_t nbx = (tx + bx - 1) / bx, nby = (ty + by - 1) / by;
     std::vector<std::vector<uint32_t>> lists(8);
-    uint32_t j = 0;
     for (uint32_t byi = 0; byi < nby; byi++) {
-        for (uint32_t k = 0; k < nbx; k++, j++) {
-            const uint32_t bxi = (byi & 1) ? nbx - 1 - k : k;
-            std::vector<uint32_t> &l = lists[j & 7];
+        for (uint32_t bxi = 0; bxi < nbx; bxi++) {
+            std::vector<uint32_t> &l = lists[(bxi + 3 * byi) & 7];
             for (uint32_t y = byi * by; y < std::min(ty, byi * by + by); y++)
                 for (uint32_t x = bxi * bx; x < std::min(tx, bxi * bx + bx); x++)
                     l.push_back(y * tx + x);

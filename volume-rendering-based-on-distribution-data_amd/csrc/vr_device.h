@@ -18,7 +18,8 @@ namespace vr {
 constexpr int kMaxSteps = 500;             // K:276
 constexpr float kTStep = 0.01f;            // K:277
 constexpr float kOpacityThreshold = 0.95f; // K:278
-constexpr int kTile = 16;                  // pixels per tile edge
+constexpr int kTileW = 64;                 // tile = one 256-thread workgroup:
+constexpr int kTileH = 4;                  //   64 x 4 pixels, one row per wave
 constexpr uint32_t kPad = 0xFFFFFFFFu;     // tile-list padding
 
 struct Params {

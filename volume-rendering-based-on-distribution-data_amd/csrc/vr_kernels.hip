@@ -2,7 +2,7 @@
 //
 //  k_march<B, M, COUNT>  the d_render per-ray march (K:272-717) for methods
 //                        1/2/3: one lane per ray, one 8x8 ray block per wave,
-//                        one 16x16-pixel tile per 256-thread workgroup,
+//                        one 64x4-pixel tile per 256-thread workgroup,
 //                        XCD-aware tile order.  Per step the statistic is
 //                        decoded from the 8 corner distribution records and
 //                        blended with 8-bit filter weights; when the wave's
@@ -80,22 +80,18 @@ __device__ __forceinline__ void mark_voxel(unsigned long long *mark, uint64_t id
     atomicOr(mark + (idx >> 6), 1ull << (idx & 63));
 }
 
-// pixel of this thread inside its tile: wave w covers the 8x8 quadrant w
+// Pixel of this thread inside its tile: wave w renders tile row w, lane = x.
+// Wide, short tiles: a footprint row of records is x-contiguous, so a tile edge
+// along y (left/right neighbour) splits every 128-B line of the rows it
+// crosses between two workgroups, while an edge along x costs only the records
+// of one voxel row.  64x4 tiles fetch 12 % fewer lines per frame than 16x16
+// (tools/footprint_sim.c, C0 at 1024^3 x 8) and each wave's gathers cover one
+// contiguous x run.
+static_assert(kTileW == 64 && kTileH * kTileW == 256, "one wave per 64-pixel tile row");
 __device__ __forceinline__ void tile_pixel(uint32_t t, uint32_t &lx, uint32_t &ly) {
-    const uint32_t wave = t >> 6, lane = t & 63;
-    lx = ((wave & 1u) << 3) | (lane & 7u);
-    ly = ((wave >> 1) << 3) | (lane >> 3);
+    lx = t & (kTileW - 1);
+    ly = t / kTileW;
 }
-
-// pixel of this thread inside its tile: wave w covers rows 4w .. 4w+3 (16x4)
-__device__ __forceinline__ void tile_pixel_rows(uint32_t t, uint32_t &lx, uint32_t &ly) {
-    lx = t & 15u;
-    ly = t >> 4;
-}
-
-#ifndef VR_PIPE_MAP
-#define VR_PIPE_MAP 1       // k_march_pipe lane->ray map: 0 8x8 blocks, 1 16x4 rows
-#endif
 
 __device__ __forceinline__ void write_pixel(const Params &P, uint64_t o, int n, float r,
                                             float g, float b, float a) {
@@ -264,10 +260,10 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
     float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
     uint32_t lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.W && y < P.H;
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     // every lane stays to the end: the staged decode needs all 64 lanes
     Ray r;
@@ -403,10 +399,10 @@ __global__ __launch_bounds__(256) void k_march_wg(const float *__restrict__ vol,
     }
     uint32_t lx, ly;
     tile_pixel(tid, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.W && y < P.H;
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
     bool alive = valid && make_ray(P, x, y, r);
@@ -663,10 +659,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
     wave_sync();
     uint32_t lx, ly;
     tile_pixel(tid, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.W && y < P.H;
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
     bool alive = valid && make_ray(P, x, y, r);
@@ -868,12 +864,11 @@ __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vo
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
     uint32_t lx, ly;
-    if (VR_PIPE_MAP == 1) tile_pixel_rows(threadIdx.x, lx, ly);
-    else tile_pixel(threadIdx.x, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.W || y >= P.H) return;  // no cross-lane work in this kernel
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
     if (!make_ray(P, x, y, r)) {
@@ -922,7 +917,8 @@ __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vo
 
 // ---- quad-cooperative pipelined march (B == 8) ----
 // Lane l = 4q + g of a wave is the home of the ray at pixel (q, g) of the
-// wave's 16x4 pixel block (the 4 waves of a workgroup stack to 16x16).  For
+// wave's 16x4 pixel block (the 4 waves of a workgroup sit side by side in the
+// 64x4 tile).  For
 // the gathers the four lanes of quad q work for ray (G, q), G = 0..3 in turn:
 // per (y,z) corner combo they read that ray's x0/x1 record pair as ONE
 // contiguous 64-byte run (lane g takes 16-byte chunk g), so every 4-lane group
@@ -1053,11 +1049,11 @@ __global__ __launch_bounds__(256) void k_march_quad(const float *__restrict__ vo
     if (tile == kPad) return;  // uniform per workgroup
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 2, g = lane & 3u;
-    const uint32_t lx = q, ly = wave * 4u + g;  // 16x4 block per wave
-    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const uint32_t lx = wave * 16u + q, ly = g;  // 16x4 block per wave, quad = a column
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.W && y < P.H;
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     // every lane stays to the end: quads cooperate on each other's rays
     Ray r;
@@ -1155,10 +1151,10 @@ __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol,
     if (tile == kPad) return;
     uint32_t lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTile + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTile + ly;
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.W || y >= P.H) return;
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * 16u + lx
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
     if (!make_ray(P, x, y, r)) {
@@ -1248,8 +1244,8 @@ __global__ __launch_bounds__(256) void k_unscatter(const uint32_t *__restrict__ 
                                                    uint32_t W, uint32_t H) {
     const uint32_t tile = lists[blockIdx.x];
     if (tile == kPad) return;
-    const uint32_t px = (tile % tiles_x) * kTile + (threadIdx.x & 15u);
-    const uint32_t py = (tile / tiles_x) * kTile + (threadIdx.x >> 4);
+    const uint32_t px = (tile % tiles_x) * kTileW + (threadIdx.x & (kTileW - 1));
+    const uint32_t py = (tile / tiles_x) * kTileH + threadIdx.x / kTileW;
     if (px >= W || py >= H) return;
     frame[(uint64_t)py * W + px] = packed[(uint64_t)blockIdx.x * 256u + threadIdx.x];
 }

@@ -6,46 +6,61 @@ inside 288 GB of HBM) and ray-casts only its own tiles.  Rays are independent
 volume), so the one exchange per frame is gathering the finished tiles to
 rank 0 (an RCCL gather over xGMI when the process group is NCCL/RCCL).
 
-Tiles are the 16x16-pixel tiles of the march kernel.  They are grouped in
-2x2-tile blocks (32x32 px); the blocks are enumerated along a serpentine
-(boustrophedon) path over the image and dealt round-robin, so every rank gets
-the same number of blocks (+-1) spread over the whole image: only ~45 % of the
-pixels hit the volume at the reference camera, so contiguous bands would be
-badly unbalanced.
+Tiles are the 64x4-pixel tiles of the march kernel (one 256-thread
+workgroup).  They are grouped in 1x4-tile blocks (64x16 px) which are dealt
+to the ranks along a diagonal lattice (below), so every rank gets about the
+same number of blocks spread over the whole image: only ~45 % of the pixels
+hit the volume at the reference camera, so contiguous bands would be badly
+unbalanced.
 
 Inside a rank the list order matters too: workgroup s of the launch renders
-list entry s and runs on XCD s % 8, each XCD with its own L2.  The rank's
-blocks are therefore dealt round-robin to the 8 XCDs along its serpentine
-order and the list interleaves them (entry 8*i + g = i-th tile of XCD g), so
-every XCD gets an equal, frame-wide share of the work while the 4 tiles of a
-block -- which share footprint records -- stay in one L2.
+list entry s and runs on XCD s % 8, each XCD with its own L2.  Block (i, j)
+goes to bin (i + m j) mod 8*world (m = 3, or the next odd number coprime
+with 8*world) -- rank = bin mod world, XCD = bin div
+world -- a diagonal lattice that spreads every (rank, XCD) pair evenly over
+the frame; the list interleaves the rank's 8 XCD sublists (entry 8*k + g =
+k-th tile of XCD g) and the tiles of a block, which share footprint records,
+stay in one L2.
 """
 from __future__ import annotations
 
 import numpy as np
 
-TILE = 16
+TILE_W, TILE_H = 64, 4
 PAD = 0xFFFFFFFF
-BLOCK = 2  # tiles per block edge
+BLOCK_X, BLOCK_Y = 1, 4  # tiles per block
 XCDS = 8   # MI355X accelerator complex dies (workgroup b runs on XCD b % 8)
 
 
 def tiles_x(width: int) -> int:
-    return (width + TILE - 1) // TILE
+    return (width + TILE_W - 1) // TILE_W
 
 
 def tiles_y(height: int) -> int:
-    return (height + TILE - 1) // TILE
+    return (height + TILE_H - 1) // TILE_H
+
+
+def _lattice_step(world_size: int) -> int:
+    """row shift of the dealing lattice: odd, > 1, coprime with 8 * world_size"""
+    import math
+    m = 3
+    while math.gcd(m, XCDS * world_size) != 1:
+        m += 2
+    return m
+
+
+def _bin(bx: int, by: int, world_size: int) -> int:
+    return (bx + _lattice_step(world_size) * by) % (XCDS * world_size)
 
 
 def owner_of(width: int, height: int, world_size: int) -> np.ndarray:
     """rank owning each tile, shape (tiles_y, tiles_x)."""
     tx, ty = tiles_x(width), tiles_y(height)
-    nbx, nby = (tx + BLOCK - 1) // BLOCK, (ty + BLOCK - 1) // BLOCK
+    nbx, nby = (tx + BLOCK_X - 1) // BLOCK_X, (ty + BLOCK_Y - 1) // BLOCK_Y
     by, bx = np.mgrid[0:nby, 0:nbx]
-    snake = np.where(by % 2 == 0, bx, nbx - 1 - bx)
-    block_rank = (by * nbx + snake) % world_size
-    return np.repeat(np.repeat(block_rank, BLOCK, 0), BLOCK, 1)[:ty, :tx].astype(np.int64)
+    m = _lattice_step(world_size)
+    block_rank = ((bx + m * by) % (XCDS * world_size)) % world_size
+    return np.repeat(np.repeat(block_rank, BLOCK_Y, 0), BLOCK_X, 1)[:ty, :tx].astype(np.int64)
 
 
 def tile_lists(width: int, height: int, world_size: int) -> np.ndarray:
@@ -53,17 +68,14 @@ def tile_lists(width: int, height: int, world_size: int) -> np.ndarray:
     docstring), PAD-padded to the longest list so every rank gathers the same
     number of bytes."""
     tx, ty = tiles_x(width), tiles_y(height)
-    nbx, nby = (tx + BLOCK - 1) // BLOCK, (ty + BLOCK - 1) // BLOCK
+    nbx, nby = (tx + BLOCK_X - 1) // BLOCK_X, (ty + BLOCK_Y - 1) // BLOCK_Y
     per_rank = [[[] for _ in range(XCDS)] for _ in range(world_size)]
-    j = 0
     for by in range(nby):
-        for k in range(nbx):
-            bx = k if by % 2 == 0 else nbx - 1 - k
-            r, q = j % world_size, j // world_size   # q-th block of rank r
-            j += 1
-            lst = per_rank[r][q % XCDS]
-            for y in range(by * BLOCK, min(ty, by * BLOCK + BLOCK)):
-                for x in range(bx * BLOCK, min(tx, bx * BLOCK + BLOCK)):
+        for bx in range(nbx):
+            b = _bin(bx, by, world_size)
+            lst = per_rank[b % world_size][b // world_size]
+            for y in range(by * BLOCK_Y, min(ty, by * BLOCK_Y + BLOCK_Y)):
+                for x in range(bx * BLOCK_X, min(tx, bx * BLOCK_X + BLOCK_X)):
                     lst.append(y * tx + x)
     ids = []
     for subs in per_rank:
