@@ -169,6 +169,12 @@ uint32_t vr_tiles_y(uint32_t height);
  * render_kernel call launched (e.g. "k_march_quad<B=8,M=1>"), "" before any */
 const char *vr_last_kernel(void);
 
+/* Device self-test: compares the entropy decode's fast float logarithm with
+ * (float)log((double)x) for every positive finite float (synchronous, about a
+ * second).  counts[0] = mismatches (must be 0), counts[1] = inputs decided by
+ * the double-log fallback. */
+int vr_selftest_logf(uint64_t counts[2]);
+
 /* library version string */
 const char *vr_version(void);
 

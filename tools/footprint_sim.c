@@ -18,6 +18,16 @@
 #define H 1080
 
 static float M[12];
+static int LAYOUT = 0; /* 0: x-rows (4 records along x per line), 1: 2x2 (x,y) micro-bricks,
+                          2: 2x1x2 (x,z) micro-bricks */
+
+static uint32_t line_of(uint32_t x, uint32_t y, uint32_t z) {
+    if (LAYOUT == 1)
+        return (uint32_t)(((uint64_t)z * (N / 2) + (y >> 1)) * (N / 2) + (x >> 1));
+    if (LAYOUT == 2)
+        return (uint32_t)(((uint64_t)(z >> 1) * N + y) * (N / 2) + (x >> 1));
+    return (uint32_t)((((uint64_t)z * N + y) * N + x) >> 2);
+}
 
 static void lin_axis(float u, int n, int *i0, int *i1) {
     u = fminf(fmaxf(u, 0.0f), 1.0f);
@@ -51,9 +61,8 @@ static int ray_lines(int x, int y, int nsteps, uint32_t *out /* 8 per step */) {
         lin_axis(pz * 0.5f + 0.5f, N, &z0, &z1);
         int ys[2] = {y0, y1}, zs[2] = {z0, z1};
         for (int c = 0; c < 4; c++) {
-            uint64_t r = ((uint64_t)zs[c >> 1] * N + ys[c & 1]) * N;
-            out[k++] = (uint32_t)(((r + x0) * 32) >> 7);
-            out[k++] = (uint32_t)(((r + x1) * 32) >> 7);
+            out[k++] = line_of(x0, ys[c & 1], zs[c >> 1]);
+            out[k++] = line_of(x1, ys[c & 1], zs[c >> 1]);
         }
         px += sx; py += sy; pz += sz;
     }
@@ -79,6 +88,7 @@ int main(int argc, char **argv) {
     const float c1[12] = {0.70710677f, 0.0f, -0.70710677f, -2.828427f, 0.35355338f, 0.8660254f,
                           0.35355338f, 1.4142135f, 0.61237246f, -0.5f, 0.61237246f, 2.4494898f};
     memcpy(M, strcmp(argv[2], "C0") == 0 ? c0 : c1, sizeof M);
+    if (getenv("LAYOUT")) LAYOUT = atoi(getenv("LAYOUT"));
     FILE *f = fopen(argv[1], "rb");
     if (!f) return 1;
     int32_t *steps = malloc(sizeof(int32_t) * W * H);

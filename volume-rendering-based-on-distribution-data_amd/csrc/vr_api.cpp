@@ -200,13 +200,18 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
         const int v = std::atoi(e);
         if (v >= 1 && v <= 32) P.wg_per_cu = v;
     }
-    // Kernel choice.  Per-ray lanes (path 2) coalesce when the screen x axis
-    // runs along the volume's voxel rows (|m[0]| ~ 1, e.g. the runSingleTest
-    // view): consecutive lanes then read consecutive records.  Otherwise the
-    // quad-cooperative gathers (path 0, B == 8) keep every 4-lane group on one
-    // contiguous 64-byte run.  VR_PATH overrides: 0 quad, 1 k_march (LDS-staged
-    // box / per-ray), 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows.
-    P.path = std::fabs(d->inv_view[0]) >= 0.95f ? 2 : 0;
+    // Kernel choice (measured at 1024^3 x 8).  When the
+    // screen x axis runs along the volume's voxel rows (|m[0]| ~ 1, e.g. the
+    // runSingleTest view) consecutive lanes read consecutive records and the
+    // per-ray pipelined march (path 2) is fastest for mean and variance; the
+    // log-heavy entropy decode prefers the wave-staged march (path 4), which
+    // decodes every record once per wave-step instead of once per touching
+    // ray.  Oblique views use the quad-cooperative gathers (path 0, B == 8),
+    // which keep every 4-lane group on one contiguous 64-byte run.
+    // VR_PATH overrides: 0 quad, 1 k_march (LDS-staged box / per-ray),
+    // 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows.
+    const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
+    P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
         if (v >= 0 && v <= 4) P.path = v;
@@ -246,6 +251,22 @@ extern "C" {
 const char *vr_version(void) { return "vrdd-amd 0.1 (gfx950)"; }
 
 const char *vr_last_kernel(void) { return vr::last_march_kernel(); }
+
+int vr_selftest_logf(uint64_t *counts) {
+    if (!counts) return fail(VR_ERR_ARG, "null pointer");
+    unsigned long long *d = nullptr;
+    VR_HIP(hipMalloc(&d, 2 * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d, 0, 2 * sizeof(unsigned long long), g.stream);
+    if (e == hipSuccess) e = vr::launch_logcheck(d, g.stream);
+    unsigned long long h[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, g.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "vr_selftest_logf");
+    counts[0] = h[0];
+    counts[1] = h[1];
+    return VR_OK;
+}
 
 #ifdef VR_WG_PROF
 // tooling build only (tools/wg_prof.py): read and reset the phase counters

@@ -153,6 +153,51 @@ __device__ __forceinline__ float raw_variance(const float (&p)[B], float mean) {
     return var;
 }
 
+// log of a float as the reference evaluates it, (float)log((double)x)
+// (DESIGN.md section 3), for finite x > 0, at a third of the double log's
+// cost.  A short atanh series in double gives y = log x to ~2^-50 relative;
+// unless y lies within 2^-44 of a float rounding midpoint, rounding y to
+// float already gives the rounding of the exact logarithm -- and so of the
+// double log -- and only the remaining ~2^-20 of inputs evaluate the double
+// log.  Exhaustively equal to (float)log((double)x) over all positive floats
+// (vr_selftest_logf, tests/test_gpu_parity.py).
+__device__ __forceinline__ bool logf_fast(float x, float &r) {
+    int e;
+    double m = frexp((double)x, &e);  // x = m 2^e, m in [0.5, 1)
+    if (m < 0.70710678118654752440) {
+        m = m * 2.0;
+        e -= 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0);  // |s| <= 0.1716
+    const double z = s * s;
+    // log m = 2 atanh s = 2s (1 + z/3 + z^2/5 + ... + z^8/17), remainder < 2^-50
+    double q = 1.0 / 17.0;
+    q = fma(q, z, 1.0 / 15.0);
+    q = fma(q, z, 1.0 / 13.0);
+    q = fma(q, z, 1.0 / 11.0);
+    q = fma(q, z, 1.0 / 9.0);
+    q = fma(q, z, 1.0 / 7.0);
+    q = fma(q, z, 1.0 / 5.0);
+    q = fma(q, z, 1.0 / 3.0);
+    const double s2 = s + s;
+    const double y = fma((double)e, VR_LN2_D, fma(s2 * z, q, s2));
+    r = (float)y;
+    if (r == 0.0f) return false;                  // x near 1: let the double log decide
+    const double d = y - (double)r;               // exact
+    int er;
+    const float mr = frexpf(fabsf(r), &er);       // |r| = mr 2^er
+    double half = ldexp(1.0, er - 25);            // half an ulp of r
+    if (mr == 0.5f && d * (double)r < 0.0) half *= 0.5;  // below a power of two
+    return fabs(fabs(d) - half) > 0x1p-44 * fabs(y);
+}
+
+__device__ __forceinline__ float logf_canon(float x) {
+    float r;
+    if (x == 1.0f) return 0.0f;
+    if (logf_fast(x, r)) return r;
+    return (float)log((double)x);
+}
+
 // K:761-769
 template <int B>
 __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
@@ -161,7 +206,7 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
     for (int i = 0; i < B; i++) {
         const float pr = p[i];
         const double t =
-            pr <= 0 ? 0.0 : div_const((double)(float)log((double)pr), VR_LN2_D, kLn2R);
+            pr <= 0 ? 0.0 : div_const((double)logf_canon(pr), VR_LN2_D, kLn2R);
         ent = (float)((double)ent + (double)pr * t);
     }
     ent = -ent;
@@ -212,7 +257,7 @@ __device__ __forceinline__ float record_stat_rt(const float *__restrict__ p, int
         for (int i = 0; i < nb; i++) {
             const float pr = p[i];
             const double t =
-                pr <= 0 ? 0.0 : div_const((double)(float)log((double)pr), VR_LN2_D, kLn2R);
+                pr <= 0 ? 0.0 : div_const((double)logf_canon(pr), VR_LN2_D, kLn2R);
             ent = (float)((double)ent + (double)pr * t);
         }
         ent = -ent;

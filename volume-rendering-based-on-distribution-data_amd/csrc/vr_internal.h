@@ -29,6 +29,7 @@ const char *last_march_kernel();
 #ifdef VR_WG_PROF
 hipError_t wg_prof_read(unsigned long long *host);   // tooling build only
 #endif
+hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,
                             uint32_t tiles_x, uint32_t *frame, uint32_t W, uint32_t H,

@@ -617,6 +617,9 @@ hipError_t wg_prof_read(unsigned long long *host) {
 constexpr int kWsTbl = 256;   // (y,z) row-table entries per wave (4 per lane)
 constexpr int kWsRows = 128;  // compacted rows per wave-step
 constexpr int kWsRec = 512;   // staged record statistics per wave-step
+#ifndef VR_WS_U3
+#define VR_WS_U3 2            // 64-record blocks in flight per lane, entropy decode
+#endif
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -635,7 +638,7 @@ __device__ __forceinline__ int wave_incl_max(int v) {
 }
 
 #ifndef VR_WS_WAVES
-#define VR_WS_WAVES 4       // waves per SIMD the wave-staged kernel is register-capped for
+#define VR_WS_WAVES 4       // the wave-staged march is latency-bound: keep >= 4 waves/SIMD
 #endif
 
 template <int B, int M>
@@ -745,14 +748,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                 }
                 wave_sync();
                 WG_PROF_T(5)
-                // consecutive lanes on consecutive records; 4 x 64 records in flight
+                // consecutive lanes on consecutive records; U x 64 records in flight
+                // (fewer for the register-hungry entropy decode)
+                constexpr int U = M == 3 ? VR_WS_U3 : 4;
                 int carry = -1;
-                for (int q0 = 0; q0 < R; q0 += 256) {
-                    float rr[4][B];
-                    int li[4];
+                for (int q0 = 0; q0 < R; q0 += 64 * U) {
+                    float rr[U][B];
+                    int li[U];
                     WG_PROF_C(15, 1)
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
+                    for (int u = 0; u < U; u++) {
                         const int q = q0 + 64 * u + (int)lane;
                         uint64_t ga = 0;
                         li[u] = -1;
@@ -776,7 +781,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                         load_rec<B>(vol, ga, rr[u]);
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; u++)
+                    for (int u = 0; u < U; u++)
                         if (li[u] >= 0) stat[li[u]] = record_stat<B, M>(rr[u], P.enorm);
                 }
                 wave_sync();
@@ -1260,6 +1265,27 @@ __global__ __launch_bounds__(256) void k_popcount(const unsigned long long *__re
     // wave reduction then one atomic per wave
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
     if ((threadIdx.x & 63) == 0) atomicAdd(total, acc);
+}
+
+// Exhaustive check of logf_canon against (float)log((double)x) over every
+// positive finite float; cnt[0] = mismatches, cnt[1] = inputs that took the
+// double-log fallback.
+__global__ __launch_bounds__(256) void k_logcheck(unsigned long long *cnt) {
+    unsigned long long bad = 0, slow = 0;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t b = 1 + blockIdx.x * blockDim.x + threadIdx.x; b < 0x7F800000u; b += stride) {
+        const float x = __uint_as_float(b);
+        float r;
+        slow += !logf_fast(x, r);
+        bad += __float_as_uint(logf_canon(x)) != __float_as_uint((float)log((double)x));
+    }
+    if (bad) atomicAdd(&cnt[0], bad);
+    if (slow) atomicAdd(&cnt[1], slow);
+}
+
+hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s) {
+    hipLaunchKernelGGL(k_logcheck, dim3(8192), dim3(256), 0, s, cnt);
+    return hipGetLastError();
 }
 
 // ------------------------------ launchers ---------------------------------
