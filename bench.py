@@ -122,7 +122,7 @@ def main():
     pkg.set_stream(stream)
     pkg.synthesize((n, n, n), nb, SEED)
 
-    lists = pkg.tiles.tile_lists(W, H, world)
+    lists = pkg.tiles.tile_lists(W, H, world, m)
     n_slots = lists.shape[1]
     frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
     with torch.cuda.stream(stream):

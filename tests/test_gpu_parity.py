@@ -224,7 +224,7 @@ def test_errors_do_not_exit(pkg, gpu):
 
 
 @pytest.mark.parametrize("path,env", [
-    ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}),
+    ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}), ("5", {}),
     ("1", {"VR_BOX_MAX": "0"}), ("1", {"VR_BOX_MAX": "64"}), ("0", {"VR_WG_PER_CU": "1"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])

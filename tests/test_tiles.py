@@ -122,3 +122,24 @@ def test_lists_match_owner_and_balance_xcds(pkg, world):
             cy = (tile // tx * T.TILE_H + T.TILE_H / 2) / H * 2 - 1
             share[r, s % T.XCDS] += (abs(cx) < 0.6) and (abs(cy) < 0.6)
     assert share.max() / share.mean() < 1.2, share
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_lists_longest_first(pkg, world):
+    """with the view matrix every XCD sublist runs its blocks longest-ray first and
+    the lists still cover every tile exactly once"""
+    T = pkg.tiles
+    W, H = 1920, 1080
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    lists = T.tile_lists(W, H, world, m)
+    real = lists[lists != T.PAD]
+    assert sorted(real.tolist()) == list(range(T.tiles_x(W) * T.tiles_y(H)))
+    tx = T.tiles_x(W)
+    for r in range(world):
+        for g in range(T.XCDS):
+            sub = [t for t in lists[r][g::T.XCDS] if t != T.PAD]
+            c = [max(T.est_steps(m, W, H, (t % tx) * T.TILE_W + k * (T.TILE_W - 1) // 2,
+                                 (t // tx) * T.TILE_H + T.TILE_H // 2) for k in range(3))
+                 for t in sub]
+            blocks = [max(c[i:i + T.BLOCK_X * T.BLOCK_Y]) for i in range(0, len(c), T.BLOCK_X * T.BLOCK_Y)]
+            assert all(a >= b - 1e-6 for a, b in zip(blocks, blocks[1:]))

@@ -1,0 +1,76 @@
+"""Per-rank render time of the multi-GPU tile split, simulated on one GPU (tooling).
+
+For N in 1, 2, 4, 8 every rank's tile list is rendered in turn into its packed
+buffer (the work one GPU does at world size N), then rank 0's unscatter of
+all N buffers is timed.  max over ranks + unscatter approximates the N-GPU
+frame time without the RCCL gather.
+
+  python tools/rank_sim.py [--config 1024x8] [--camera C0] [--reps 5]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="1024x8")
+    ap.add_argument("--camera", default="C0")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-lpt", action="store_true", help="tile lists without longest-first order")
+    args = ap.parse_args()
+    import torch
+    import __graft_entry__ as g
+    import bench
+    pkg = g.load_package()
+    n, nb, W, H = bench.CONFIGS[args.config]
+    pkg.synthesize((n, n, n), nb, bench.SEED)
+    m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
+         else pkg.camera.display_inv_view((30.0, 45.0)))
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.reps
+
+    full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    dfull = pkg.make_desc(full, W, H, m)
+    t1 = timed(lambda: pkg.render(dfull))
+    print(f"{args.config} {args.camera}: full frame {t1:.3f} ms")
+    # latency floor: k centre-most tiles alone on the GPU
+    lists1 = pkg.tiles.tile_lists(W, H, 1, m)[0]
+    for k in (1, 64, 512, 1024):
+        sel = torch.from_numpy(lists1[:k].view(np.int32).copy()).cuda()
+        pk = torch.zeros(k * 256, dtype=torch.int32, device="cuda")
+        dk = pkg.make_desc(pk, W, H, m, d_tile_list=sel, n_tiles=k)
+        print(f"  {k:5d} longest tiles alone: {timed(lambda dk=dk: pkg.render(dk)):.3f} ms")
+    for world in (2, 4, 8):
+        lists = pkg.tiles.tile_lists(W, H, world, None if args.no_lpt else m)
+        slots = lists.shape[1]
+        packed = torch.zeros((world, slots * 256), dtype=torch.int32, device="cuda")
+        dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+        per = []
+        for r in range(world):
+            d = pkg.make_desc(packed[r], W, H, m, d_tile_list=dl[r], n_tiles=slots)
+            per.append(timed(lambda d=d: pkg.render(d)))
+        frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        tu = timed(lambda: pkg.unscatter_tiles(packed, dl, world, slots, frame, W, H))
+        torch.cuda.synchronize()
+        ok = torch.equal(frame, full)
+        print(f"  N={world}: per-rank ms {' '.join(f'{x:.3f}' for x in per)}  max {max(per):.3f}"
+              f"  unscatter {tu:.3f}  -> est. speedup {t1 / (max(per) + tu):.2f}x"
+              f"  frame {'identical' if ok else 'DIFFERS'}")
+
+
+if __name__ == "__main__":
+    main()

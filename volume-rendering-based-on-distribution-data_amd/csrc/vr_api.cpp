@@ -29,7 +29,8 @@ struct State {
     int status = VR_OK;
     // full-frame workgroup -> tile order (frame_order), cached per frame shape
     uint32_t *perm = nullptr;
-    uint32_t perm_key[4] = {0, 0, 0, 0};
+    size_t perm_cap = 0;
+    uint32_t perm_key[18] = {0};
     std::vector<uint32_t> perm_host;
 };
 
@@ -100,6 +101,25 @@ int check_method(int m) {
     return fail(VR_ERR_ARG, "unknown queryMethod %d", m);
 }
 
+// Host estimate of the samples a ray takes before leaving the volume (the
+// slab test of K:136-156 on the pixel's ray; early termination ignored).
+float est_steps(const float *M, uint32_t W, uint32_t H, float x, float y) {
+    const float u = (x / (float)W) * 2.0f - 1.0f, v = (y / (float)H) * 2.0f - 1.0f;
+    const float inv = 1.0f / std::sqrt(u * u + v * v + 4.0f);
+    const float ax = u * inv, ay = v * inv, az = -2.0f * inv;
+    const float d[3] = {ax * M[0] + ay * M[1] + az * M[2], ax * M[4] + ay * M[5] + az * M[6],
+                        ax * M[8] + ay * M[9] + az * M[10]};
+    const float o[3] = {M[3], M[7], M[11]};
+    float tn = -1e30f, tf = 1e30f;
+    for (int k = 0; k < 3; k++) {
+        const float a = (-1.0f - o[k]) / d[k], b = (1.0f - o[k]) / d[k];
+        tn = std::max(tn, std::min(a, b));
+        tf = std::min(tf, std::max(a, b));
+    }
+    tn = std::max(tn, 0.0f);
+    return tf > tn ? (tf - tn) / vr::kTStep : 0.0f;
+}
+
 // Full-frame tile order.  Workgroup b runs on XCD b % 8, and each XCD has its
 // own L2.  Tiles are grouped in bx x by blocks (neighbouring tiles share the
 // records along their common edges, so a block keeps that sharing inside one
@@ -107,9 +127,12 @@ int check_method(int m) {
 // every XCD an evenly spread eighth of any region spanning a few blocks -- so
 // the hit region, and with it the ray-marching work, is split evenly (a raster
 // split hands the frame's empty top and bottom strips to whole XCDs).  Each
-// XCD walks its blocks row by row.  VR_XBLOCK="bx,by" (default 1,4 = 64x16
-// pixels; "0" = plain raster order).
-int frame_order(uint32_t tx, uint32_t ty, const uint32_t *&perm) {
+// XCD takes its blocks longest-ray first (longest-processing-time order on
+// the view's ray lengths): a tile's march is a chain of dependent gathers, so
+// the frame ends no earlier than its longest tile started plus that tile's
+// length.  VR_XBLOCK="bx,by" (default 1,4 = 64x16 pixels; "0" = plain raster
+// order).
+int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_t *&perm) {
     uint32_t bx = 1, by = 4;
     if (const char *e = std::getenv("VR_XBLOCK")) {
         char *end = nullptr;
@@ -120,20 +143,38 @@ int frame_order(uint32_t tx, uint32_t ty, const uint32_t *&perm) {
         bx = (uint32_t)std::min(a, 64L);
         by = (uint32_t)std::min(b, 64L);
     }
-    const uint32_t key[4] = {tx, ty, bx, by};
+    uint32_t key[18] = {d->width, d->height, bx, by};
+    std::memcpy(key + 4, d->inv_view, sizeof d->inv_view);
+    key[16] = std::getenv("VR_NO_LPT") ? 1u : 0u;
     if (g.perm && std::memcmp(key, g.perm_key, sizeof key) == 0) {
         perm = g.perm;
         return VR_OK;
     }
     const uint32_t nbx = (tx + bx - 1) / bx, nby = (ty + by - 1) / by;
-    std::vector<std::vector<uint32_t>> lists(8);
+    struct Blk { float cost; uint32_t i, j; };
+    std::vector<std::vector<Blk>> blocks(8);
     for (uint32_t byi = 0; byi < nby; byi++) {
         for (uint32_t bxi = 0; bxi < nbx; bxi++) {
-            std::vector<uint32_t> &l = lists[(bxi + 3 * byi) & 7];
+            float c = 0.0f;
             for (uint32_t y = byi * by; y < std::min(ty, byi * by + by); y++)
                 for (uint32_t x = bxi * bx; x < std::min(tx, bxi * bx + bx); x++)
-                    l.push_back(y * tx + x);
+                    for (int k = 0; k < 3; k++)
+                        c = std::max(c, est_steps(d->inv_view, d->width, d->height,
+                                                  (float)(x * vr::kTileW + k * (vr::kTileW - 1) / 2),
+                                                  (float)(y * vr::kTileH + vr::kTileH / 2)));
+            blocks[(bxi + 3 * byi) & 7].push_back({c, bxi, byi});
         }
+    }
+    std::vector<std::vector<uint32_t>> lists(8);
+    for (int x8 = 0; x8 < 8; x8++) {
+        std::vector<Blk> &bl = blocks[x8];
+        if (!key[16])
+            std::stable_sort(bl.begin(), bl.end(),
+                             [](const Blk &a, const Blk &b) { return a.cost > b.cost; });
+        for (const Blk &b : bl)
+            for (uint32_t y = b.j * by; y < std::min(ty, b.j * by + by); y++)
+                for (uint32_t x = b.i * bx; x < std::min(tx, b.i * bx + bx); x++)
+                    lists[x8].push_back(y * tx + x);
     }
     std::vector<uint32_t> &h = g.perm_host;
     h.clear();
@@ -142,9 +183,13 @@ int frame_order(uint32_t tx, uint32_t ty, const uint32_t *&perm) {
     for (size_t i = 0; i < longest; i++)
         for (auto &l : lists)
             if (i < l.size()) h.push_back(l[i]);
-    if (g.perm) (void)hipFree(g.perm);
-    g.perm = nullptr;
-    VR_HIP(hipMalloc(&g.perm, h.size() * sizeof(uint32_t)));
+    if (h.size() > g.perm_cap) {  // grow; otherwise rewrite in stream order
+        if (g.perm) (void)hipFree(g.perm);
+        g.perm = nullptr;
+        g.perm_cap = 0;
+        VR_HIP(hipMalloc(&g.perm, h.size() * sizeof(uint32_t)));
+        g.perm_cap = h.size();
+    }
     VR_HIP(hipMemcpyAsync(g.perm, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                           g.stream));
     std::memcpy(g.perm_key, key, sizeof key);
@@ -181,7 +226,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     P.tile_list = d->d_tile_list;
     P.perm = nullptr;
     if (!d->d_tile_list) {
-        int rc = frame_order(tiles_x(d->width), tiles_y(d->height), P.perm);
+        int rc = frame_order(d, tiles_x(d->width), tiles_y(d->height), P.perm);
         if (rc != VR_OK) return rc;
     }
     P.out = d->d_output;
@@ -209,12 +254,13 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     // ray.  Oblique views use the quad-cooperative gathers (path 0, B == 8),
     // which keep every 4-lane group on one contiguous 64-byte run.
     // VR_PATH overrides: 0 quad, 1 k_march (LDS-staged box / per-ray),
-    // 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows.
+    // 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows,
+    // 5 per-ray half-step pipelined.
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
-        if (v >= 0 && v <= 4) P.path = v;
+        if (v >= 0 && v <= 5) P.path = v;
     }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {

@@ -920,6 +920,81 @@ __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vo
                 sw * P.brightness);
 }
 
+// ---- half-step pipelined per-ray march (B <= 8) ----
+// k_march_pipe keeps a whole step of corner records in flight while the
+// previous step decodes (2 x 8 records per lane: 238 VGPRs at B = 8, two
+// waves per SIMD).  Here the next step's gathers are issued one half at a
+// time, each half into the registers whose records were just decoded, so at
+// most 8 records per lane are live: half the registers, twice the waves per
+// CU, and a ray's dependent step chain still overlaps half a step of loads.
+template <int B>
+__device__ __forceinline__ void gather4(const float *__restrict__ vol, const Params &P,
+                                        const Foot &f, int zsel, float (&rec)[4][B]) {
+    const uint64_t z = zsel ? (uint64_t)f.z1 : (uint64_t)f.z0;
+    const uint64_t r0 = z * P.sz + (uint64_t)f.y0 * P.sy;
+    const uint64_t r1 = z * P.sz + (uint64_t)f.y1 * P.sy;
+    load_rec<B>(vol, r0 + f.x0, rec[0]);
+    load_rec<B>(vol, r0 + f.x1, rec[1]);
+    load_rec<B>(vol, r1 + f.x0, rec[2]);
+    load_rec<B>(vol, r1 + f.x1, rec[3]);
+}
+
+#ifndef VR_HALF_WAVES
+#define VR_HALF_WAVES 4     // waves per SIMD the half-step march is register-capped for
+#endif
+
+template <int B, int M>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_HALF_WAVES, 8))) void k_march_half(const float *__restrict__ vol, Params P) {
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    uint32_t lx, ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    if (x >= P.W || y >= P.H) return;  // no cross-lane work in this kernel
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    if (!make_ray(P, x, y, r)) {
+        if (P.out_n) P.out_n[o] = -1;
+        return;
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    Foot fc = footprint(P, px, py, pz);
+    float lo[4][B], hi[4][B];  // z0 and z1 corner records of the current step
+    gather4<B>(vol, P, fc, 0, lo);
+    gather4<B>(vol, P, fc, 1, hi);
+    for (int i = 0; i < kMaxSteps; i++) {
+        const float tn = t + kTStep;                               // K:701
+        const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, K:381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;   // K:706
+        Foot fn = fc;
+        if (cont) fn = footprint(P, nx, ny, nz);
+        float sv[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) sv[j] = record_stat<B, M>(lo[j], P.enorm);
+        if (cont) gather4<B>(vol, P, fn, 0, lo);
+#pragma unroll
+        for (int j = 0; j < 4; j++) sv[4 + j] = record_stat<B, M>(hi[j], P.enorm);
+        if (cont) gather4<B>(vol, P, fn, 1, hi);
+        const float sample = blend8(sv, fc);
+        n = i + 1;
+        if (composite(P, sample, sx, sy, sz, sw) || !cont) break;
+        t = tn;
+        px = nx;
+        py = ny;
+        pz = nz;
+        fc = fn;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 // ---- quad-cooperative pipelined march (B == 8) ----
 // Lane l = 4q + g of a wave is the home of the ray at pixel (q, g) of the
 // wave's 16x4 pixel block (the 4 waves of a workgroup sit side by side in the
@@ -1322,6 +1397,15 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             case 1: hipLaunchKernelGGL((k_march_wg<B, 1>), grid, block, 0, s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_wg<B, 2>), grid, block, 0, s, vol, P); break;
             case 3: hipLaunchKernelGGL((k_march_wg<B, 3>), grid, block, 0, s, vol, P); break;
+            }
+            return hipGetLastError();
+        }
+        if (P.path == 5 && method >= 1 && method <= 3) {
+            note_kernel("k_march_half", B, method);
+            switch (method) {
+            case 1: hipLaunchKernelGGL((k_march_half<B, 1>), grid, block, 0, s, vol, P); break;
+            case 2: hipLaunchKernelGGL((k_march_half<B, 2>), grid, block, 0, s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_half<B, 3>), grid, block, 0, s, vol, P); break;
             }
             return hipGetLastError();
         }

@@ -63,24 +63,60 @@ def owner_of(width: int, height: int, world_size: int) -> np.ndarray:
     return np.repeat(np.repeat(block_rank, BLOCK_Y, 0), BLOCK_X, 1)[:ty, :tx].astype(np.int64)
 
 
-def tile_lists(width: int, height: int, world_size: int) -> np.ndarray:
+def est_steps(inv_view, width: int, height: int, px, py) -> np.ndarray:
+    """samples a pixel's ray takes before leaving the volume (slab test, K:136-156;
+    early termination ignored) -- the cost estimate of the longest-first order"""
+    M = np.asarray(inv_view, dtype=np.float64).reshape(3, 4)
+    u = np.asarray(px, np.float64) / width * 2 - 1
+    v = np.asarray(py, np.float64) / height * 2 - 1
+    inv = 1 / np.sqrt(u * u + v * v + 4)
+    a = np.stack([u * inv, v * inv, -2 * inv])
+    d = M[:, :3] @ a.reshape(3, -1)
+    o = M[:, 3:4]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t1, t2 = (-1 - o) / d, (1 - o) / d
+    tn = np.maximum(np.nanmax(np.minimum(t1, t2), axis=0), 0)
+    tf = np.nanmin(np.maximum(t1, t2), axis=0)
+    return np.where(tf > tn, (tf - tn) / 0.01, 0.0).reshape(np.shape(u))
+
+
+def tile_lists(width: int, height: int, world_size: int, inv_view=None) -> np.ndarray:
     """(world_size, n_slots) uint32 tile ids, XCD-interleaved per rank (module
     docstring), PAD-padded to the longest list so every rank gathers the same
-    number of bytes."""
+    number of bytes.  With the view matrix, each XCD's blocks are ordered
+    longest-ray first (as the library orders full frames): a tile's march is a
+    chain of dependent gathers, so the longest tiles must start first."""
     tx, ty = tiles_x(width), tiles_y(height)
     nbx, nby = (tx + BLOCK_X - 1) // BLOCK_X, (ty + BLOCK_Y - 1) // BLOCK_Y
-    per_rank = [[[] for _ in range(XCDS)] for _ in range(world_size)]
+    cost = np.zeros((nby, nbx))
+    if inv_view is not None:
+        gy, gx = np.mgrid[0:ty, 0:tx]
+        c = np.zeros((ty, tx))
+        for k in range(3):
+            c = np.maximum(c, est_steps(inv_view, width, height,
+                                        gx * TILE_W + k * (TILE_W - 1) // 2,
+                                        gy * TILE_H + TILE_H // 2))
+        pad = np.zeros((nby * BLOCK_Y, nbx * BLOCK_X))
+        pad[:ty, :tx] = c
+        cost = pad.reshape(nby, BLOCK_Y, nbx, BLOCK_X).max(axis=(1, 3))
+    subs_blocks = [[[] for _ in range(XCDS)] for _ in range(world_size)]
     for by in range(nby):
         for bx in range(nbx):
             b = _bin(bx, by, world_size)
-            lst = per_rank[b % world_size][b // world_size]
-            for y in range(by * BLOCK_Y, min(ty, by * BLOCK_Y + BLOCK_Y)):
-                for x in range(bx * BLOCK_X, min(tx, bx * BLOCK_X + BLOCK_X)):
-                    lst.append(y * tx + x)
+            subs_blocks[b % world_size][b // world_size].append((bx, by))
     ids = []
-    for subs in per_rank:
-        longest = max((len(l) for l in subs), default=0)
-        ids.append(np.array([l[i] for i in range(longest) for l in subs if i < len(l)],
+    for subs in subs_blocks:
+        lists = []
+        for blocks in subs:
+            blocks = sorted(blocks, key=lambda q: -cost[q[1], q[0]])  # stable
+            lst = []
+            for bx, by in blocks:
+                for y in range(by * BLOCK_Y, min(ty, by * BLOCK_Y + BLOCK_Y)):
+                    for x in range(bx * BLOCK_X, min(tx, bx * BLOCK_X + BLOCK_X)):
+                        lst.append(y * tx + x)
+            lists.append(lst)
+        longest = max((len(l) for l in lists), default=0)
+        ids.append(np.array([l[i] for i in range(longest) for l in lists if i < len(l)],
                             dtype=np.uint32))
     n_slots = max((len(i) for i in ids), default=0)
     out = np.full((world_size, n_slots), PAD, dtype=np.uint32)
