@@ -43,8 +43,9 @@ typedef struct { float x, y; } vr_float2;                     /* == float2     *
  * own gfx950 launch geometry (64x4-pixel tiles, one 64-pixel row per wave).
  * volumeSize is used exactly where the reference uses it: the method-7 corner
  * grid (K:322-352).  queryMethod: 1 mean, 2 variance, 3 entropy,
- * 7 software-interpolated mean.  4/5/6 and 8/9/0 need the fractal codec and
- * the flexible-block pre-pass (out of scope): the call records an error and
+ * 7 software-interpolated mean, 4/5/6 fractal-codec mean / variance / entropy
+ * (needs the codec arrays of initCuda or vr_init_codec).  8/9/0 need the
+ * flexible-block pre-pass (out of scope): the call records an error and
  * writes nothing.  Asynchronous on the library stream (default: null stream),
  * like the reference's default-stream launch. */
 void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output,
@@ -60,8 +61,10 @@ void copyInvViewMatrix(float *invViewMatrix, size_t sizeofMatrix);
  * B = histogramSize.width and r = x + X*(y + Y*z) -- the reference's layered
  * layout (bin, r % height, r / height) is exactly this AoS order (K:363-364).
  * histogramSize.height*depth must equal volumeSize.width*height*depth.
- * The codec / flexible-block arrays (args 4-18) feed methods 4-6 and 8/9/0
- * only; they are accepted and ignored. */
+ * Args 4-9 (codebook, templates, errorsbook and their sizes) make the codec
+ * volume of methods 4/5/6 resident when all three arrays are non-null (see
+ * vr_init_codec); the flexible-block arrays (args 10-18) feed methods 8/9/0
+ * only and are accepted and ignored. */
 void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
               vr_int4 *h_codebook, vr_extent codebookSize, float *h_templates,
               vr_extent templatesSize, vr_float2 *h_errorsbook, vr_extent errorsbookSize,
@@ -109,6 +112,20 @@ int vr_init_distribution(const float *bins, vr_extent dims, int nbins, int where
 /* Generate the seeded synthetic distribution volume of DESIGN.md section 5
  * directly in HBM (library-owned). */
 int vr_synthesize(vr_extent dims, int nbins, uint64_t seed);
+
+/* Fractal/template codec volume for methods 4/5/6 (the initCuda arrays of
+ * K:1893-1900, as the reference's loaders fill them, C:558-675):
+ *   codebook  dims.width*height*depth x (template id, shift, flip, NE), voxel
+ *             order x + X*(y + Y*z);
+ *   templates ntemplates x nbins floats;
+ *   errors    err_slots (bin id, value) pairs per voxel, the first NE used.
+ * where: 0 = host arrays, 1 = device arrays (copied).  Entries are validated
+ * (template id < ntemplates, 0 <= shift < nbins, 0 <= NE <= err_slots);
+ * error bin ids outside [0, nbins) are skipped at decode.  nbins must be one
+ * of 1, 2, 4, 8, 16, 32.  initCuda calls this when its codebook, templates and
+ * errorsbook arguments are non-null. */
+int vr_init_codec(const vr_int4 *codebook, vr_extent dims, const float *templates,
+                  int ntemplates, const vr_float2 *errors, int err_slots, int nbins, int where);
 
 /* dims, bin count and device pointer of the resident volume */
 int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins);

@@ -57,12 +57,99 @@ def lib():
         L.orc_count_footprint.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.POINTER(RenderParams), ctypes.c_int]
         L.orc_count_footprint.restype = ctypes.c_int64
+        L.orc_render_codec.argtypes = [ctypes.POINTER(Codec), ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.POINTER(RenderParams),
+                                       u32p, fp, i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_render_codec.restype = ctypes.c_int64
+        L.orc_codec_decode.argtypes = [ctypes.POINTER(Codec), ctypes.c_int, ctypes.c_size_t, fp]
+        L.orc_codec_stats.argtypes = [ctypes.POINTER(Codec), ctypes.c_int, ctypes.c_size_t, fp]
         L.orc_splitmix64.argtypes = [ctypes.c_uint64]
         L.orc_splitmix64.restype = ctypes.c_uint64
         L.orc_synth_fill.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_uint64, fp, ctypes.c_int]
         _lib = L
     return _lib
+
+
+class Codec(ctypes.Structure):
+    _fields_ = [("codebook", ctypes.POINTER(ctypes.c_int32)),
+                ("templates", ctypes.POINTER(ctypes.c_float)),
+                ("ntemplates", ctypes.c_int),
+                ("errors", ctypes.POINTER(ctypes.c_float)),
+                ("err_slots", ctypes.c_int)]
+
+
+def _codec(codebook, templates, errors):
+    """ctypes view of (codebook int32[..., 4], templates float32[T, B], errors float32[..., E, 2]);
+    the arrays must stay alive while the struct is used"""
+    c = Codec()
+    c.codebook = codebook.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    c.templates = _fp(templates)
+    c.ntemplates = templates.shape[0]
+    c.errors = _fp(errors)
+    c.err_slots = errors.shape[-2]
+    return c
+
+
+def codec_decode(codebook, templates, errors, vidx):
+    codebook, templates, errors = _codec_arrays(codebook, templates, errors)
+    out = np.zeros(templates.shape[1], np.float32)
+    lib().orc_codec_decode(ctypes.byref(_codec(codebook, templates, errors)), templates.shape[1],
+                           int(vidx), _fp(out))
+    return out
+
+
+def codec_stats(codebook, templates, errors, vidx):
+    codebook, templates, errors = _codec_arrays(codebook, templates, errors)
+    out = np.zeros(3, np.float32)
+    lib().orc_codec_stats(ctypes.byref(_codec(codebook, templates, errors)), templates.shape[1],
+                          int(vidx), _fp(out))
+    return out
+
+
+def _codec_arrays(codebook, templates, errors):
+    return (np.ascontiguousarray(codebook, dtype=np.int32),
+            np.ascontiguousarray(templates, dtype=np.float32),
+            np.ascontiguousarray(errors, dtype=np.float32))
+
+
+def render_codec(codebook, templates, errors, params, row_start=0, row_stride=1, nthreads=0):
+    """methods 4/5/6 from a codec volume: codebook int32 (nz, ny, nx, 4), templates
+    float32 (T, B), errors float32 (nz, ny, nx, E, 2).  Returns like render()."""
+    codebook, templates, errors = _codec_arrays(codebook, templates, errors)
+    nz, ny, nx, _ = codebook.shape
+    H, W = params.height, params.width
+    out = np.zeros((H, W), dtype=np.uint32)
+    out_f = np.zeros((H, W, 4), dtype=np.float32)
+    out_n = np.full((H, W), -2, dtype=np.int32)
+    total = lib().orc_render_codec(
+        ctypes.byref(_codec(codebook, templates, errors)), nx, ny, nz, templates.shape[1],
+        ctypes.byref(params), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _fp(out_f),
+        out_n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row_start, row_stride, nthreads)
+    return out, out_f, out_n, total
+
+
+def synth_codec(nx, ny, nz, nbins, ntemplates=24, slots=None, seed=20261015):
+    """seeded synthetic codec volume (test input): templates are
+    normalised discretised Gaussians; per voxel a template, shift, flip and 0-3 sparse
+    errors drawn from splitmix64."""
+    slots = nbins if slots is None else slots
+    rng = np.random.default_rng(seed)
+    mu = rng.uniform(0.1, 0.9, ntemplates)
+    sig = rng.uniform(0.05, 0.3, ntemplates)
+    c = (np.arange(nbins) + 0.5) / nbins
+    t = np.exp(-((c[None, :] - mu[:, None]) ** 2) / (2 * sig[:, None] ** 2))
+    templates = (t / t.sum(1, keepdims=True)).astype(np.float32)
+    n = nx * ny * nz
+    codebook = np.zeros((n, 4), np.int32)
+    codebook[:, 0] = rng.integers(0, ntemplates, n)
+    codebook[:, 1] = rng.integers(0, nbins, n)
+    codebook[:, 2] = rng.integers(0, 2, n)
+    codebook[:, 3] = rng.integers(0, min(4, slots) + 1, n)
+    errors = np.zeros((n, slots, 2), np.float32)
+    errors[:, :, 0] = rng.integers(0, nbins, (n, slots))
+    errors[:, :, 1] = rng.uniform(-0.08, 0.08, (n, slots)).astype(np.float32)
+    return (codebook.reshape(nz, ny, nx, 4), templates, errors.reshape(nz, ny, nx, slots, 2))
 
 
 def _fp(a):

@@ -158,6 +158,7 @@ typedef struct {
     int nx, ny, nz, nb;
     float enorm;
     uint64_t *mark; /* optional footprint bitset */
+    const orc_codec *codec; /* methods 4/5/6 */
 } vol_t;
 
 static inline const float *rec_at(const vol_t *v, int x, int y, int z) {
@@ -168,6 +169,63 @@ static inline const float *rec_at(const vol_t *v, int x, int y, int z) {
 static inline void mark_voxel(const vol_t *v, int x, int y, int z) {
     size_t idx = ((size_t)z * (size_t)v->ny + (size_t)y) * (size_t)v->nx + (size_t)x;
     __atomic_fetch_or(&v->mark[idx >> 6], (uint64_t)1 << (idx & 63), __ATOMIC_RELAXED);
+}
+
+/* Fractal/template codec record (d_basicDataProcessing K:775-871 with
+ * fractalDecoding K:195-222), restated with these choices for the reference's
+ * undefined behaviour: fractalDecoding's result is the decoded array (K:221
+ * returns a pointer to a local), error entries whose bin id is outside
+ * [0, nbins) are skipped (K:810 admits == nbins, an out-of-bounds write), and
+ * the inputs are validated (template id, 0 <= shift < nbins, NE <= slots), so
+ * the wrap `m - nBins` of K:204-206 is exact. */
+void orc_codec_decode(const orc_codec *c, int nbins, size_t vidx, float *dec) {
+    const int32_t *cb = c->codebook + 4 * vidx;
+    const int tid = cb[0], shift = cb[1], flip = cb[2] != 0, ne = cb[3];
+    const float *orig = c->templates + (size_t)tid * (size_t)nbins;
+    for (int i = 0; i < nbins; i++) { /* K:199-219 */
+        int m = i + shift;
+        if (m >= nbins) m = m - nbins;
+        dec[m] = flip ? orig[nbins - 1 - i] : orig[i];
+    }
+    const float *err = c->errors + 2 * vidx * (size_t)c->err_slots;
+    for (int j = 0; j < ne; j++) { /* K:805-823 */
+        int idx = (int)err[2 * j];
+        if (idx < 0 || idx >= nbins) continue;
+        dec[idx] = dec[idx] + err[2 * j + 1];
+        if (dec[idx] < 0) dec[idx] = 0;
+    }
+    float total = 0.0f; /* K:826-835 */
+    for (int i = 0; i < nbins; i++) total = total + dec[i];
+    for (int i = 0; i < nbins; i++)
+        if (total > 0) dec[i] = dec[i] / total;
+}
+
+/* statistics of a decoded codec record, K:837-868: the bin centre is used in
+ * both mean and variance (unlike K:750-755) */
+static void codec_stats3(const orc_codec *c, int nbins, float enorm, size_t vidx, float out[3]) {
+    float dec[256];
+    orc_codec_decode(c, nbins, vidx, dec);
+    const float bw = bin_width(nbins);
+    float mean = raw_mean(dec, nbins);
+    float var = 0.0f;
+    for (int i = 0; i < nbins; i++) {
+        double d = ((double)(bw * (float)i) + (double)bw / 2.0) - (double)mean;
+        var = (float)((double)var + (double)dec[i] * d * d);
+    }
+    out[0] = (float)((double)mean / 0.0217);
+    out[1] = (float)((double)var / 0.000021);
+    float ent = 0.0f;
+    for (int i = 0; i < nbins; i++) {
+        float pr = dec[i];
+        double t = pr <= 0 ? 0.0 : ((double)logf_cr(pr) / LN2_D);
+        ent = (float)((double)ent + (double)pr * t);
+    }
+    ent = -ent;
+    out[2] = ent / enorm;
+}
+
+void orc_codec_stats(const orc_codec *c, int nbins, size_t vidx, float out[3]) {
+    codec_stats3(c, nbins, entropy_norm(nbins), vidx, out);
 }
 
 /* methods 1/2/3: tex3D(originalQueryTex, p) with hardware trilinear (K:601, 619,
@@ -188,8 +246,24 @@ static float sample_stat(const vol_t *v, f3 pos, int comp) {
         mark_voxel(v, x0, y0, z1); mark_voxel(v, x1, y0, z1);
         mark_voxel(v, x0, y1, z1); mark_voxel(v, x1, y1, z1);
     }
-    const int want = comp == 0 ? 1 : (comp == 1 ? 3 : 4);
     float s[8][3];
+    if (comp >= 3) { /* methods 4/5/6: fractalQueryTex, K:639-652 */
+        const int xs[2] = {x0, x1}, ys[2] = {y0, y1}, zs[2] = {z0, z1};
+        for (int j = 0; j < 8; j++) {
+            size_t idx = ((size_t)zs[j >> 2] * (size_t)v->ny + (size_t)ys[(j >> 1) & 1]) *
+                             (size_t)v->nx + (size_t)xs[j & 1];
+            codec_stats3(v->codec, v->nb, v->enorm, idx, s[j]);
+        }
+        comp -= 3;
+        float c00 = lerpq(s[0][comp], s[1][comp], ax);
+        float c10 = lerpq(s[2][comp], s[3][comp], ax);
+        float c01 = lerpq(s[4][comp], s[5][comp], ax);
+        float c11 = lerpq(s[6][comp], s[7][comp], ax);
+        float c0 = lerpq(c00, c10, ay);
+        float c1 = lerpq(c01, c11, ay);
+        return lerpq(c0, c1, az);
+    }
+    const int want = comp == 0 ? 1 : (comp == 1 ? 3 : 4);
     stats3(rec_at(v, x0, y0, z0), v->nb, v->enorm, want, s[0]);
     stats3(rec_at(v, x1, y0, z0), v->nb, v->enorm, want, s[1]);
     stats3(rec_at(v, x0, y1, z0), v->nb, v->enorm, want, s[2]);
@@ -315,6 +389,8 @@ static int render_pixel(const vol_t *v, const orc_render_params *p, int x, int y
             sample = sample_stat(v, pos, 1);
         } else if (method == 3) {
             sample = sample_stat(v, pos, 2);
+        } else if (method >= 4 && method <= 6 && v->codec) {
+            sample = sample_stat(v, pos, method - 1);
         }
         n = i + 1;
         float col[4];
@@ -377,7 +453,16 @@ static void run_rows(const vol_t *v, const orc_render_params *p, uint32_t *out,
 int64_t orc_render(const float *vol, int nx, int ny, int nz, int nbins,
                    const orc_render_params *p, uint32_t *out, float *out_f,
                    int32_t *out_n, int row_start, int row_stride, int nthreads) {
-    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), NULL};
+    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), NULL, NULL};
+    int64_t total = 0;
+    run_rows(&v, p, out, out_f, out_n, row_start, row_stride, nthreads, &total);
+    return total;
+}
+
+int64_t orc_render_codec(const orc_codec *codec, int nx, int ny, int nz, int nbins,
+                         const orc_render_params *p, uint32_t *out, float *out_f,
+                         int32_t *out_n, int row_start, int row_stride, int nthreads) {
+    vol_t v = {NULL, nx, ny, nz, nbins, entropy_norm(nbins), NULL, codec};
     int64_t total = 0;
     run_rows(&v, p, out, out_f, out_n, row_start, row_stride, nthreads, &total);
     return total;
@@ -389,7 +474,7 @@ int64_t orc_count_footprint(const float *vol, int nx, int ny, int nz, int nbins,
     size_t nwords = (nvox + 63) / 64;
     uint64_t *mark = (uint64_t *)calloc(nwords, sizeof(uint64_t));
     if (!mark) return -1;
-    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), mark};
+    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), mark, NULL};
     int64_t total = 0;
     run_rows(&v, p, NULL, NULL, NULL, 0, 1, nthreads, &total);
     int64_t u = 0;

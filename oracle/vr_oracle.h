@@ -15,6 +15,7 @@
 #ifndef VR_ORACLE_H
 #define VR_ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -30,6 +31,30 @@ typedef struct {
     int   query_method;           /* 1 mean, 2 variance, 3 entropy, 7 interp   */
     int   m7_dims[3];             /* render_kernel's volumeSize (K:2399)        */
 } orc_render_params;
+
+/* Fractal/template codec (methods 4/5/6), the initCuda arrays of K:1893-1900:
+ * codebook: 4 int32 per voxel (template id, shift, flip, NE), voxel order
+ *           x + X*(y + Y*z) (C:620, K:777);
+ * templates: ntemplates x nbins floats (C:657-675, K:792-793);
+ * errors: err_slots (bin id, value) float pairs per voxel, NE used (C:626-641,
+ *         K:805-807). */
+typedef struct {
+    const int32_t *codebook;
+    const float *templates;
+    int ntemplates;
+    const float *errors;
+    int err_slots;
+} orc_codec;
+
+/* decoded, error-corrected, normalised histogram of voxel vidx (K:775-835) */
+void orc_codec_decode(const orc_codec *c, int nbins, size_t vidx, float *dec);
+/* its mean / variance / entropy as the fractal pre-pass computes them (K:837-868) */
+void orc_codec_stats(const orc_codec *c, int nbins, size_t vidx, float out[3]);
+
+/* orc_render for methods 4/5/6 from a codec-encoded volume */
+int64_t orc_render_codec(const orc_codec *codec, int nx, int ny, int nz, int nbins,
+                         const orc_render_params *p, uint32_t *out, float *out_f,
+                         int32_t *out_n, int row_start, int row_stride, int nthreads);
 
 /* statistic of one B-bin record: d_basicDataProcessing K:736-773 */
 void orc_record_stats(const float *rec, int nbins, float out[3]);

@@ -170,14 +170,15 @@ def _render(vol, W, H, m, method, density, brightness, toff, tscale, m7_dims, fo
             m1 = bl(m01, m11, yd)
             sample = bl(m0, m1, zd) * f32(50)
         else:
-            comp = method - 1
+            comp = method - 1 if method <= 3 else method - 4
+            sfun = stat if method <= 3 else codec_stat  # 4/5/6: vol = codec_decode(...)
             ax = [_lin(pos[k] * f32(0.5) + f32(0.5), dims[k]) for k in range(3)]
             vals = []
             for j in range(8):
                 xi = ax[0][1] if j & 1 else ax[0][0]
                 yi = ax[1][1] if j & 2 else ax[1][0]
                 zi = ax[2][1] if j & 4 else ax[2][0]
-                vals.append(stat(vol[zi, yi, xi], comp))
+                vals.append(sfun(vol[zi, yi, xi], comp))
                 if footprint is not None:
                     flat = (zi * ny + yi) * nx + xi
                     footprint.update(np.unique(flat[active]).tolist())
@@ -209,3 +210,44 @@ def pack(rgba):
     c = np.where(r > 0, np.where(r > 1, f32(1), r), f32(0))
     q = (c * f32(255)).astype(np.uint32)
     return (q[..., 3] << 24) | (q[..., 2] << 16) | (q[..., 1] << 8) | q[..., 0]
+
+
+# ---- fractal/template codec, methods 4/5/6 (K:195-222, 775-871) ----
+
+def codec_decode(codebook, templates, errors):
+    """codebook int32 (..., 4), templates float32 (T, B), errors float32 (..., E, 2)
+    -> decoded, error-corrected, normalised histograms float32 (..., B)"""
+    nb = templates.shape[1]
+    tid, shift, flip, ne = (codebook[..., k] for k in range(4))
+    orig = templates[tid]                                     # (..., B)
+    src = np.where(flip[..., None] != 0, orig[..., ::-1], orig)
+    idx = (np.arange(nb) - shift[..., None]) % nb             # dec[m] = src[m - shift]
+    dec = np.take_along_axis(src, idx, axis=-1).astype(np.float32)
+    for j in range(errors.shape[-2]):
+        use = j < ne
+        b = errors[..., j, 0].astype(np.int64)
+        ok = use & (b >= 0) & (b < nb)
+        bb = np.where(ok, b, 0)
+        cur = np.take_along_axis(dec, bb[..., None], axis=-1)[..., 0]
+        new = cur + errors[..., j, 1]
+        new = np.where(new < 0, f32(0), new)
+        np.put_along_axis(dec, bb[..., None], np.where(ok, new, cur)[..., None], axis=-1)
+    total = np.zeros(dec.shape[:-1], np.float32)
+    for i in range(nb):
+        total = total + dec[..., i]
+    return np.where(total[..., None] > 0, dec / total[..., None], dec).astype(np.float32)
+
+
+def codec_stat(dec, comp):
+    """K:837-868: bin centre in both mean and variance"""
+    nb = dec.shape[-1]
+    if comp != 1:
+        return stat(dec, comp)
+    bw = _bw(nb)
+    mean = raw_mean(dec)
+    var = np.zeros_like(mean)
+    for i in range(nb):
+        c = np.float64(bw * f32(i)) + np.float64(bw) / 2.0
+        d = c - mean.astype(np.float64)
+        var = (var.astype(np.float64) + dec[..., i].astype(np.float64) * d * d).astype(np.float32)
+    return (var.astype(np.float64) / 0.000021).astype(np.float32)

@@ -209,6 +209,7 @@ def test_tile_split_and_unscatter(pkg, orc, gpu, world):
 
 def test_errors_do_not_exit(pkg, gpu):
     import torch
+    pkg.freeCudaBuffers()  # no codec volume resident either
     vol = np.zeros((4, 4, 4, 2), np.float32)
     pkg.init_distribution(vol)
     out = torch.zeros(16, dtype=torch.int32, device="cuda")
@@ -268,3 +269,69 @@ def test_fast_log_is_exact_for_every_float(pkg, gpu):
     assert L.vr_selftest_logf(counts) == 0, L.vr_last_error()
     assert counts[0] == 0, f"{counts[0]} floats differ"
     assert counts[1] < 1 << 16, f"{counts[1]} fallbacks"
+
+
+# ---- methods 4/5/6: fractal/template codec ----
+
+def codec_render(pkg, W, H, m, method, torch):
+    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    out_f = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+    steps = torch.full((H * W,), -2, dtype=torch.int32, device="cuda")
+    d = pkg.make_desc(out, W, H, m, query_method=method, volume_size=(1, 1, 1), d_output_f=out_f,
+                      d_steps=steps)
+    pkg.render(d)
+    torch.cuda.synchronize()
+    return (out.cpu().numpy().view(np.uint32).reshape(H, W),
+            out_f.cpu().numpy().reshape(H, W, 4), steps.cpu().numpy().reshape(H, W))
+
+
+@pytest.mark.parametrize("method", [4, 5, 6])
+@pytest.mark.parametrize("nb", [4, 8, 32])
+def test_codec_methods(pkg, orc, gpu, method, nb):
+    import torch
+    cb, t, e = orc.synth_codec(22, 18, 14, nb, seed=nb + method)
+    pkg.init_codec(cb, t, e)
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view()):
+        got = codec_render(pkg, 72, 56, cam, method, torch)
+        ref = orc.render_codec(cb, t, e, orc.make_params(72, 56, cam, query_method=method))[:3]
+        assert_parity(got, ref, f"codec nb={nb} m{method}")
+    assert pkg.last_kernel().startswith("k_march_codec")
+
+
+def test_codec_via_reference_initCuda(pkg, orc, gpu):
+    """the reference's own shapes: 50x50x10 voxels, 32 bins, templatesSize (32, T, 1),
+    errorsbookSize (32, 2500, 10) -- initCuda with all codec arrays, then render_kernel
+    with queryMethod 4/5/6 (C:1200-1203, K:1893-2050)"""
+    import torch
+    cb, t, e = orc.synth_codec(50, 50, 10, 32, ntemplates=40, seed=9)
+    vol = orc.synth_volume(50, 50, 10, 32)
+    pkg.initCuda(vol.reshape(-1), (50, 50, 10), (32, 2500, 10), cb.reshape(-1, 4), (50, 50, 10),
+                 t, (32, 40, 1), e.reshape(-1, 2), (32, 2500, 10))
+    m = pkg.camera.single_test_inv_view()
+    pkg.copyInvViewMatrix(m, 48)
+    W = H = 128
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    for method in (4, 5, 6):
+        out.zero_()
+        pkg.render_kernel((W // 16, H // 16, 1), (16, 16, 1), out, W, H, 0.05, 1.0, 0.0, 1.0,
+                          method, (50, 50, 10))
+        torch.cuda.synchronize()
+        ref = orc.render_codec(cb, t, e, orc.make_params(W, H, m, query_method=method))[0]
+        assert np.array_equal(out.cpu().numpy().view(np.uint32).reshape(H, W), ref), method
+    # methods 1/2/3 still read the raw histograms
+    out.zero_()
+    pkg.render_kernel((W // 16, H // 16, 1), (16, 16, 1), out, W, H, 0.05, 1.0, 0.0, 1.0, 1,
+                      (50, 50, 10))
+    torch.cuda.synchronize()
+    ref = orc.render(vol, orc.make_params(W, H, m, query_method=1))[0]
+    assert np.array_equal(out.cpu().numpy().view(np.uint32).reshape(H, W), ref)
+
+
+def test_codec_validation(pkg, orc, gpu):
+    cb, t, e = orc.synth_codec(6, 5, 4, 8)
+    for field, value in ((0, 24), (1, 8), (1, -1), (3, 9)):
+        bad = cb.copy()
+        bad[1, 2, 3, field] = value
+        with pytest.raises(pkg.VRError):
+            pkg.init_codec(bad, t, e)
+    pkg.init_codec(cb[..., :4], t, e)  # the unmodified volume is accepted

@@ -180,3 +180,66 @@ def test_golden_fixture(orc, path):
     assert np.array_equal(n, z["steps"].astype(np.int32))
     if "rgba_f" in z.files:
         assert np.array_equal(f, z["rgba_f"])
+
+
+# ---- fractal/template codec (methods 4/5/6) ----
+
+def test_codec_decode_known_answers(orc):
+    """flip -> circular shift -> sparse errors (clamped at 0) -> renormalise (K:195-222,
+    775-835), on one-hot and ramp templates"""
+    B = 8
+    templates = np.zeros((2, B), np.float32)
+    templates[0, 2] = 1.0
+    templates[1] = np.arange(1, B + 1, dtype=np.float32) / 36.0
+    errors = np.zeros((1, 1, 1, B, 2), np.float32)
+    cb = np.array([[[[0, 3, 0, 0]]]], np.int32)
+    assert np.argmax(orc.codec_decode(cb, templates, errors, 0)) == 5      # 2 + 3
+    cb[..., 2] = 1
+    assert np.argmax(orc.codec_decode(cb, templates, errors, 0)) == (B - 1 - 2 + 3) % B
+    cb[:] = [1, 0, 1, 0]                                                    # reversed ramp
+    d = orc.codec_decode(cb, templates, errors, 0)
+    assert np.allclose(d, templates[1][::-1]) and d[0] > d[-1]
+    # errors: +0.5 on bin 0, then -1 on bin 7 (clamped to 0), renormalised
+    cb[:] = [1, 0, 0, 2]
+    errors[0, 0, 0, 0] = [0, 0.5]
+    errors[0, 0, 0, 1] = [7, -1.0]
+    d = orc.codec_decode(cb, templates, errors, 0)
+    expect = templates[1].copy()
+    expect[0] += np.float32(0.5)
+    expect[7] = 0
+    tot = np.float32(0)
+    for v in expect:
+        tot = np.float32(tot + v)
+    assert np.array_equal(d, (expect / tot).astype(np.float32))
+    assert abs(float(d.sum()) - 1.0) < 1e-6
+    # an error bin id of nBins (admitted by K:810) is skipped
+    errors[0, 0, 0, 1] = [B, -1.0]
+    d2 = orc.codec_decode(cb, templates, errors, 0)
+    assert d2[7] > 0
+
+
+@pytest.mark.parametrize("nb", [4, 8, 32])
+def test_codec_matches_numpy(orc, nb):
+    """decode and statistics bit-identical to the independent numpy restatement"""
+    import ref_numpy as R
+    cb, t, e = orc.synth_codec(7, 6, 5, nb, seed=nb)
+    dec = R.codec_decode(cb, t, e)
+    for vidx in range(0, 7 * 6 * 5, 13):
+        assert np.array_equal(orc.codec_decode(cb, t, e, vidx), dec.reshape(-1, nb)[vidx])
+        s = orc.codec_stats(cb, t, e, vidx)
+        d1 = dec.reshape(-1, nb)[vidx:vidx + 1]
+        for comp in range(3):
+            assert np.array_equal(s[comp], R.codec_stat(d1, comp)[0]), (vidx, comp)
+
+
+@pytest.mark.parametrize("method", [4, 5, 6])
+@pytest.mark.parametrize("cam", ["C0", "C1"])
+def test_codec_render_matches_numpy(orc, cams, method, cam):
+    import ref_numpy as R
+    cb, t, e = orc.synth_codec(12, 10, 9, 8, seed=3)
+    W, H = 40, 32
+    f, n = R.render(R.codec_decode(cb, t, e), W, H, cams[cam], method)
+    o8, of, on, _ = orc.render_codec(cb, t, e, orc.make_params(W, H, cams[cam], query_method=method))
+    assert np.array_equal(n, on)
+    assert np.array_equal(f, of)
+    assert np.array_equal(np.where(n >= 0, R.pack(f), 0), o8)

@@ -70,16 +70,53 @@ def copyInvViewMatrix(invViewMatrix, sizeofMatrix: int = 48) -> None:
     check_last()
 
 
-def initCuda(h_histogram, volumeSize, histogramSize, *codec_and_flexible_arrays) -> None:
+def initCuda(h_histogram, volumeSize, histogramSize, h_codebook=None, codebookSize=None,
+             h_templates=None, templatesSize=None, h_errorsbook=None, errorsbookSize=None,
+             *flexible_arrays) -> None:
     """initCuda, K:1893-2358.  h_histogram: host fp32 array of B-bin records in
-    AoS order (record = x + X*(y + Y*z)); the remaining 15 reference arguments
-    (codebook/templates/flexible-block arrays) are accepted and ignored."""
+    AoS order (record = x + X*(y + Y*z)).  h_codebook (int32 [..., 4]),
+    h_templates (fp32 [T, B]) and h_errorsbook (fp32 [..., slots, 2]) make the
+    codec volume of methods 4/5/6 resident (sizes as the reference passes them:
+    codebookSize = volumeSize, templatesSize = (B, T, 1), errorsbookSize =
+    (slots, rows, layers)); the flexible-block arrays are accepted and ignored."""
     h = np.ascontiguousarray(np.asarray(h_histogram, dtype=np.float32))
     L = _lib.load()
     z = Extent(0, 0, 0)
-    L.initCuda(h.ctypes.data, _extent(volumeSize), _extent(histogramSize), None, z, None, z,
-               None, z, None, None, None, None, None, None, None, None, None)
+    keep = []
+
+    def arr(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+        keep.append(a)
+        return a.ctypes.data
+
+    L.initCuda(h.ctypes.data, _extent(volumeSize), _extent(histogramSize),
+               arr(h_codebook, np.int32), _extent(codebookSize) if codebookSize else z,
+               arr(h_templates, np.float32), _extent(templatesSize) if templatesSize else z,
+               arr(h_errorsbook, np.float32), _extent(errorsbookSize) if errorsbookSize else z,
+               None, None, None, None, None, None, None, None, None)
     check_last()
+
+
+def init_codec(codebook, templates, errors) -> None:
+    """Make a fractal/template codec volume resident (methods 4/5/6).
+    codebook int32 (nz, ny, nx, 4) = (template id, shift, flip, NE); templates fp32
+    (T, B); errors fp32 (nz, ny, nx, slots, 2) = (bin id, value).  Host numpy arrays
+    or CUDA tensors (copied)."""
+    L = _lib.load()
+    if hasattr(codebook, "data_ptr") and getattr(codebook, "is_cuda", False):
+        nz, ny, nx, _ = codebook.shape
+        check(L.vr_init_codec(_ptr(codebook), _extent((nx, ny, nz)), _ptr(templates),
+                              int(templates.shape[0]), _ptr(errors), int(errors.shape[-2]),
+                              int(templates.shape[1]), 1))
+        return
+    cb = np.ascontiguousarray(codebook, dtype=np.int32)
+    tp = np.ascontiguousarray(templates, dtype=np.float32)
+    er = np.ascontiguousarray(errors, dtype=np.float32)
+    nz, ny, nx, _ = cb.shape
+    check(L.vr_init_codec(cb.ctypes.data, _extent((nx, ny, nz)), tp.ctypes.data, tp.shape[0],
+                          er.ctypes.data, er.shape[-2], tp.shape[1], 0))
 
 
 def freeCudaBuffers() -> None:
@@ -206,7 +243,8 @@ def version() -> str:
 
 __all__ = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers", "setTextureFilterMode",
-    "basicDataProcessing", "dataProcessing", "init_distribution", "synthesize", "volume_info",
+    "basicDataProcessing", "dataProcessing", "init_distribution", "init_codec", "synthesize",
+    "volume_info",
     "volume_layout",
     "set_stream", "make_desc", "render", "count_footprint", "unscatter_tiles", "last_kernel", "version",
     "VRError", "PAD",

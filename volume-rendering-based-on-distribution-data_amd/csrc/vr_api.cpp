@@ -27,6 +27,11 @@ struct State {
     bool linear_filter = false;     // tex.filterMode = point after initCuda (K:2163)
     std::string err;
     int status = VR_OK;
+    // fractal/template codec volume (methods 4/5/6)
+    int4 *cb = nullptr;
+    float *tpl = nullptr;
+    float2 *cerr = nullptr;
+    int cnx = 0, cny = 0, cnz = 0, cnb = 0, ntpl = 0, err_slots = 0;
     // full-frame workgroup -> tile order (frame_order), cached per frame shape
     uint32_t *perm = nullptr;
     size_t perm_cap = 0;
@@ -90,11 +95,18 @@ float entropy_norm(int nb) {
 uint32_t tiles_x(uint32_t w) { return (w + vr::kTileW - 1) / vr::kTileW; }
 uint32_t tiles_y(uint32_t h) { return (h + vr::kTileH - 1) / vr::kTileH; }
 
+void release_codec() {
+    if (g.cb) (void)hipFree(g.cb);
+    if (g.tpl) (void)hipFree(g.tpl);
+    if (g.cerr) (void)hipFree(g.cerr);
+    g.cb = nullptr;
+    g.tpl = nullptr;
+    g.cerr = nullptr;
+    g.cnx = g.cny = g.cnz = g.cnb = g.ntpl = g.err_slots = 0;
+}
+
 int check_method(int m) {
-    if (m == 1 || m == 2 || m == 3 || m == 7) return VR_OK;
-    if (m == 4 || m == 5 || m == 6)
-        return fail(VR_ERR_UNSUPPORTED,
-                    "queryMethod %d needs the fractal/template codec (out of scope)", m);
+    if (m == 1 || m == 2 || m == 3 || m == 7 || m == 4 || m == 5 || m == 6) return VR_OK;
     if (m == 8 || m == 9 || m == 0)
         return fail(VR_ERR_UNSUPPORTED,
                     "queryMethod %d needs the flexible-block pre-pass (out of scope)", m);
@@ -199,7 +211,11 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
 
 int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     if (!d) return fail(VR_ERR_ARG, "null render descriptor");
-    if (!g.vol) return fail(VR_ERR_STATE, "no volume resident (initCuda / vr_init_* first)");
+    const bool codec = d->query_method >= 4 && d->query_method <= 6;
+    if (codec && !g.cb)
+        return fail(VR_ERR_STATE, "queryMethod %d needs a codec volume (initCuda's codebook / "
+                                  "vr_init_codec)", d->query_method);
+    if (!codec && !g.vol) return fail(VR_ERR_STATE, "no volume resident (initCuda / vr_init_* first)");
     if (!d->d_output) return fail(VR_ERR_ARG, "d_output is null");
     if (d->width == 0 || d->height == 0) return fail(VR_ERR_ARG, "empty image");
     int rc = check_method(d->query_method);
@@ -215,13 +231,25 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     P.brightness = d->brightness;
     P.toff = d->transfer_offset;
     P.tscale = d->transfer_scale;
-    P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
-    P.sy = g.sy; P.sz = g.sz;
+    if (codec) {  // the codec volume: dense voxel order, its own bin count
+        P.nx = g.cnx; P.ny = g.cny; P.nz = g.cnz;
+        P.sy = (uint64_t)g.cnx;
+        P.sz = (uint64_t)g.cnx * (uint64_t)g.cny;
+        P.nb = g.cnb;
+        P.cb = g.cb;
+        P.tpl = g.tpl;
+        P.err = g.cerr;
+        P.ntpl = g.ntpl;
+        P.err_slots = g.err_slots;
+    } else {
+        P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
+        P.sy = g.sy; P.sz = g.sz;
+        P.nb = g.nb;
+    }
     P.m7x = (int)d->volume_size.width;
     P.m7y = (int)d->volume_size.height;
     P.m7z = (int)d->volume_size.depth;
-    P.enorm = entropy_norm(g.nb);
-    P.nb = g.nb;
+    P.enorm = entropy_norm(P.nb);
     P.tiles_x = tiles_x(d->width);
     P.tile_list = d->d_tile_list;
     P.perm = nullptr;
@@ -332,6 +360,53 @@ uint32_t vr_tiles_y(uint32_t height) { return tiles_y(height); }
 
 int vr_set_stream(void *stream) {
     g.stream = (hipStream_t)stream;
+    return VR_OK;
+}
+
+int vr_init_codec(const vr_int4 *codebook, vr_extent dims, const float *templates,
+                  int ntemplates, const vr_float2 *errors, int err_slots, int nbins, int where) {
+    if (!codebook || !templates || (!errors && err_slots > 0))
+        return fail(VR_ERR_ARG, "vr_init_codec: null array");
+    if (where != 0 && where != 1) return fail(VR_ERR_ARG, "vr_init_codec: where must be 0 or 1");
+    if (dims.width == 0 || dims.height == 0 || dims.depth == 0 || nbins <= 0 ||
+        ntemplates <= 0 || err_slots < 0 || dims.width > 65535 || dims.height > 65535 ||
+        dims.depth > 65535)
+        return fail(VR_ERR_ARG, "vr_init_codec: bad sizes");
+    if (nbins != 1 && nbins != 2 && nbins != 4 && nbins != 8 && nbins != 16 && nbins != 32)
+        return fail(VR_ERR_UNSUPPORTED, "vr_init_codec: %d bins (compiled: 1,2,4,8,16,32)", nbins);
+    const uint64_t nvox = (uint64_t)dims.width * dims.height * dims.depth;
+    release_codec();
+    const hipMemcpyKind kind = where == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    const size_t bcb = nvox * sizeof(int4), btp = (size_t)ntemplates * nbins * sizeof(float);
+    const size_t ber = nvox * (size_t)err_slots * sizeof(float2);
+    VR_HIP(hipMalloc(&g.cb, bcb));
+    VR_HIP(hipMalloc(&g.tpl, btp));
+    if (ber) VR_HIP(hipMalloc(&g.cerr, ber));
+    hipError_t e = hipMemcpy(g.cb, codebook, bcb, kind);
+    if (e == hipSuccess) e = hipMemcpy(g.tpl, templates, btp, kind);
+    if (e == hipSuccess && ber) e = hipMemcpy(g.cerr, errors, ber, kind);
+    unsigned long long *bad = nullptr, hbad = 0;
+    if (e == hipSuccess) e = hipMalloc(&bad, sizeof hbad);
+    if (e == hipSuccess) e = hipMemset(bad, 0, sizeof hbad);
+    if (e == hipSuccess) e = vr::launch_codec_check(g.cb, nvox, ntemplates, nbins, err_slots, bad, 0);
+    if (e == hipSuccess) e = hipMemcpy(&hbad, bad, sizeof hbad, hipMemcpyDeviceToHost);
+    if (bad) (void)hipFree(bad);
+    if (e != hipSuccess) {
+        release_codec();
+        return hip_fail(e, "vr_init_codec");
+    }
+    if (hbad) {
+        release_codec();
+        return fail(VR_ERR_ARG,
+                    "vr_init_codec: %llu codebook entries out of range (template id < %d, "
+                    "0 <= shift < %d, 0 <= NE <= %d)", hbad, ntemplates, nbins, err_slots);
+    }
+    g.cnx = (int)dims.width;
+    g.cny = (int)dims.height;
+    g.cnz = (int)dims.depth;
+    g.cnb = nbins;
+    g.ntpl = ntemplates;
+    g.err_slots = err_slots;
     return VR_OK;
 }
 
@@ -486,7 +561,15 @@ int vr_render(const vr_render_desc *desc) {
     uint32_t nslots = 0;
     int rc = fill_params(desc, P, nslots);
     if (rc != VR_OK) return rc;
-    hipError_t e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
+    hipError_t e;
+    if (desc->query_method >= 4 && desc->query_method <= 6) {
+        e = vr::launch_march_codec(P.nb, desc->query_method, P, nslots, g.stream);
+        if (e == hipErrorInvalidValue)
+            return fail(VR_ERR_UNSUPPORTED, "codec volumes with %d bins (compiled: 1,2,4,8,16,32)",
+                        P.nb);
+    } else {
+        e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
+    }
     if (e != hipSuccess) return hip_fail(e, "launch(k_march)");
     return VR_OK;
 }
@@ -496,7 +579,7 @@ int64_t vr_count_footprint(const vr_render_desc *desc) {
     uint32_t nslots = 0;
     int rc = fill_params(desc, P, nslots);
     if (rc != VR_OK) return rc;
-    if (desc->query_method == 7)
+    if (desc->query_method < 1 || desc->query_method > 3)
         return fail(VR_ERR_UNSUPPORTED, "footprint count is defined for methods 1/2/3");
     const uint64_t nvox = (uint64_t)g.nx * g.ny * g.nz;
     const uint64_t nwords = (nvox + 63) / 64;
@@ -568,12 +651,10 @@ void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
               vr_int4 *h_flexibleCodebook, vr_float2 *h_flexibleErrorsbook,
               vr_int4 *h_simpleLow, vr_int4 *h_simpleHigh, int *h_simpleCount,
               vr_float2 *h_simpleHistogram, float *h_flexibleTemplates) {
-    // arrays 4-18 feed the codec / flexible-block methods only (out of scope)
-    (void)h_codebook; (void)codebookSize; (void)h_templates; (void)templatesSize;
-    (void)h_errorsbook; (void)errorsbookSize; (void)h_codebookSpanLow;
-    (void)h_codebookSpanHigh; (void)h_flexibleCodebook; (void)h_flexibleErrorsbook;
-    (void)h_simpleLow; (void)h_simpleHigh; (void)h_simpleCount; (void)h_simpleHistogram;
-    (void)h_flexibleTemplates;
+    // arrays 10-18 feed the flexible-block methods 8/9/0 only (out of scope)
+    (void)h_codebookSpanLow; (void)h_codebookSpanHigh; (void)h_flexibleCodebook;
+    (void)h_flexibleErrorsbook; (void)h_simpleLow; (void)h_simpleHigh; (void)h_simpleCount;
+    (void)h_simpleHistogram; (void)h_flexibleTemplates;
     const size_t nvox = volumeSize.width * volumeSize.height * volumeSize.depth;
     if (histogramSize.width == 0 || histogramSize.height * histogramSize.depth != nvox) {
         fail(VR_ERR_ARG,
@@ -584,12 +665,28 @@ void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
         return;
     }
     if (vr_init_distribution((const float *)h_histogram, volumeSize, (int)histogramSize.width,
-                             0) == VR_OK)
-        g.linear_filter = false;
+                             0) != VR_OK)
+        return;
+    g.linear_filter = false;
+    // codec arrays (methods 4/5/6, K:1920-2050): codebook (X,Y,Z) int4, templates
+    // (nBins, nTemplates, layers) -- layer 0 is used, the reference reads layer 1
+    // of a 1-layer array (K:792-793) --, errorsbook (slots, rows, layers) with one
+    // row of `slots` (bin, error) pairs per voxel
+    if (h_codebook && h_templates && h_errorsbook) {
+        if (codebookSize.width != volumeSize.width || codebookSize.height != volumeSize.height ||
+            codebookSize.depth != volumeSize.depth || templatesSize.width != histogramSize.width ||
+            errorsbookSize.height * errorsbookSize.depth != nvox) {
+            fail(VR_ERR_ARG, "initCuda: codebook/templates/errorsbook sizes do not match the volume");
+            return;
+        }
+        (void)vr_init_codec(h_codebook, codebookSize, h_templates, (int)templatesSize.height,
+                            h_errorsbook, (int)errorsbookSize.width, (int)templatesSize.width, 0);
+    }
 }
 
 void freeCudaBuffers(void) {
     release_volume();
+    release_codec();
 }
 
 void setTextureFilterMode(bool bLinearFilter) { g.linear_filter = bLinearFilter; }

@@ -41,7 +41,13 @@ struct Params {
     unsigned long long *mark;    // footprint bitset (count mode only)
     int box_max;                 // LDS-staged footprint box capacity (voxels per wave), 0 = off
     int wg_per_cu;               // occupancy cap through the LDS request (0 = none)
-    int path;                    // 0 quad pipelined, 1 k_march, 2 per-ray pipelined
+    int path;                    // kernel variant (vr_api.cpp fill_params)
+    // fractal/template codec (methods 4/5/6): codebook int4 per voxel, templates
+    // [ntpl][nb], (bin, value) errors [voxel][err_slots]
+    const int4 *cb;
+    const float *tpl;
+    const float2 *err;
+    int ntpl, err_slots;
 };
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)
@@ -223,6 +229,66 @@ __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
         return (float)div_const((double)raw_variance<B>(p, mean), kVarD, kVarR);
     } else {
         return entropy<B>(p, enorm);
+    }
+}
+
+// ---- fractal/template codec, methods 4/5/6 (K:195-222, 775-871) ----
+// Decode of one codec voxel: template row, flipped and circularly shifted
+// (fractalDecoding, K:195-222), NE sparse errors added with a clamp at 0
+// (K:805-823; bin ids outside [0, B) skipped), renormalised (K:826-835).
+template <int B>
+__device__ __forceinline__ void codec_decode(const Params &P, uint64_t vidx, float (&dec)[B]) {
+    const int4 c = P.cb[vidx];
+    const float *row = P.tpl + (uint64_t)c.x * B;
+#pragma unroll
+    for (int m = 0; m < B; m++) {
+        int i = m - c.y;                    // dec[(i + shift) mod B] = src[i]
+        if (i < 0) i += B;
+        dec[m] = row[c.z ? B - 1 - i : i];
+    }
+    const float2 *e = P.err + vidx * (uint64_t)P.err_slots;
+    for (int j = 0; j < c.w; j++) {
+        const float2 ev = e[j];
+        const int idx = (int)ev.x;
+#pragma unroll
+        for (int m = 0; m < B; m++) {
+            if (m == idx) {
+                float v = dec[m] + ev.y;
+                if (v < 0) v = 0;
+                dec[m] = v;
+            }
+        }
+    }
+    float total = 0.0f;
+#pragma unroll
+    for (int i = 0; i < B; i++) total = total + dec[i];
+    if (total > 0) {
+#pragma unroll
+        for (int i = 0; i < B; i++) dec[i] = dec[i] / total;
+    }
+}
+
+// statistic C (0 mean, 1 variance, 2 entropy) of a codec voxel, K:837-868: the
+// bin centre is used in both mean and variance
+template <int B, int C>
+__device__ __forceinline__ float codec_stat(const Params &P, uint64_t vidx) {
+    float dec[B];
+    codec_decode<B>(P, vidx, dec);
+    if constexpr (C == 0) {
+        return (float)div_const((double)raw_mean<B>(dec), kMeanD, kMeanR);
+    } else if constexpr (C == 1) {
+        const float mean = raw_mean<B>(dec);
+        const float bw = bin_width(B);
+        const double half = (double)bw / 2.0;
+        float var = 0.0f;
+#pragma unroll
+        for (int i = 0; i < B; i++) {
+            const double d = ((double)(bw * (float)i) + half) - (double)mean;
+            var = (float)((double)var + (double)dec[i] * d * d);
+        }
+        return (float)div_const((double)var, kVarD, kVarR);
+    } else {
+        return entropy<B>(dec, P.enorm);
     }
 }
 

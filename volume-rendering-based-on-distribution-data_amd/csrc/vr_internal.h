@@ -29,6 +29,10 @@ const char *last_march_kernel();
 #ifdef VR_WG_PROF
 hipError_t wg_prof_read(unsigned long long *host);   // tooling build only
 #endif
+hipError_t launch_march_codec(int nb, int method, const Params &P, uint32_t nslots,
+                              hipStream_t s);
+hipError_t launch_codec_check(const int4 *cb, uint64_t n, int ntpl, int nb, int slots,
+                              unsigned long long *bad, hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,

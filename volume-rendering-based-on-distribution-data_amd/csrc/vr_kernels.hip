@@ -47,6 +47,14 @@ __device__ __forceinline__ uint32_t tile_of(const Params &P, uint32_t slot) {
     return slot;
 }
 
+static char g_last_kernel[64] = "";
+
+static void note_kernel(const char *kind, int B, int method) {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "%s<B=%d,M=%d>", kind, B, method);
+}
+
+const char *last_march_kernel() { return g_last_kernel; }
+
 struct Ray {
     float ox, oy, oz, dx, dy, dz, tnear, tfar;
 };
@@ -1224,6 +1232,112 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
                                    (j & 4) ? m.cz : m.fz);
 }
 
+// ---- methods 4/5/6: fractal/template codec volume ----
+// The reference pre-bakes the decoded statistics into fractalQueryTex
+// (K:775-871) and samples it with the texture trilinear (K:639-652); here, as
+// for methods 1/2/3, each of the 8 corners is decoded from its codebook entry,
+// template and sparse errors at every step and blended with the quantised
+// weights.  One lane per ray.
+template <int B, int C>
+__global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ unused, Params P) {
+    (void)unused;
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    uint32_t lx, ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    if (x >= P.W || y >= P.H) return;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    if (!make_ray(P, x, y, r)) {
+        if (P.out_n) P.out_n[o] = -1;
+        return;
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    for (int i = 0; i < kMaxSteps; i++) {
+        const Foot f = footprint(P, px, py, pz);
+        const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
+        const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
+        const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
+        const uint64_t r11 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y1 * P.sy;
+        float sv[8];
+        sv[0] = codec_stat<B, C>(P, r00 + f.x0);
+        sv[1] = codec_stat<B, C>(P, r00 + f.x1);
+        sv[2] = codec_stat<B, C>(P, r10 + f.x0);
+        sv[3] = codec_stat<B, C>(P, r10 + f.x1);
+        sv[4] = codec_stat<B, C>(P, r01 + f.x0);
+        sv[5] = codec_stat<B, C>(P, r01 + f.x1);
+        sv[6] = codec_stat<B, C>(P, r11 + f.x0);
+        sv[7] = codec_stat<B, C>(P, r11 + f.x1);
+        n = i + 1;
+        if (composite(P, blend8(sv, f), sx, sy, sz, sw)) break;
+        t = t + kTStep;
+        if (t > r.tfar) break;
+        px = px + stx;
+        py = py + sty;
+        pz = pz + stz;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
+template <int B>
+static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream_t s) {
+    const dim3 grid(nslots), block(256);
+    note_kernel("k_march_codec", B, method);
+    switch (method) {
+    case 4: hipLaunchKernelGGL((k_march_codec<B, 0>), grid, block, 0, s, nullptr, P); break;
+    case 5: hipLaunchKernelGGL((k_march_codec<B, 1>), grid, block, 0, s, nullptr, P); break;
+    case 6: hipLaunchKernelGGL((k_march_codec<B, 2>), grid, block, 0, s, nullptr, P); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_march_codec(int nb, int method, const Params &P, uint32_t nslots,
+                              hipStream_t s) {
+    if (nslots == 0) return hipSuccess;
+    switch (nb) {
+    case 1: return march_codec_b<1>(method, P, nslots, s);
+    case 2: return march_codec_b<2>(method, P, nslots, s);
+    case 4: return march_codec_b<4>(method, P, nslots, s);
+    case 8: return march_codec_b<8>(method, P, nslots, s);
+    case 16: return march_codec_b<16>(method, P, nslots, s);
+    case 32: return march_codec_b<32>(method, P, nslots, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// Codec validation: counts codebook entries the decode cannot take (template
+// id outside [0, ntpl), shift outside [0, nb), NE outside [0, err_slots]).
+__global__ __launch_bounds__(256) void k_codec_check(const int4 *__restrict__ cb, uint64_t n,
+                                                     int ntpl, int nb, int slots,
+                                                     unsigned long long *bad) {
+    unsigned long long b = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        const int4 c = cb[i];
+        b += c.x < 0 || c.x >= ntpl || c.y < 0 || c.y >= nb || c.w < 0 || c.w > slots;
+    }
+    if (b) atomicAdd(bad, b);
+}
+
+hipError_t launch_codec_check(const int4 *cb, uint64_t n, int ntpl, int nb, int slots,
+                              unsigned long long *bad, hipStream_t s) {
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_codec_check, dim3((uint32_t)blocks), dim3(256), 0, s, cb, n, ntpl, nb,
+                       slots, bad);
+    return hipGetLastError();
+}
+
 template <int B>
 __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
@@ -1365,13 +1479,6 @@ hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s) {
 
 // ------------------------------ launchers ---------------------------------
 
-static char g_last_kernel[64] = "";
-
-static void note_kernel(const char *kind, int B, int method) {
-    snprintf(g_last_kernel, sizeof g_last_kernel, "%s<B=%d,M=%d>", kind, B, method);
-}
-
-const char *last_march_kernel() { return g_last_kernel; }
 
 template <int B, bool COUNT>
 static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslots,
