@@ -39,6 +39,26 @@ def scenes(cam):
     return out
 
 
+def codec_scenes(cam):
+    c0, c1 = cam.single_test_inv_view(), cam.display_inv_view((30.0, 45.0))
+    return [(f"codec12x10x9x8_{c}_m{m}", (12, 10, 9, 8), (48, 40), mat, m)
+            for c, mat in (("c0", c0), ("c1", c1)) for m in (4, 5, 6)]
+
+
+def main_codec(orc, cam):
+    """methods 4/5/6: the codec inputs are stored in the fixture itself"""
+    for name, (nx, ny, nz, nb), (W, H), m, method in codec_scenes(cam):
+        cb, t, e = orc.synth_codec(nx, ny, nz, nb, seed=SEED)
+        p = orc.make_params(W, H, m, query_method=method)
+        out, f, n, _ = orc.render_codec(cb, t, e, p)
+        np.savez_compressed(
+            os.path.join(HERE, name + ".npz"), codebook=cb, templates=t, errors=e,
+            image=np.array([W, H]), inv_view=np.asarray(m, np.float32), density=np.float32(0.05),
+            brightness=np.float32(1.0), toff=np.float32(0.0), tscale=np.float32(1.0),
+            method=np.int32(method), rgba8=out, steps=n.astype(np.int16), rgba_f=f)
+        print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
+
+
 def main():
     orc = graft.load_oracle()
     cam = graft.load_package().camera
@@ -57,6 +77,7 @@ def main():
             arrays["rgba_f"] = f
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
         print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
+    main_codec(orc, cam)
 
 
 if __name__ == "__main__":
