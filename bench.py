@@ -33,6 +33,7 @@ CONFIGS = {
     "1024x8": (1024, 8, 1920, 1080),
 }
 SEED = 20261015
+CODEC_TEMPLATES, CODEC_SLOTS = 64, 4  # synthetic codec volume (methods 4/5/6)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
 
 
@@ -42,7 +43,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="1024x8", choices=sorted(CONFIGS))
-    ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 7])
+    ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 4, 5, 6, 7])
     ap.add_argument("--camera", default="C0", choices=["C0", "C1"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump-frame", default="",
@@ -66,26 +67,33 @@ def cpu_baseline(pkg, cfg_name, m, method, row_stride):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     if row_stride <= 0:
         row_stride = 1  # the whole frame
-    vol = orc.synth_volume(n, n, n, nb, SEED, threads)
+    codec = method in (4, 5, 6)
+    if codec:
+        cb, tp, er = orc.synth_codec_field(n, n, n, nb, CODEC_TEMPLATES, CODEC_SLOTS, SEED)
+    else:
+        vol = orc.synth_volume(n, n, n, nb, SEED, threads)
     p = orc.make_params(W, H, m, query_method=method, m7_dims=(n, n, n))
     # repeat the frame until ~24 core-seconds of work have been timed
     frames, samples, dt = 0, 0, 0.0
     while frames == 0 or dt * threads < 24.0 and frames < 16:
         t0 = time.perf_counter()
-        _, _, _, s = orc.render(vol, p, row_start=0, row_stride=row_stride, nthreads=threads,
-                                want_float=False, want_steps=False)
+        if codec:
+            _, _, _, s = orc.render_codec(cb, tp, er, p, row_start=0, row_stride=row_stride,
+                                          nthreads=threads)
+        else:
+            _, _, _, s = orc.render(vol, p, row_start=0, row_stride=row_stride,
+                                    nthreads=threads, want_float=False, want_steps=False)
         dt += time.perf_counter() - t0
         samples += s
         frames += 1
     rows = len(range(0, H, row_stride))
     rays = rows * W * frames
-    del vol
     return {
         "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
         "sample": (f"oracle/vr_oracle.c (-O3, OpenMP) on every {row_stride}th row of the "
                    f"{W}x{H} frame, {frames} frame(s) ({rays} rays, {samples} samples, "
                    f"{dt:.2f} s on {threads} threads), "
-                   f"full {n}^3x{nb} volume in host RAM"),
+                   f"full {n}^3x{nb} {'codec ' if codec else ''}volume in host RAM"),
     }
 
 
@@ -120,7 +128,10 @@ def main():
 
     stream = torch.cuda.Stream(device=dev)
     pkg.set_stream(stream)
-    pkg.synthesize((n, n, n), nb, SEED)
+    if args.method in (4, 5, 6):
+        pkg.synthesize_codec((n, n, n), nb, CODEC_TEMPLATES, CODEC_SLOTS, SEED)
+    else:
+        pkg.synthesize((n, n, n), nb, SEED)
 
     lists = pkg.tiles.tile_lists(W, H, world, m)
     n_slots = lists.shape[1]
@@ -181,11 +192,14 @@ def main():
         np.save(args.dump_frame, frame.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
 
-    # algorithmic bytes of one launch on this rank: U*S_rec + pixels*4
-    u = pkg.count_footprint(desc)
+    # algorithmic bytes of one launch on this rank: the volume bytes
+    # under the footprints (U*S_rec; codec: codebook + used error pairs) + pixels*4
     pixels = W * H if world == 1 else int(np.sum(lists[rank] != pkg.tiles.PAD)) * 256
-    alg_bytes = u * nb * 4 + pixels * 4
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    u = pkg.count_footprint(desc) if args.method in (1, 2, 3) else None
+    vol_bytes = (u * nb * 4 if u is not None
+                 else pkg.footprint_bytes(desc) if args.method in (4, 5, 6) else None)
+    alg_bytes = (vol_bytes + pixels * 4) if vol_bytes is not None else None
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
 
     # HBM bytes per launch from the committed PMC passes of this same workload
     # (tools/pmc_traffic.py; FETCH_SIZE x 2 + WRITE_SIZE), only if measured on
@@ -228,12 +242,14 @@ def main():
                 if world > 1 else ""),
             },
             "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "kernel": kernel,
                 "kernel_ms": round(kern_ms, 4),
-                "alg_bytes_per_launch": int(alg_bytes), "U_records": int(u),
+                "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
+                "U_records": int(u) if u is not None else None,
             },
             "cpu_baseline": cpu,
         }

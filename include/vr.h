@@ -127,6 +127,16 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed);
 int vr_init_codec(const vr_int4 *codebook, vr_extent dims, const float *templates,
                   int ntemplates, const vr_float2 *errors, int err_slots, int nbins, int where);
 
+/* Generate the seeded synthetic codec volume of DESIGN.md section 5 in HBM
+ * (the section-5 scalar field encoded against ntemplates templates, `slots`
+ * error pairs per voxel). */
+int vr_synthesize_codec(vr_extent dims, int nbins, int ntemplates, int slots, uint64_t seed);
+
+/* shape and device arrays of the resident codec volume (codebook int4 per
+ * voxel, templates [ntemplates][nbins] fp32, errors [voxel][slots] float2) */
+int vr_codec_info(vr_extent *dims, int *nbins, int *ntemplates, int *slots,
+                  const void **codebook, const float **templates, const void **errors);
+
 /* dims, bin count and device pointer of the resident volume */
 int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins);
 
@@ -169,6 +179,12 @@ int vr_render(const vr_render_desc *desc);
  * footprints of all samples taken (methods 1/2/3).  Synchronous; allocates a
  * bitset of voxels/8 bytes.  Returns U, or a negative status. */
 int64_t vr_count_footprint(const vr_render_desc *desc);
+
+/* Algorithmic bytes of one launch's volume reads: methods
+ * 1/2/3: U * nbins * 4; methods 4/5/6: 16 bytes of codebook and 8 bytes per
+ * used error pair for every distinct voxel the footprints touch, plus the
+ * template table once.  Synchronous.  Returns bytes or a negative status. */
+int64_t vr_footprint_bytes(const vr_render_desc *desc);
 
 /* Rank-0 assembly of the multi-GPU frame: d_packed holds n_ranks x n_slots
  * tiles (each 256 uint32) gathered from the ranks, d_tile_lists the matching

@@ -63,6 +63,8 @@ def lib():
         L.orc_render_codec.restype = ctypes.c_int64
         L.orc_codec_decode.argtypes = [ctypes.POINTER(Codec), ctypes.c_int, ctypes.c_size_t, fp]
         L.orc_codec_stats.argtypes = [ctypes.POINTER(Codec), ctypes.c_int, ctypes.c_size_t, fp]
+        L.orc_synth_codec.argtypes = [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_void_p,
+                                                           ctypes.c_void_p, ctypes.c_void_p]
         L.orc_splitmix64.argtypes = [ctypes.c_uint64]
         L.orc_splitmix64.restype = ctypes.c_uint64
         L.orc_synth_fill.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -129,10 +131,23 @@ def render_codec(codebook, templates, errors, params, row_start=0, row_stride=1,
     return out, out_f, out_n, total
 
 
+def synth_codec_field(nx, ny, nz, nbins, ntemplates=64, slots=4, seed=20261015):
+    """the library's synthetic codec volume (vr_synthesize_codec):
+    returns (codebook int32 (nz,ny,nx,4), templates float32 (T,B), errors float32
+    (nz,ny,nx,slots,2))"""
+    cb = np.zeros((nz, ny, nx, 4), np.int32)
+    tp = np.zeros((ntemplates, nbins), np.float32)
+    er = np.zeros((nz, ny, nx, max(slots, 1), 2), np.float32)[..., :slots, :].copy()
+    lib().orc_synth_codec(nx, ny, nz, nbins, ntemplates, slots, seed, cb.ctypes.data,
+                          tp.ctypes.data, er.ctypes.data)
+    return cb, tp, er
+
+
 def synth_codec(nx, ny, nz, nbins, ntemplates=24, slots=None, seed=20261015):
-    """seeded synthetic codec volume (test input): templates are
-    normalised discretised Gaussians; per voxel a template, shift, flip and 0-3 sparse
-    errors drawn from splitmix64."""
+    """random codec volume for the parity tests (numpy PCG64, seeded): templates are
+    normalised discretised Gaussians; per voxel a random template, shift, flip and
+    0-4 sparse errors -- every decode branch is exercised, unlike the smooth
+    synth_codec_field."""
     slots = nbins if slots is None else slots
     rng = np.random.default_rng(seed)
     mu = rng.uniform(0.1, 0.9, ntemplates)

@@ -574,3 +574,64 @@ void orc_synth_fill(int nx, int ny, int nz, int nbins, uint64_t seed, float *vol
     free(gy);
     free(gz);
 }
+
+/* Synthetic codec volume: the section-5 field encoded
+ * against ntpl templates; mirrors k_synth_codec bit for bit. */
+void orc_synth_codec(int nx, int ny, int nz, int nbins, int ntpl, int slots, uint64_t seed,
+                     int32_t *cb, float *tpl, float *err) {
+    float amp[SYN_K];
+    float *gx = (float *)malloc(sizeof(float) * SYN_K * (size_t)nx);
+    float *gy = (float *)malloc(sizeof(float) * SYN_K * (size_t)ny);
+    float *gz = (float *)malloc(sizeof(float) * SYN_K * (size_t)nz);
+    for (int k = 0; k < SYN_K; k++) {
+        double r[5];
+        for (int j = 0; j < 5; j++) r[j] = u01(orc_splitmix64(seed + 0x100u + 8u * (uint64_t)k + (uint64_t)j));
+        amp[k] = (float)(0.3 + 0.7 * r[0]);
+        double s = 0.05 + 0.15 * r[4];
+        axis_table(nx, 0.2 + 0.6 * r[1], s, gx + (size_t)k * nx);
+        axis_table(ny, 0.2 + 0.6 * r[2], s, gy + (size_t)k * ny);
+        axis_table(nz, 0.2 + 0.6 * r[3], s, gz + (size_t)k * nz);
+    }
+    double *e = (double *)malloc(sizeof(double) * (size_t)nbins);
+    for (int t = 0; t < ntpl; t++) {
+        double mu = ((double)t + 0.5) / (double)ntpl, sum = 0.0;
+        for (int b = 0; b < nbins; b++) {
+            double dd = ((double)b + 0.5) / (double)nbins - mu;
+            e[b] = exp(-dd * dd / (2.0 * 0.06 * 0.06));
+            sum += e[b];
+        }
+        for (int b = 0; b < nbins; b++) tpl[(size_t)t * nbins + b] = (float)(e[b] / sum);
+    }
+    free(e);
+    const int nemax = (slots < 3 ? slots : 3) + 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+    for (int z = 0; z < nz; z++)
+        for (int y = 0; y < ny; y++)
+            for (int x = 0; x < nx; x++) {
+                float f = 0.0f;
+                for (int k = 0; k < SYN_K; k++)
+                    f = f + ((amp[k] * gx[(size_t)k * nx + x]) * gy[(size_t)k * ny + y]) *
+                                gz[(size_t)k * nz + z];
+                if (f > 1.0f) f = 1.0f;
+                int t = (int)(f * (float)ntpl);
+                if (t > ntpl - 1) t = ntpl - 1;
+                uint64_t v = ((uint64_t)z * (uint64_t)ny + (uint64_t)y) * (uint64_t)nx + (uint64_t)x;
+                uint64_t h = orc_splitmix64(seed ^ v);
+                int32_t *c = cb + 4 * v;
+                c[0] = t;
+                c[1] = (int)((h >> 8) & 1) % nbins;
+                c[2] = ((h >> 16) & 7) == 0 ? 1 : 0;
+                c[3] = (int)((h >> 24) % (uint64_t)nemax);
+                for (int j = 0; j < slots; j++) {
+                    uint64_t h2 = orc_splitmix64(seed + 0x5bd1e995ull + v * (uint64_t)slots + (uint64_t)j);
+                    err[2 * (v * (uint64_t)slots + (uint64_t)j)] = (float)(h2 % (uint64_t)nbins);
+                    err[2 * (v * (uint64_t)slots + (uint64_t)j) + 1] =
+                        (float)(((double)(h2 >> 11) * 0x1.0p-53 - 0.5) / 10.0);
+                }
+            }
+    free(gx);
+    free(gy);
+    free(gz);
+}

@@ -335,3 +335,56 @@ def test_codec_validation(pkg, orc, gpu):
         with pytest.raises(pkg.VRError):
             pkg.init_codec(bad, t, e)
     pkg.init_codec(cb[..., :4], t, e)  # the unmodified volume is accepted
+
+
+def test_synth_codec_matches_oracle(pkg, orc, gpu):
+    """the on-device codec generator writes the oracle's codec volume, and methods 4/5/6
+    render it identically"""
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    for (nx, ny, nz), nb, nt, slots in [((14, 11, 9), 8, 64, 4), ((9, 7, 5), 32, 16, 2),
+                                        ((8, 8, 8), 4, 8, 0)]:
+        pkg.synthesize_codec((nx, ny, nz), nb, nt, slots, seed=20261015)
+        dims, b, t, s, pcb, ptp, per = pkg.codec_info()
+        assert dims == (nx, ny, nz) and (b, t, s) == (nb, nt, slots)
+        cb, tp, er = orc.synth_codec_field(nx, ny, nz, nb, nt, slots)
+        got_cb = np.zeros_like(cb)
+        got_tp = np.zeros_like(tp)
+        got_er = np.zeros_like(er)
+        torch.cuda.synchronize()
+        assert hip.hipMemcpy(ctypes.c_void_p(got_cb.ctypes.data), ctypes.c_void_p(pcb),
+                             ctypes.c_size_t(got_cb.nbytes), 2) == 0
+        assert hip.hipMemcpy(ctypes.c_void_p(got_tp.ctypes.data), ctypes.c_void_p(ptp),
+                             ctypes.c_size_t(got_tp.nbytes), 2) == 0
+        if slots:
+            assert hip.hipMemcpy(ctypes.c_void_p(got_er.ctypes.data), ctypes.c_void_p(per),
+                                 ctypes.c_size_t(got_er.nbytes), 2) == 0
+        assert np.array_equal(got_cb, cb) and np.array_equal(got_tp, tp)
+        assert np.array_equal(got_er, er)
+        for method in (4, 5, 6):
+            m = pkg.camera.display_inv_view((20.0, 60.0))
+            got = codec_render(pkg, 48, 40, m, method, torch)
+            ref = orc.render_codec(cb, tp, er, orc.make_params(48, 40, m, query_method=method))[:3]
+            assert_parity(got, ref, f"synth codec {nb} m{method}")
+
+
+def test_codec_footprint_bytes(pkg, orc, gpu):
+    """vr_footprint_bytes for methods 4/5/6 = sum over the distinct footprint voxels
+    (numpy restatement) of 16 + 8 NE, plus the template table; methods 1/2/3 = U*B*4"""
+    import torch
+    import ref_numpy as R
+    cb, t, e = orc.synth_codec(20, 16, 12, 8, seed=5)
+    pkg.init_codec(cb, t, e)
+    m = pkg.camera.display_inv_view()
+    out = torch.zeros(64 * 48, dtype=torch.int32, device="cuda")
+    for method in (4, 6):
+        fp = set()
+        R.render(R.codec_decode(cb, t, e), 64, 48, m, method, footprint=fp)
+        ne = cb.reshape(-1, 4)[:, 3]
+        expect = sum(16 + 8 * int(ne[v]) for v in fp) + t.size * 4
+        d = pkg.make_desc(out, 64, 48, m, query_method=method, volume_size=(1, 1, 1))
+        assert pkg.footprint_bytes(d) == expect
+    vol = orc.synth_volume(20, 16, 12, 8)
+    pkg.init_distribution(vol)
+    d = pkg.make_desc(out, 64, 48, m, query_method=1)
+    assert pkg.footprint_bytes(d) == pkg.count_footprint(d) * 8 * 4

@@ -61,8 +61,8 @@ class RenderDesc(ctypes.Structure):
 EXPORTS = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers",
     "setTextureFilterMode", "basicDataProcessing", "dataProcessing",
-    "vr_last_error", "vr_last_status", "vr_clear_error", "vr_init_distribution", "vr_init_codec",
-    "vr_synthesize", "vr_volume_info", "vr_volume_layout", "vr_set_stream", "vr_render", "vr_count_footprint",
+    "vr_last_error", "vr_last_status", "vr_clear_error", "vr_init_distribution", "vr_init_codec", "vr_synthesize_codec", "vr_codec_info",
+    "vr_synthesize", "vr_volume_info", "vr_footprint_bytes", "vr_volume_layout", "vr_set_stream", "vr_render", "vr_count_footprint",
     "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version", "vr_last_kernel", "vr_selftest_logf",
 ]
 
@@ -128,6 +128,12 @@ def load() -> ctypes.CDLL:
     L.vr_selftest_logf.restype = ctypes.c_int
     L.vr_init_codec.argtypes = [vp, Extent, vp, i32, vp, i32, i32, i32]
     L.vr_init_codec.restype = i32
+    L.vr_synthesize_codec.argtypes = [Extent, i32, i32, i32, ctypes.c_uint64]
+    L.vr_synthesize_codec.restype = i32
+    L.vr_codec_info.argtypes = [vp] * 7
+    L.vr_codec_info.restype = i32
+    L.vr_footprint_bytes.argtypes = [ctypes.POINTER(RenderDesc)]
+    L.vr_footprint_bytes.restype = ctypes.c_int64
     L.vr_last_kernel.argtypes = []
     L.vr_last_kernel.restype = ctypes.c_char_p
     _lib = L

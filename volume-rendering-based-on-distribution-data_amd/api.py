@@ -167,6 +167,25 @@ def init_distribution(bins, nbins: Optional[int] = None, dims=None, adopt: bool 
     check(L.vr_init_distribution(a.ctypes.data, _extent(dims), int(nb), 0))
 
 
+def synthesize_codec(dims, nbins: int, ntemplates: int = 64, slots: int = 4,
+                     seed: int = 20261015) -> None:
+    """Generate the seeded synthetic codec volume (methods 4/5/6) directly in HBM."""
+    check(_lib.load().vr_synthesize_codec(_extent(dims), int(nbins), int(ntemplates), int(slots),
+                                          int(seed)))
+
+
+def codec_info():
+    """((X, Y, Z), nbins, ntemplates, slots, codebook_ptr, templates_ptr, errors_ptr)"""
+    e = Extent()
+    nb, nt, sl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    cb, tp, er = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    check(_lib.load().vr_codec_info(ctypes.byref(e), ctypes.byref(nb), ctypes.byref(nt),
+                                    ctypes.byref(sl), ctypes.byref(cb), ctypes.byref(tp),
+                                    ctypes.byref(er)))
+    return ((e.width, e.height, e.depth), nb.value, nt.value, sl.value, cb.value, tp.value,
+            er.value)
+
+
 def synthesize(dims, nbins: int, seed: int = 20261015) -> None:
     """Generate the seeded synthetic distribution volume directly in HBM."""
     check(_lib.load().vr_synthesize(_extent(dims), int(nbins), int(seed)))
@@ -208,8 +227,12 @@ def make_desc(d_output, width: int, height: int, inv_view, density=0.05, brightn
     d.density, d.brightness = float(density), float(brightness)
     d.transfer_offset, d.transfer_scale = float(transfer_offset), float(transfer_scale)
     d.query_method = int(query_method)
-    if volume_size is None:
-        volume_size = volume_info()[0]
+    if volume_size is None:  # method 7's grid defaults to the resident volume's dims
+        try:
+            volume_size = volume_info()[0]
+        except VRError:
+            _lib.load().vr_clear_error()
+            volume_size = codec_info()[0]
     d.volume_size = _extent(volume_size)
     d.d_tile_list = _ptr(d_tile_list)
     d.n_tiles = int(n_tiles)
@@ -224,6 +247,11 @@ def render(desc: RenderDesc) -> None:
 def count_footprint(desc: RenderDesc) -> int:
     """U: distinct records under all trilinear footprints (synchronous)."""
     return int(check(_lib.load().vr_count_footprint(ctypes.byref(desc))))
+
+
+def footprint_bytes(desc: RenderDesc) -> int:
+    """algorithmic volume bytes of one launch (methods 1-6; synchronous)"""
+    return int(check(_lib.load().vr_footprint_bytes(ctypes.byref(desc))))
 
 
 def unscatter_tiles(d_packed, d_tile_lists, n_ranks: int, n_slots: int, d_frame, width: int,
@@ -243,9 +271,9 @@ def version() -> str:
 
 __all__ = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers", "setTextureFilterMode",
-    "basicDataProcessing", "dataProcessing", "init_distribution", "init_codec", "synthesize",
+    "basicDataProcessing", "dataProcessing", "init_distribution", "init_codec", "synthesize", "synthesize_codec", "codec_info",
     "volume_info",
     "volume_layout",
-    "set_stream", "make_desc", "render", "count_footprint", "unscatter_tiles", "last_kernel", "version",
+    "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "version",
     "VRError", "PAD",
 ]

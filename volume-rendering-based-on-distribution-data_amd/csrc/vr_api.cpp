@@ -456,17 +456,12 @@ int vr_init_distribution(const float *bins, vr_extent dims, int nbins, int where
     return VR_OK;
 }
 
-int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
-    if (nbins < 1) return fail(VR_ERR_ARG, "nbins must be >= 1 (got %d)", nbins);
-    if (dims.width == 0 || dims.height == 0 || dims.depth == 0)
-        return fail(VR_ERR_ARG, "empty volume");
-    if (dims.width > 65536 || dims.height > 65536 || dims.depth > 65536)
-        return fail(VR_ERR_ARG, "volume dimension > 65536");
-    const int nx = (int)dims.width, ny = (int)dims.height, nz = (int)dims.depth;
-    const size_t nvox = dims.width * dims.height * dims.depth;
-    vr::SynthArgs a{};
-    std::vector<float> gx((size_t)vr::kSynthBlobs * nx), gy((size_t)vr::kSynthBlobs * ny),
-        gz((size_t)vr::kSynthBlobs * nz);
+// the section-5 blob field tables (host), shared by both synthesizers
+void blob_tables(int nx, int ny, int nz, uint64_t seed, vr::SynthArgs &a, std::vector<float> &gx,
+                 std::vector<float> &gy, std::vector<float> &gz) {
+    gx.assign((size_t)vr::kSynthBlobs * nx, 0.0f);
+    gy.assign((size_t)vr::kSynthBlobs * ny, 0.0f);
+    gz.assign((size_t)vr::kSynthBlobs * nz, 0.0f);
     for (int k = 0; k < vr::kSynthBlobs; k++) {
         double r[5];
         for (int j = 0; j < 5; j++)
@@ -477,6 +472,91 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
         blob_axis(ny, 0.2 + 0.6 * r[2], s, gy.data() + (size_t)k * ny);
         blob_axis(nz, 0.2 + 0.6 * r[3], s, gz.data() + (size_t)k * nz);
     }
+}
+
+int vr_synthesize_codec(vr_extent dims, int nbins, int ntemplates, int slots, uint64_t seed) {
+    if (nbins != 1 && nbins != 2 && nbins != 4 && nbins != 8 && nbins != 16 && nbins != 32)
+        return fail(VR_ERR_UNSUPPORTED, "codec volumes with %d bins (compiled: 1,2,4,8,16,32)", nbins);
+    if (ntemplates < 1 || slots < 0 || slots > nbins)
+        return fail(VR_ERR_ARG, "vr_synthesize_codec: bad template count or slots");
+    if (dims.width == 0 || dims.height == 0 || dims.depth == 0 || dims.width > 65535 ||
+        dims.height > 65535 || dims.depth > 65535)
+        return fail(VR_ERR_ARG, "vr_synthesize_codec: bad dims");
+    const int nx = (int)dims.width, ny = (int)dims.height, nz = (int)dims.depth;
+    const uint64_t nvox = (uint64_t)nx * ny * nz;
+    vr::SynthArgs a{};
+    std::vector<float> gx, gy, gz;
+    blob_tables(nx, ny, nz, seed, a, gx, gy, gz);
+    // templates: discretised Gaussians of mean (t + 0.5) / T, sigma 0.06 (double, normalised)
+    std::vector<float> tpl((size_t)ntemplates * nbins);
+    for (int t = 0; t < ntemplates; t++) {
+        const double mu = ((double)t + 0.5) / (double)ntemplates;
+        std::vector<double> e(nbins);
+        double sum = 0.0;
+        for (int b = 0; b < nbins; b++) {
+            const double dd = ((double)b + 0.5) / (double)nbins - mu;
+            e[b] = std::exp(-dd * dd / (2.0 * 0.06 * 0.06));
+            sum += e[b];
+        }
+        for (int b = 0; b < nbins; b++) tpl[(size_t)t * nbins + b] = (float)(e[b] / sum);
+    }
+    release_codec();
+    float *dgx = nullptr, *dgy = nullptr, *dgz = nullptr;
+    hipError_t e = hipMalloc(&g.cb, nvox * sizeof(int4));
+    if (e == hipSuccess && slots) e = hipMalloc(&g.cerr, nvox * (size_t)slots * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&g.tpl, tpl.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgx, gx.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgy, gy.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgz, gz.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(g.tpl, tpl.data(), tpl.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgx, gx.data(), gx.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgy, gy.data(), gy.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgz, gz.data(), gz.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        a.gx = dgx; a.gy = dgy; a.gz = dgz;
+        a.nx = nx; a.ny = ny; a.nz = nz; a.nb = nbins; a.seed = seed;
+        e = vr::launch_synth_codec(g.cb, g.cerr, a, ntemplates, slots, g.stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    if (dgx) (void)hipFree(dgx);
+    if (dgy) (void)hipFree(dgy);
+    if (dgz) (void)hipFree(dgz);
+    if (e != hipSuccess) {
+        release_codec();
+        return hip_fail(e, "vr_synthesize_codec");
+    }
+    g.cnx = nx; g.cny = ny; g.cnz = nz; g.cnb = nbins; g.ntpl = ntemplates; g.err_slots = slots;
+    return VR_OK;
+}
+
+int vr_codec_info(vr_extent *dims, int *nbins, int *ntemplates, int *slots, const void **codebook,
+                  const float **templates, const void **errors) {
+    if (!g.cb) return fail(VR_ERR_STATE, "no codec volume resident");
+    if (dims) {
+        dims->width = (size_t)g.cnx;
+        dims->height = (size_t)g.cny;
+        dims->depth = (size_t)g.cnz;
+    }
+    if (nbins) *nbins = g.cnb;
+    if (ntemplates) *ntemplates = g.ntpl;
+    if (slots) *slots = g.err_slots;
+    if (codebook) *codebook = g.cb;
+    if (templates) *templates = g.tpl;
+    if (errors) *errors = g.cerr;
+    return VR_OK;
+}
+
+int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
+    if (nbins < 1) return fail(VR_ERR_ARG, "nbins must be >= 1 (got %d)", nbins);
+    if (dims.width == 0 || dims.height == 0 || dims.depth == 0)
+        return fail(VR_ERR_ARG, "empty volume");
+    if (dims.width > 65536 || dims.height > 65536 || dims.depth > 65536)
+        return fail(VR_ERR_ARG, "volume dimension > 65536");
+    const int nx = (int)dims.width, ny = (int)dims.height, nz = (int)dims.depth;
+    const size_t nvox = dims.width * dims.height * dims.depth;
+    vr::SynthArgs a{};
+    std::vector<float> gx, gy, gz;
+    blob_tables(nx, ny, nz, seed, a, gx, gy, gz);
     std::vector<float> tab;
     if (nbins > 1) {
         tab.resize((size_t)vr::kSynthG * vr::kSynthQ * nbins);
@@ -563,7 +643,7 @@ int vr_render(const vr_render_desc *desc) {
     if (rc != VR_OK) return rc;
     hipError_t e;
     if (desc->query_method >= 4 && desc->query_method <= 6) {
-        e = vr::launch_march_codec(P.nb, desc->query_method, P, nslots, g.stream);
+        e = vr::launch_march_codec(P.nb, desc->query_method, P, nslots, false, g.stream);
         if (e == hipErrorInvalidValue)
             return fail(VR_ERR_UNSUPPORTED, "codec volumes with %d bins (compiled: 1,2,4,8,16,32)",
                         P.nb);
@@ -597,6 +677,35 @@ int64_t vr_count_footprint(const vr_render_desc *desc) {
     (void)hipFree(bits);
     if (e != hipSuccess) return hip_fail(e, "vr_count_footprint");
     return (int64_t)u;
+}
+
+int64_t vr_footprint_bytes(const vr_render_desc *desc) {
+    vr::Params P;
+    uint32_t nslots = 0;
+    int rc = fill_params(desc, P, nslots);
+    if (rc != VR_OK) return rc;
+    const int m = desc->query_method;
+    if (m == 7 || m < 1 || m > 6)
+        return fail(VR_ERR_UNSUPPORTED, "footprint bytes are defined for methods 1-6");
+    if (m <= 3) {
+        const int64_t u = vr_count_footprint(desc);
+        return u < 0 ? u : u * (int64_t)g.nb * 4;
+    }
+    const uint64_t nvox = (uint64_t)P.nx * P.ny * P.nz;
+    const uint64_t nwords = (nvox + 63) / 64;
+    unsigned long long *bits = nullptr;
+    VR_HIP(hipMalloc(&bits, nwords * 8 + 8));
+    unsigned long long *total = bits + nwords;
+    hipError_t e = hipMemsetAsync(bits, 0, nwords * 8 + 8, g.stream);
+    P.mark = bits;
+    if (e == hipSuccess) e = vr::launch_march_codec(P.nb, m, P, nslots, true, g.stream);
+    if (e == hipSuccess) e = vr::launch_codec_bytes(bits, nvox, g.cb, total, g.stream);
+    unsigned long long b = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&b, total, 8, hipMemcpyDeviceToHost, g.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    (void)hipFree(bits);
+    if (e != hipSuccess) return hip_fail(e, "vr_footprint_bytes");
+    return (int64_t)b + (int64_t)g.ntpl * g.cnb * 4;  // + the template table, read once
 }
 
 int vr_unscatter_tiles(const uint32_t *d_packed, const uint32_t *d_tile_lists, uint32_t n_ranks,

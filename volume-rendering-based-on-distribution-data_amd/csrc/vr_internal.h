@@ -29,10 +29,14 @@ const char *last_march_kernel();
 #ifdef VR_WG_PROF
 hipError_t wg_prof_read(unsigned long long *host);   // tooling build only
 #endif
-hipError_t launch_march_codec(int nb, int method, const Params &P, uint32_t nslots,
+hipError_t launch_march_codec(int nb, int method, const Params &P, uint32_t nslots, bool count,
                               hipStream_t s);
+hipError_t launch_codec_bytes(const unsigned long long *bits, uint64_t nvox, const int4 *cb,
+                              unsigned long long *total, hipStream_t s);
 hipError_t launch_codec_check(const int4 *cb, uint64_t n, int ntpl, int nb, int slots,
                               unsigned long long *bad, hipStream_t s);
+hipError_t launch_synth_codec(int4 *cb, float2 *err, const SynthArgs &a, int ntpl, int slots,
+                              hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,

@@ -1238,7 +1238,7 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
 // for methods 1/2/3, each of the 8 corners is decoded from its codebook entry,
 // template and sparse errors at every step and blended with the quantised
 // weights.  One lane per ray.
-template <int B, int C>
+template <int B, int C, bool COUNT>
 __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ unused, Params P) {
     (void)unused;
     const uint32_t slot = launch_slot(P);
@@ -1263,6 +1263,7 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
     int n = 0;
     for (int i = 0; i < kMaxSteps; i++) {
         const Foot f = footprint(P, px, py, pz);
+        if constexpr (COUNT) mark_foot(P, f);
         const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
         const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
         const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
@@ -1288,31 +1289,58 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
                 sw * P.brightness);
 }
 
-template <int B>
+template <int B, bool COUNT>
 static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream_t s) {
     const dim3 grid(nslots), block(256);
-    note_kernel("k_march_codec", B, method);
+    if (!COUNT) note_kernel("k_march_codec", B, method);
     switch (method) {
-    case 4: hipLaunchKernelGGL((k_march_codec<B, 0>), grid, block, 0, s, nullptr, P); break;
-    case 5: hipLaunchKernelGGL((k_march_codec<B, 1>), grid, block, 0, s, nullptr, P); break;
-    case 6: hipLaunchKernelGGL((k_march_codec<B, 2>), grid, block, 0, s, nullptr, P); break;
+    case 4: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT>), grid, block, 0, s, nullptr, P); break;
+    case 5: hipLaunchKernelGGL((k_march_codec<B, 1, COUNT>), grid, block, 0, s, nullptr, P); break;
+    case 6: hipLaunchKernelGGL((k_march_codec<B, 2, COUNT>), grid, block, 0, s, nullptr, P); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_march_codec(int nb, int method, const Params &P, uint32_t nslots,
-                              hipStream_t s) {
-    if (nslots == 0) return hipSuccess;
+template <bool COUNT>
+static hipError_t march_codec_dispatch(int nb, int method, const Params &P, uint32_t nslots,
+                                       hipStream_t s) {
     switch (nb) {
-    case 1: return march_codec_b<1>(method, P, nslots, s);
-    case 2: return march_codec_b<2>(method, P, nslots, s);
-    case 4: return march_codec_b<4>(method, P, nslots, s);
-    case 8: return march_codec_b<8>(method, P, nslots, s);
-    case 16: return march_codec_b<16>(method, P, nslots, s);
-    case 32: return march_codec_b<32>(method, P, nslots, s);
+    case 1: return march_codec_b<1, COUNT>(method, P, nslots, s);
+    case 2: return march_codec_b<2, COUNT>(method, P, nslots, s);
+    case 4: return march_codec_b<4, COUNT>(method, P, nslots, s);
+    case 8: return march_codec_b<8, COUNT>(method, P, nslots, s);
+    case 16: return march_codec_b<16, COUNT>(method, P, nslots, s);
+    case 32: return march_codec_b<32, COUNT>(method, P, nslots, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_march_codec(int nb, int method, const Params &P, uint32_t nslots, bool count,
+                              hipStream_t s) {
+    if (nslots == 0) return hipSuccess;
+    return count ? march_codec_dispatch<true>(nb, method, P, nslots, s)
+                 : march_codec_dispatch<false>(nb, method, P, nslots, s);
+}
+
+// Algorithmic bytes of the marked codec voxels: a 16-byte codebook entry and
+// NE 8-byte error pairs each.
+__global__ __launch_bounds__(256) void k_codec_bytes(const unsigned long long *__restrict__ bits,
+                                                     uint64_t nvox, const int4 *__restrict__ cb,
+                                                     unsigned long long *total) {
+    unsigned long long acc = 0;
+    for (uint64_t v = blockIdx.x * 256ull + threadIdx.x; v < nvox; v += gridDim.x * 256ull)
+        if ((bits[v >> 6] >> (v & 63)) & 1ull) acc += 16ull + 8ull * (unsigned)cb[v].w;
+    if (acc) atomicAdd(total, acc);
+}
+
+hipError_t launch_codec_bytes(const unsigned long long *bits, uint64_t nvox, const int4 *cb,
+                              unsigned long long *total, hipStream_t s) {
+    uint64_t blocks = (nvox + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_codec_bytes, dim3((uint32_t)blocks), dim3(256), 0, s, bits, nvox, cb,
+                       total);
+    return hipGetLastError();
 }
 
 // Codec validation: counts codebook entries the decode cannot take (template
@@ -1430,6 +1458,51 @@ __global__ __launch_bounds__(256) void k_synth(float *__restrict__ vol, SynthArg
             for (int i = 0; i < nb; i++) dst[i] = src[i];
         }
     }
+}
+
+// Synthetic codec volume: the section-5 scalar field f
+// encoded against templates of mean (t + 0.5) / T; per voxel
+// h = splitmix64(seed ^ v): shift (h >> 8) & 1 (mod B), flip when
+// ((h >> 16) & 7) == 0, NE = (h >> 24) % (min(slots, 3) + 1); error j is
+// bin h2 % B, value (u01(h2) - 0.5) / 10 with h2 = splitmix64(seed +
+// 0x5bd1e995 + v * slots + j).
+__global__ __launch_bounds__(256) void k_synth_codec(int4 *__restrict__ cb, float2 *__restrict__ err,
+                                                     SynthArgs a, int ntpl, int slots) {
+    const uint64_t nvox = (uint64_t)a.nx * a.ny * a.nz;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int nemax = (slots < 3 ? slots : 3) + 1;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvox; v += stride) {
+        const uint32_t x = (uint32_t)(v % (uint64_t)a.nx);
+        const uint64_t yz = v / (uint64_t)a.nx;
+        const uint32_t y = (uint32_t)(yz % (uint64_t)a.ny);
+        const uint32_t z = (uint32_t)(yz / (uint64_t)a.ny);
+        float f = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kSynthBlobs; k++)
+            f = f + ((a.amp[k] * a.gx[k * a.nx + x]) * a.gy[k * a.ny + y]) * a.gz[k * a.nz + z];
+        if (f > 1.0f) f = 1.0f;
+        int t = (int)(f * (float)ntpl);
+        if (t > ntpl - 1) t = ntpl - 1;
+        const uint64_t h = splitmix64(a.seed ^ v);
+        cb[v] = make_int4(t, (int)((h >> 8) & 1) % a.nb, ((h >> 16) & 7) == 0 ? 1 : 0,
+                          (int)((h >> 24) % (uint64_t)nemax));
+        for (int j = 0; j < slots; j++) {
+            const uint64_t h2 = splitmix64(a.seed + 0x5bd1e995ull + v * (uint64_t)slots + j);
+            err[v * (uint64_t)slots + j] =
+                make_float2((float)(h2 % (uint64_t)a.nb),
+                            (float)(((double)(h2 >> 11) * 0x1.0p-53 - 0.5) / 10.0));
+        }
+    }
+}
+
+hipError_t launch_synth_codec(int4 *cb, float2 *err, const SynthArgs &a, int ntpl, int slots,
+                              hipStream_t s) {
+    const uint64_t nvox = (uint64_t)a.nx * a.ny * a.nz;
+    uint64_t blocks = (nvox + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_synth_codec, dim3((uint32_t)blocks), dim3(256), 0, s, cb, err, a, ntpl,
+                       slots);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_unscatter(const uint32_t *__restrict__ packed,
