@@ -208,6 +208,31 @@ const char *vr_last_kernel(void);
  * the double-log fallback. */
 int vr_selftest_logf(uint64_t counts[2]);
 
+/* ---- the reference's input files ---- */
+
+/* Parse a codebook file (loadCodebook's format, C:558-642): int nSteps,
+ * int nBlocks, per block int spanId, int templateId, int shift, 1-byte flip,
+ * int NE, NE int bin ids, NE double errors.  Writes min(nBlocks, max_blocks)
+ * entries: codebook 4 x int32 per block, errors nbins (bin, value) float pairs
+ * per block (unused pairs 0).  Either output may be NULL.  Returns nBlocks,
+ * -1 if unreadable/truncated, -2 if a block has NE > nbins. */
+long long vr_parse_codebook(const char *path, int nbins, long long max_blocks, int32_t *codebook,
+                            float *errors);
+
+/* Parse a templates file (loadTemplates' format, C:645-675): int nTemplates,
+ * per template 6 doubles (ignored) + nbins doubles.  Writes
+ * min(nTemplates, max_templates) x nbins floats (may be NULL).  Returns
+ * nTemplates or -1. */
+long long vr_parse_templates(const char *path, int nbins, long long max_templates,
+                             float *templates);
+
+/* Load the reference's input files and make them resident, as its main()
+ * does (C:1156-1203): the raw fp32 histogram volume (nBlocks x nbins), and
+ * optionally the codebook + templates files for methods 4/5/6.
+ * histogram_path may be NULL; codebook/templates both NULL or both given. */
+int vr_load_reference_files(const char *histogram_path, const char *codebook_path,
+                            const char *templates_path, vr_extent dims, int nbins);
+
 /* library version string */
 const char *vr_version(void);
 

@@ -63,7 +63,8 @@ EXPORTS = [
     "setTextureFilterMode", "basicDataProcessing", "dataProcessing",
     "vr_last_error", "vr_last_status", "vr_clear_error", "vr_init_distribution", "vr_init_codec", "vr_synthesize_codec", "vr_codec_info",
     "vr_synthesize", "vr_volume_info", "vr_footprint_bytes", "vr_volume_layout", "vr_set_stream", "vr_render", "vr_count_footprint",
-    "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version", "vr_last_kernel", "vr_selftest_logf",
+    "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version", "vr_last_kernel", "vr_selftest_logf", "vr_parse_codebook", "vr_parse_templates",
+    "vr_load_reference_files",
 ]
 
 _lib = None
@@ -124,6 +125,13 @@ def load() -> ctypes.CDLL:
     L.vr_tiles_y.restype = u32
     L.vr_version.argtypes = []
     L.vr_version.restype = ctypes.c_char_p
+    L.vr_parse_codebook.argtypes = [ctypes.c_char_p, i32, ctypes.c_longlong, vp, vp]
+    L.vr_parse_codebook.restype = ctypes.c_longlong
+    L.vr_parse_templates.argtypes = [ctypes.c_char_p, i32, ctypes.c_longlong, vp]
+    L.vr_parse_templates.restype = ctypes.c_longlong
+    L.vr_load_reference_files.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                          Extent, i32]
+    L.vr_load_reference_files.restype = i32
     L.vr_selftest_logf.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.vr_selftest_logf.restype = ctypes.c_int
     L.vr_init_codec.argtypes = [vp, Extent, vp, i32, vp, i32, i32, i32]

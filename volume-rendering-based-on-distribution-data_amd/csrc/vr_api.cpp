@@ -320,6 +320,10 @@ void blob_axis(int n, double c, double s, float *out) {
 
 }  // namespace
 
+namespace vr {
+int record_error(int status, const char *msg) { return fail(status, "%s", msg); }
+}  // namespace vr
+
 extern "C" {
 
 const char *vr_version(void) { return "vrdd-amd 0.1 (gfx950)"; }

@@ -22,6 +22,9 @@ struct SynthArgs {
     uint64_t seed;
 };
 
+// records an error for vr_last_error() (vr_api.cpp); returns status
+int record_error(int status, const char *msg);
+
 hipError_t launch_march(int nb, int method, const float *vol, const Params &P,
                         uint32_t nslots, bool count, hipStream_t s);
 // name of the march kernel the last non-counting launch_march() chose
