@@ -241,6 +241,10 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
         P.err = g.cerr;
         P.ntpl = g.ntpl;
         P.err_slots = g.err_slots;
+        // template tables up to 32 KiB are staged in LDS (VR_CODEC_LDS=0 disables)
+        const size_t tb = (size_t)g.ntpl * g.cnb * sizeof(float);
+        const char *el = std::getenv("VR_CODEC_LDS");
+        P.tpl_lds = (tb <= 32768 && !(el && std::atoi(el) == 0)) ? (int)tb : 0;
     } else {
         P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
         P.sy = g.sy; P.sz = g.sz;

@@ -48,6 +48,7 @@ struct Params {
     const float *tpl;
     const float2 *err;
     int ntpl, err_slots;
+    int tpl_lds;                 // codec march: template table copied to LDS (bytes, 0 = no)
 };
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)
@@ -236,19 +237,32 @@ __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
 // Decode of one codec voxel: template row, flipped and circularly shifted
 // (fractalDecoding, K:195-222), NE sparse errors added with a clamp at 0
 // (K:805-823; bin ids outside [0, B) skipped), renormalised (K:826-835).
+constexpr int kCodecPre = 4;  // error pairs per voxel gathered with the codebook entry
+
+// tpl: the template table (global or an LDS copy); pre: the voxel's first
+// kCodecPre error pairs (gathered unconditionally when err_slots allows);
+// further pairs are read from e.
 template <int B>
-__device__ __forceinline__ void codec_decode(const Params &P, uint64_t vidx, float (&dec)[B]) {
-    const int4 c = P.cb[vidx];
-    const float *row = P.tpl + (uint64_t)c.x * B;
+__device__ __forceinline__ void codec_decode_pre(const float *tpl, const int4 c,
+                                                 const float2 (&pre)[kCodecPre],
+                                                 const float2 *e, float (&dec)[B]) {
+    const float *row = tpl + (uint32_t)c.x * B;
 #pragma unroll
     for (int m = 0; m < B; m++) {
         int i = m - c.y;                    // dec[(i + shift) mod B] = src[i]
         if (i < 0) i += B;
         dec[m] = row[c.z ? B - 1 - i : i];
     }
-    const float2 *e = P.err + vidx * (uint64_t)P.err_slots;
     for (int j = 0; j < c.w; j++) {
-        const float2 ev = e[j];
+        float2 ev;
+        if (j < kCodecPre) {
+            ev = pre[0];
+#pragma unroll
+            for (int k = 1; k < kCodecPre; k++)
+                if (j == k) ev = pre[k];
+        } else {
+            ev = e[j];
+        }
         const int idx = (int)ev.x;
 #pragma unroll
         for (int m = 0; m < B; m++) {
@@ -268,12 +282,19 @@ __device__ __forceinline__ void codec_decode(const Params &P, uint64_t vidx, flo
     }
 }
 
+template <int B>
+__device__ __forceinline__ void codec_decode(const Params &P, uint64_t vidx, float (&dec)[B]) {
+    const float2 *e = P.err + vidx * (uint64_t)P.err_slots;
+    float2 pre[kCodecPre];
+#pragma unroll
+    for (int k = 0; k < kCodecPre; k++) pre[k] = k < P.err_slots ? e[k] : make_float2(0.f, 0.f);
+    codec_decode_pre<B>(P.tpl, P.cb[vidx], pre, e, dec);
+}
+
 // statistic C (0 mean, 1 variance, 2 entropy) of a codec voxel, K:837-868: the
 // bin centre is used in both mean and variance
 template <int B, int C>
-__device__ __forceinline__ float codec_stat(const Params &P, uint64_t vidx) {
-    float dec[B];
-    codec_decode<B>(P, vidx, dec);
+__device__ __forceinline__ float codec_stat_of(const float (&dec)[B], float enorm) {
     if constexpr (C == 0) {
         return (float)div_const((double)raw_mean<B>(dec), kMeanD, kMeanR);
     } else if constexpr (C == 1) {
@@ -288,8 +309,15 @@ __device__ __forceinline__ float codec_stat(const Params &P, uint64_t vidx) {
         }
         return (float)div_const((double)var, kVarD, kVarR);
     } else {
-        return entropy<B>(dec, P.enorm);
+        return entropy<B>(dec, enorm);
     }
+}
+
+template <int B, int C>
+__device__ __forceinline__ float codec_stat(const Params &P, uint64_t vidx) {
+    float dec[B];
+    codec_decode<B>(P, vidx, dec);
+    return codec_stat_of<B, C>(dec, P.enorm);
 }
 
 // ---- runtime-B variants (bin counts without a compiled specialisation) ----

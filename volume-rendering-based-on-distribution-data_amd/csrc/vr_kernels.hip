@@ -1241,9 +1241,17 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
 template <int B, int C, bool COUNT>
 __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ unused, Params P) {
     (void)unused;
+    extern __shared__ __attribute__((aligned(16))) float s_tpl[];
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
-    if (tile == kPad) return;
+    if (tile == kPad) return;  // whole workgroup
+    const float *tpl = P.tpl;
+    if (P.tpl_lds) {  // small template tables live in LDS: no gathers for them
+        const uint32_t n = (uint32_t)P.tpl_lds / 4;
+        for (uint32_t i = threadIdx.x; i < n; i += 256) s_tpl[i] = P.tpl[i];
+        __syncthreads();
+        tpl = s_tpl;
+    }
     uint32_t lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
@@ -1260,6 +1268,7 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
     float t = r.tnear;
     float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
     const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    const int npre = P.err_slots < kCodecPre ? P.err_slots : kCodecPre;
     int n = 0;
     for (int i = 0; i < kMaxSteps; i++) {
         const Foot f = footprint(P, px, py, pz);
@@ -1268,15 +1277,27 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
         const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
         const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
         const uint64_t r11 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y1 * P.sy;
+        const uint64_t v[8] = {r00 + f.x0, r00 + f.x1, r10 + f.x0, r10 + f.x1,
+                               r01 + f.x0, r01 + f.x1, r11 + f.x0, r11 + f.x1};
+        // all 8 codebook entries and their first error pairs in one batch
+        int4 c[8];
+        float2 pre[8][kCodecPre];
+#pragma unroll
+        for (int j = 0; j < 8; j++) c[j] = P.cb[v[j]];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float2 *e = P.err + v[j] * (uint64_t)P.err_slots;
+#pragma unroll
+            for (int k = 0; k < kCodecPre; k++)
+                pre[j][k] = k < npre ? e[k] : make_float2(0.f, 0.f);
+        }
         float sv[8];
-        sv[0] = codec_stat<B, C>(P, r00 + f.x0);
-        sv[1] = codec_stat<B, C>(P, r00 + f.x1);
-        sv[2] = codec_stat<B, C>(P, r10 + f.x0);
-        sv[3] = codec_stat<B, C>(P, r10 + f.x1);
-        sv[4] = codec_stat<B, C>(P, r01 + f.x0);
-        sv[5] = codec_stat<B, C>(P, r01 + f.x1);
-        sv[6] = codec_stat<B, C>(P, r11 + f.x0);
-        sv[7] = codec_stat<B, C>(P, r11 + f.x1);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            float dec[B];
+            codec_decode_pre<B>(tpl, c[j], pre[j], P.err + v[j] * (uint64_t)P.err_slots, dec);
+            sv[j] = codec_stat_of<B, C>(dec, P.enorm);
+        }
         n = i + 1;
         if (composite(P, blend8(sv, f), sx, sy, sz, sw)) break;
         t = t + kTStep;
@@ -1293,10 +1314,11 @@ template <int B, bool COUNT>
 static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream_t s) {
     const dim3 grid(nslots), block(256);
     if (!COUNT) note_kernel("k_march_codec", B, method);
+    const size_t lds = (size_t)P.tpl_lds;
     switch (method) {
-    case 4: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT>), grid, block, 0, s, nullptr, P); break;
-    case 5: hipLaunchKernelGGL((k_march_codec<B, 1, COUNT>), grid, block, 0, s, nullptr, P); break;
-    case 6: hipLaunchKernelGGL((k_march_codec<B, 2, COUNT>), grid, block, 0, s, nullptr, P); break;
+    case 4: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT>), grid, block, lds, s, nullptr, P); break;
+    case 5: hipLaunchKernelGGL((k_march_codec<B, 1, COUNT>), grid, block, lds, s, nullptr, P); break;
+    case 6: hipLaunchKernelGGL((k_march_codec<B, 2, COUNT>), grid, block, lds, s, nullptr, P); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
