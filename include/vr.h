@@ -157,6 +157,9 @@ int vr_set_stream(void *stream);
  * order the list so every 8th entry forms an equally loaded, spatially
  * compact set (tiles.py tile_lists does).  Full frames use the library's own
  * XCD-balanced order.
+ * In tile-list mode miss pixels are written as 0, so packed buffers need no
+ * clearing between frames (full frames keep the reference's behaviour: misses
+ * untouched).
  * d_output_f (optional) receives the saturated float RGBA of every written
  * pixel, d_steps (optional) the samples taken (-1 for a miss; written for
  * every pixel inside the image). */

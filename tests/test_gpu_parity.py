@@ -193,7 +193,8 @@ def test_tile_split_and_unscatter(pkg, orc, gpu, world):
     pkg.render(pkg.make_desc(full, W, H, m, query_method=1))
     lists = pkg.tiles.tile_lists(W, H, world)
     n_slots = lists.shape[1]
-    packed = torch.zeros((world, n_slots * 256), dtype=torch.int32, device="cuda")
+    # garbage-filled: tile-list renders write every in-image pixel (misses as 0)
+    packed = torch.full((world, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
     dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
     for r in range(world):
         pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],

@@ -101,10 +101,18 @@ __device__ __forceinline__ void tile_pixel(uint32_t t, uint32_t &lx, uint32_t &l
     ly = t / kTileW;
 }
 
+__device__ __forceinline__ void write_miss(const Params &P, uint64_t o) {
+    if (P.out_n) P.out_n[o] = -1;
+    if (P.tile_list) P.out[o] = 0u;  // packed tile slots are cleared (see write_pixel)
+}
+
 __device__ __forceinline__ void write_pixel(const Params &P, uint64_t o, int n, float r,
                                             float g, float b, float a) {
     if (P.out_n) P.out_n[o] = n;
-    if (n < 0) return;
+    if (n < 0) {  // a miss leaves a full frame untouched (K:302-303) but clears a packed
+        if (P.tile_list) P.out[o] = 0u;  // tile slot, so tile buffers need no memset
+        return;
+    }
     P.out[o] = pack_rgba(r, g, b, a);
     if (P.out_f) {
         reinterpret_cast<float4 *>(P.out_f)[o] = make_float4(sat(r), sat(g), sat(b), sat(a));
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
     }
     if (!valid) return;
     if (n == 0) {  // miss (K:302-303): nothing written
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
@@ -598,7 +606,7 @@ __global__ __launch_bounds__(256) void k_march_wg(const float *__restrict__ vol,
 #endif
     if (!valid) return;
     if (n == 0) {  // miss (K:302-303): nothing written
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
@@ -831,7 +839,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
 #endif
     if (!valid) return;
     if (n == 0) {  // miss (K:302-303): nothing written
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
@@ -885,7 +893,7 @@ __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vo
                                    : (uint64_t)y * P.W + x;
     Ray r;
     if (!make_ray(P, x, y, r)) {
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
@@ -965,7 +973,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_HALF_WAV
                                    : (uint64_t)y * P.W + x;
     Ray r;
     if (!make_ray(P, x, y, r)) {
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
@@ -1002,6 +1010,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_HALF_WAV
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
                 sw * P.brightness);
 }
+
+#ifndef VR_QUAD_MAP
+#define VR_QUAD_MAP 0
+#endif
 
 // ---- quad-cooperative pipelined march (B == 8) ----
 // Lane l = 4q + g of a wave is the home of the ray at pixel (q, g) of the
@@ -1137,7 +1149,11 @@ __global__ __launch_bounds__(256) void k_march_quad(const float *__restrict__ vo
     if (tile == kPad) return;  // uniform per workgroup
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 2, g = lane & 3u;
-    const uint32_t lx = wave * 16u + q, ly = g;  // 16x4 block per wave, quad = a column
+#if VR_QUAD_MAP == 1  // wave = one 64-pixel row, quad = 4 consecutive pixels
+    const uint32_t lx = lane, ly = wave;
+#else                 // 16x4 block per wave, quad = a column
+    const uint32_t lx = wave * 16u + q, ly = g;
+#endif
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.W && y < P.H;
@@ -1189,7 +1205,7 @@ __global__ __launch_bounds__(256) void k_march_quad(const float *__restrict__ vo
     }
     if (!valid) return;
     if (!hit) {
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
@@ -1261,7 +1277,7 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
                                    : (uint64_t)y * P.W + x;
     Ray r;
     if (!make_ray(P, x, y, r)) {
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
@@ -1402,7 +1418,7 @@ __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol,
                                    : (uint64_t)y * P.W + x;
     Ray r;
     if (!make_ray(P, x, y, r)) {
-        if (P.out_n) P.out_n[o] = -1;
+        write_miss(P, o);
         return;
     }
     float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
