@@ -226,7 +226,7 @@ def test_errors_do_not_exit(pkg, gpu):
 
 
 @pytest.mark.parametrize("path,env", [
-    ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}), ("5", {}),
+    ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}), ("5", {}), ("6", {}),
     ("1", {"VR_BOX_MAX": "0"}), ("1", {"VR_BOX_MAX": "64"}), ("0", {"VR_WG_PER_CU": "1"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
@@ -389,3 +389,18 @@ def test_codec_footprint_bytes(pkg, orc, gpu):
     pkg.init_distribution(vol)
     d = pkg.make_desc(out, 64, 48, m, query_method=1)
     assert pkg.footprint_bytes(d) == pkg.count_footprint(d) * 8 * 4
+
+
+def test_large_volume_64bit_offsets(pkg, orc, gpu):
+    """4096 x 4096 x 36 voxels x 8 bins = 4.8e9 floats: record offsets and float
+    offsets beyond 2^32, device-generated volume against the oracle's"""
+    import torch
+    nx, ny, nz, nb = 4096, 4096, 36, 8
+    pkg.synthesize((nx, ny, nz), nb)
+    m = pkg.camera.display_inv_view((25.0, -40.0))
+    got = gpu_render(pkg, None, 96, 64, m, 1, torch)
+    vol = orc.synth_volume(nx, ny, nz, nb)
+    ref = orc.render(vol, orc.make_params(96, 64, m, query_method=1))[:3]
+    del vol
+    assert_parity(got, ref, "4096x4096x36x8")
+    pkg.freeCudaBuffers()

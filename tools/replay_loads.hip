@@ -50,6 +50,7 @@ __global__ __launch_bounds__(256) void k_replay(const float *__restrict__ vol, P
     else if (PAT == 3) { lx = lane; ly = wave; TW = 64; TH = 4; }
     else if (PAT == 4) { lx = lane & 31u; ly = wave * 2 + (lane >> 5); TW = 32; TH = 8; }
     else if (PAT == 5) { lx = lane & 15u; ly = wave * 4 + (lane >> 4); }
+    else if (PAT == 7) { lx = lane; ly = wave; TW = 64; TH = 4; }
     else if (PAT == 6) { lx = lane & 31u; ly = wave * 2 + (lane >> 5); TW = 32; TH = 8; }
     else { lx = lane >> 2; ly = wave * 4 + (lane & 3); }
     const uint32_t ntx = (P.W + TW - 1) / TW;
@@ -57,12 +58,13 @@ __global__ __launch_bounds__(256) void k_replay(const float *__restrict__ vol, P
     float px = 0, py = 0, pz = 0, dx = 0, dy = 0, dz = 0;
     int nsteps = 0;
     const bool hit = x < P.W && y < P.H && ray_of(P, x, y, px, py, pz, dx, dy, dz, nsteps);
-    if ((PAT == 0 || PAT >= 3) && !hit) return;
+    if ((PAT == 0 || (PAT >= 3 && PAT != 7)) && !hit) return;
     float acc = 0.0f;
     int i = 0;
     while (true) {
         const bool alive = hit && i < nsteps;
-        if (PAT == 0 || PAT >= 3) { if (!alive) break; }
+        if (PAT == 0 || (PAT >= 3 && PAT != 7)) { if (!alive) break; }
+        else if (PAT == 7) { if (__ballot(alive) == 0) break; }
         else if (__ballot(alive) == 0) break;
         int x0, x1, y0, y1, z0, z1;
         float a;
@@ -71,7 +73,23 @@ __global__ __launch_bounds__(256) void k_replay(const float *__restrict__ vol, P
         lin_axis(qy * 0.5f + 0.5f, P.ny, y0, y1, a);
         lin_axis(qz * 0.5f + 0.5f, P.nz, z0, z1, a);
         float4 r[16];
-        if constexpr (PAT == 0 || PAT >= 3) {
+        if constexpr (PAT == 7) {
+            // x0 record per combo for every lane; x1 only where the right neighbour's
+            // x0 is not this lane's x1 (here: lane 63 and every 14th lane)
+            const bool fix = lane == 63 || (lane % 14) == 13;
+            const uint64_t rows[4] = {z0 * P.sz + y0 * P.sy, z0 * P.sz + y1 * P.sy,
+                                      z1 * P.sz + y0 * P.sy, z1 * P.sz + y1 * P.sy};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float4 *p0 = reinterpret_cast<const float4 *>(vol + (rows[j] + x0) * 8);
+                r[4 * j + 0] = p0[0]; r[4 * j + 1] = p0[1];
+                r[4 * j + 2] = make_float4(0, 0, 0, 0); r[4 * j + 3] = r[4 * j + 2];
+                if (fix && alive) {
+                    const float4 *p1 = reinterpret_cast<const float4 *>(vol + (rows[j] + x1) * 8);
+                    r[4 * j + 2] = p1[0]; r[4 * j + 3] = p1[1];
+                }
+            }
+        } else if constexpr (PAT == 0 || PAT >= 3) {
             const uint64_t rows[4] = {z0 * P.sz + y0 * P.sy, z0 * P.sz + y1 * P.sy,
                                       z1 * P.sz + y0 * P.sy, z1 * P.sz + y1 * P.sy};
 #pragma unroll
@@ -144,10 +162,11 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char *names[] = {"per-ray", "quad", "quad-contig", "per-ray 64x1", "per-ray 32x2", "per-ray 16x4", "32x2 pipelined"};
+    const char *names[] = {"per-ray", "quad", "quad-contig", "per-ray 64x1", "per-ray 32x2", "per-ray 16x4", "32x2 pipelined", "x0 + neighbour x1"};
     for (int cam = 0; cam < 2; cam++) {
         memcpy(P.m, cam ? c1 : c0, sizeof c0);
-        for (int pat = 0; pat < 6; pat++) {
+        for (int pat = 0; pat < 8; pat++) {
+            if (pat == 6) continue;
             float best = 1e30f;
             for (int rep = 0; rep < 3; rep++) {
                 auto go = [&]() {
@@ -157,6 +176,7 @@ int main() {
                     if (pat == 3) hipLaunchKernelGGL(k_replay<3>, dim3(30 * 270), dim3(256), 0, 0, vol, P);
                     if (pat == 4) hipLaunchKernelGGL(k_replay<4>, dim3(60 * 135), dim3(256), 0, 0, vol, P);
                     if (pat == 5) hipLaunchKernelGGL(k_replay<5>, dim3(ntiles), dim3(256), 0, 0, vol, P);
+                    if (pat == 7) hipLaunchKernelGGL(k_replay<7>, dim3(30 * 270), dim3(256), 0, 0, vol, P);
                 };
                 go();
                 hipEventRecord(e0);

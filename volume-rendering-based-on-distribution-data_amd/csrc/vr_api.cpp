@@ -287,12 +287,12 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     // which keep every 4-lane group on one contiguous 64-byte run.
     // VR_PATH overrides: 0 quad, 1 k_march (LDS-staged box / per-ray),
     // 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows,
-    // 5 per-ray half-step pipelined.
+    // 5 per-ray half-step pipelined, 6 per-ray with neighbour-shared x1 records.
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
-        if (v >= 0 && v <= 5) P.path = v;
+        if (v >= 0 && v <= 6) P.path = v;
     }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {

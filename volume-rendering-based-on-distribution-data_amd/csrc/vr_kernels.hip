@@ -936,6 +936,130 @@ __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vo
                 sw * P.brightness);
 }
 
+// ---- neighbour-shared per-ray march (B % 4 == 0, row-aligned views) ----
+// A wave is one 64-pixel row.  When the screen x axis runs along the voxel
+// rows, a lane's x1 corner is usually its right neighbour's x0 corner, so each
+// lane gathers only its 4 x0 records and takes the 4 x1 records from lane + 1
+// with a DPP wave shift; lanes whose neighbour is not adjacent in HBM (gaps,
+// other rows, lane 63) gather their x1 record themselves, in instructions that
+// touch only a few lines.  Half the full-width gathers of k_march_pipe, same
+// registers, same two-step pipeline; the loop is wave-uniform so the DPP
+// always reads live lanes.
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v, uint32_t edge) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x130, 0xF, 0xF, false);
+}
+
+template <int B>
+struct PairStep {
+    float lo[4][B];   // x0 record of each (y, z) corner row
+    float hi[4][B];   // x1 record where gathered (fix lanes)
+    uint32_t fix;     // bit c: x1 of row c gathered by this lane
+    uint32_t same;    // bit c: x1 == x0 (clamped edge)
+};
+
+template <int B>
+__device__ __forceinline__ void gather_pair(const float *__restrict__ vol, const Params &P,
+                                            const Foot &f, bool act, PairStep<B> &st) {
+    const uint64_t rows[4] = {(uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy,
+                              (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy,
+                              (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy,
+                              (uint64_t)f.z1 * P.sz + (uint64_t)f.y1 * P.sy};
+    st.fix = 0;
+    st.same = f.x1 == f.x0 ? 0xFu : 0u;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint64_t i0 = rows[c] + (uint64_t)f.x0, i1 = rows[c] + (uint64_t)f.x1;
+        if (act) load_rec<B>(vol, i0, st.lo[c]);
+        // the right neighbour's x0 index (lane 63 and dead lanes: no match)
+        const uint64_t mine = act ? i0 : ~0ull;
+        const uint32_t nlo = wave_shl1((uint32_t)mine, 0xFFFFFFFFu);
+        const uint32_t nhi = wave_shl1((uint32_t)(mine >> 32), 0xFFFFFFFFu);
+        const bool need = act && f.x1 != f.x0 && (nlo != (uint32_t)i1 || nhi != (uint32_t)(i1 >> 32));
+        if (need) {
+            load_rec<B>(vol, i1, st.hi[c]);
+            st.fix |= 1u << c;
+        }
+    }
+}
+
+template <int B, int M>
+__device__ __forceinline__ float decode_pair(const Params &P, const PairStep<B> &st,
+                                             const Foot &f) {
+    float s[8];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        float x1[B];
+#pragma unroll
+        for (int k = 0; k < B; k++) {  // all lanes execute the shift
+            const float nb = __uint_as_float(wave_shl1(__float_as_uint(st.lo[c][k]), 0u));
+            x1[k] = (st.same >> c) & 1u ? st.lo[c][k] : ((st.fix >> c) & 1u ? st.hi[c][k] : nb);
+        }
+        s[2 * c] = record_stat<B, M>(st.lo[c], P.enorm);
+        s[2 * c + 1] = record_stat<B, M>(x1, P.enorm);
+    }
+    return blend8(s, f);
+}
+
+template <int B, int M>
+__global__ __launch_bounds__(256) void k_march_pair(const float *__restrict__ vol, Params P) {
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    uint32_t lx, ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    if (!alive) {
+        r.ox = r.oy = r.oz = r.dx = r.dy = r.dz = 0.0f;
+        r.tnear = r.tfar = 0.0f;
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    Foot fa = footprint(P, px, py, pz), fb = fa;
+    PairStep<B> a, b;
+    gather_pair<B>(vol, P, fa, alive, a);
+    auto step = [&](int i, const Foot &fc, const PairStep<B> &sc, Foot &fn, PairStep<B> &sn) {
+        const float tn = t + kTStep;                                        // K:701
+        const bool cont = alive && !(tn > r.tfar) && (i + 1 < kMaxSteps);   // K:703, K:381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
+        fn = footprint(P, nx, ny, nz);
+        gather_pair<B>(vol, P, fn, cont, sn);
+        const float sample = decode_pair<B, M>(P, sc, fc);  // wave-wide (DPP)
+        if (alive) {
+            n = i + 1;
+            if (composite(P, sample, sx, sy, sz, sw) || !cont) {
+                alive = false;
+            } else {
+                t = tn;
+                px = nx;
+                py = ny;
+                pz = nz;
+            }
+        }
+    };
+    for (int i = 0; i < kMaxSteps; i += 2) {
+        if (!wave_any(alive)) break;
+        step(i, fa, a, fb, b);
+        if (!wave_any(alive)) break;
+        step(i + 1, fb, b, fa, a);
+    }
+    if (!valid) return;
+    if (n == 0) {
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 // ---- half-step pipelined per-ray march (B <= 8) ----
 // k_march_pipe keeps a whole step of corner records in flight while the
 // previous step decodes (2 x 8 records per lane: 238 VGPRs at B = 8, two
@@ -1617,6 +1741,17 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             case 3: hipLaunchKernelGGL((k_march_wg<B, 3>), grid, block, 0, s, vol, P); break;
             }
             return hipGetLastError();
+        }
+        if constexpr (B % 4 == 0) {
+            if (P.path == 6 && method >= 1 && method <= 3) {
+                note_kernel("k_march_pair", B, method);
+                switch (method) {
+                case 1: hipLaunchKernelGGL((k_march_pair<B, 1>), grid, block, 0, s, vol, P); break;
+                case 2: hipLaunchKernelGGL((k_march_pair<B, 2>), grid, block, 0, s, vol, P); break;
+                case 3: hipLaunchKernelGGL((k_march_pair<B, 3>), grid, block, 0, s, vol, P); break;
+                }
+                return hipGetLastError();
+            }
         }
         if (P.path == 5 && method >= 1 && method <= 3) {
             note_kernel("k_march_half", B, method);
