@@ -3,7 +3,9 @@
 
 One step = one frame: clear the output, ray-cast every pixel of the frame (each
 rank its own image tiles), and for N > 1 gather the tiles to rank 0 (RCCL over
-xGMI) and assemble the frame.  The distribution volume is generated in HBM
+xGMI) and assemble the frame.  For N > 1 frames are pipelined: frame f+1 renders
+while frame f's gather and rank 0's assembly run on their own streams (double-
+buffered tile buffers); the timed region ends when every frame is assembled.  The distribution volume is generated in HBM
 before timing (synthetic, seeded) and replicated per GPU.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1024x8]
@@ -138,33 +140,55 @@ def main():
     frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
     with torch.cuda.stream(stream):
         if world > 1:
-            packed = torch.zeros(n_slots * 256, dtype=torch.int32, device=dev)
+            # two packed buffers (and two gather targets on rank 0): frame f+1 renders
+            # while the gather and rank 0's assembly of frame f are in flight
+            packed = [torch.zeros(n_slots * 256, dtype=torch.int32, device=dev) for _ in range(2)]
+            recv = ([torch.empty((world, n_slots * 256), dtype=torch.int32, device=dev)
+                     for _ in range(2)] if rank == 0 else [None, None])
             my_list = torch.from_numpy(lists[rank].view(np.int32).copy()).to(dev)
             all_lists = torch.from_numpy(lists.view(np.int32).copy()).to(dev)
-            desc = pkg.make_desc(packed, W, H, m, query_method=args.method,
-                                 d_tile_list=my_list, n_tiles=n_slots)
+            descs = [pkg.make_desc(packed[b], W, H, m, query_method=args.method,
+                                   d_tile_list=my_list, n_tiles=n_slots) for b in range(2)]
         else:
-            desc = pkg.make_desc(frame, W, H, m, query_method=args.method)
+            descs = [pkg.make_desc(frame, W, H, m, query_method=args.method)]
+    desc = descs[0]
     torch.cuda.synchronize()
+    assemble = torch.cuda.Stream(device=dev) if world > 1 else None
+    works, assembled = [None, None], [None, None]
 
     ev = []
+    nframe = [0]
 
     def step(timed):
+        b = nframe[0] % 2
+        nframe[0] += 1
         with torch.cuda.stream(stream):
             if world == 1:
                 frame.zero_()  # C:208 (tile slots need none: misses are written as 0)
+            else:
+                if works[b] is not None:
+                    works[b].wait()           # the gather of frame f-2 has read packed[b]
+                if assembled[b] is not None:
+                    stream.wait_event(assembled[b])  # rank 0 has unscattered recv[b]
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-            pkg.render(desc)
+            pkg.render(descs[b % len(descs)])
             if timed:
                 e1.record(stream)
                 ev.append((e0, e1))
             if world > 1:
-                gathered = pkg.tiles.gather_packed(packed, world, rank)
-                if rank == 0:
-                    pkg.unscatter_tiles(gathered, all_lists, world, n_slots, frame, W, H)
+                works[b] = pkg.tiles.gather_packed_into(packed[b], recv[b], world, rank)
+        if world > 1 and rank == 0:
+            with torch.cuda.stream(assemble):
+                works[b].wait()
+                pkg.set_stream(assemble)
+                pkg.unscatter_tiles(recv[b], all_lists, world, n_slots, frame, W, H)
+                pkg.set_stream(stream)
+                done = torch.cuda.Event()
+                done.record(assemble)
+                assembled[b] = done
 
     for _ in range(args.warmup):
         step(False)

@@ -228,6 +228,7 @@ def test_errors_do_not_exit(pkg, gpu):
 @pytest.mark.parametrize("path,env", [
     ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}), ("5", {}), ("6", {}),
     ("1", {"VR_BOX_MAX": "0"}), ("1", {"VR_BOX_MAX": "64"}), ("0", {"VR_WG_PER_CU": "1"}),
+    ("7", {"VR_SEG": "2"}), ("7", {"VR_SEG": "4"}), ("7", {"VR_SEG": "8"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, monkeypatch):
@@ -245,6 +246,47 @@ def test_every_kernel_path(pkg, orc, gpu, path, env, nb, monkeypatch):
             got = gpu_render(pkg, None, 80, 64, cam, method, torch)
             ref = orc.render(vol, orc.make_params(80, 64, cam, query_method=method))[:3]
             assert_parity(got, ref, f"path {path} {env} nb={nb} m{method}")
+
+
+@pytest.mark.parametrize("seg", ["2", "4", "8"])
+@pytest.mark.parametrize("nb", [1, 2, 8])
+def test_segmented_march_early_exit(pkg, orc, gpu, seg, nb, monkeypatch):
+    """ray-segmented march (S lanes per ray): early exits inside a window, rays that end
+    on any lane of a window and tile lists give the one-lane march's results bit for bit"""
+    import torch
+    monkeypatch.setenv("VR_PATH", "7")
+    monkeypatch.setenv("VR_SEG", seg)
+    vol = orc.synth_volume(30, 26, 22, nb)
+    pkg.init_distribution(vol)
+    cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))]
+    for cam in cams:
+        for density, bright in ((0.05, 1.0), (0.6, 1.3), (3.0, 0.7)):
+            for method in (1, 2, 3):
+                got = gpu_render(pkg, None, 72, 40, cam, method, torch, density=density,
+                                 brightness=bright)
+                ref = orc.render(vol, orc.make_params(72, 40, cam, query_method=method,
+                                                      density=density, brightness=bright))[:3]
+                assert_parity(got, ref, f"seg {seg} nb={nb} m{method} d={density}")
+    # tile lists (multi-GPU ranks): packed slots, misses cleared
+    W, H = 136, 72
+    m = cams[1]
+    full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    monkeypatch.setenv("VR_PATH", "2")
+    pkg.render(pkg.make_desc(full, W, H, m, query_method=1))
+    monkeypatch.setenv("VR_PATH", "7")
+    world = 3
+    lists = pkg.tiles.tile_lists(W, H, world, m)
+    n_slots = lists.shape[1]
+    packed = torch.full((world, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    for r in range(world):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+    assert pkg.last_kernel().startswith(f"k_march_seg{seg}")
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full)
 
 
 def test_padded_layout(pkg, orc, gpu, monkeypatch):

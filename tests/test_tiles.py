@@ -82,9 +82,14 @@ def _worker(rank, world, port, W, H, q):
                 packed[s * 256 + i] = frame[py * W + px]
     t = torch.from_numpy(packed.view(np.int32).copy())
     got = T.gather_packed(t, world, rank)
+    # the asynchronous form the pipelined bench uses, into a preallocated target
+    recv = torch.full((world, t.numel()), -7, dtype=torch.int32) if rank == 0 else None
+    T.gather_packed_into(t, recv, world, rank).wait()
     if rank == 0:
         g_np = got.numpy().view(np.uint32)
-        q.put(bool(np.array_equal(_unscatter_np(g_np, lists, W, H, T), frame)))
+        ok = np.array_equal(_unscatter_np(g_np, lists, W, H, T), frame)
+        ok = ok and np.array_equal(recv.numpy().view(np.uint32), g_np)
+        q.put(bool(ok))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--config", default="1024x8")
     ap.add_argument("--camera", default="C0")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--no-lpt", action="store_true", help="tile lists without longest-first order")
     args = ap.parse_args()
     import torch
@@ -44,15 +45,16 @@ def main():
         return e0.elapsed_time(e1) / args.reps
 
     full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-    dfull = pkg.make_desc(full, W, H, m)
+    dfull = pkg.make_desc(full, W, H, m, query_method=args.method)
     t1 = timed(lambda: pkg.render(dfull))
-    print(f"{args.config} {args.camera}: full frame {t1:.3f} ms")
+    print(f"{args.config} {args.camera} m{args.method}: full frame {t1:.3f} ms "
+          f"({pkg.last_kernel()})")
     # latency floor: k centre-most tiles alone on the GPU
     lists1 = pkg.tiles.tile_lists(W, H, 1, m)[0]
     for k in (1, 64, 512, 1024):
         sel = torch.from_numpy(lists1[:k].view(np.int32).copy()).cuda()
         pk = torch.zeros(k * 256, dtype=torch.int32, device="cuda")
-        dk = pkg.make_desc(pk, W, H, m, d_tile_list=sel, n_tiles=k)
+        dk = pkg.make_desc(pk, W, H, m, query_method=args.method, d_tile_list=sel, n_tiles=k)
         print(f"  {k:5d} longest tiles alone: {timed(lambda dk=dk: pkg.render(dk)):.3f} ms")
     for world in (2, 4, 8):
         lists = pkg.tiles.tile_lists(W, H, world, None if args.no_lpt else m)
@@ -61,7 +63,8 @@ def main():
         dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
         per = []
         for r in range(world):
-            d = pkg.make_desc(packed[r], W, H, m, d_tile_list=dl[r], n_tiles=slots)
+            d = pkg.make_desc(packed[r], W, H, m, query_method=args.method, d_tile_list=dl[r],
+                              n_tiles=slots)
             per.append(timed(lambda d=d: pkg.render(d)))
         frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
         tu = timed(lambda: pkg.unscatter_tiles(packed, dl, world, slots, frame, W, H))

@@ -287,12 +287,28 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     // which keep every 4-lane group on one contiguous 64-byte run.
     // VR_PATH overrides: 0 quad, 1 k_march (LDS-staged box / per-ray),
     // 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows,
-    // 5 per-ray half-step pipelined, 6 per-ray with neighbour-shared x1 records.
+    // 5 per-ray half-step pipelined, 6 per-ray with neighbour-shared x1 records,
+    // 7 ray-segmented (VR_SEG lanes per ray).
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
+    // Launches of few rays (a rank's tile list at 4+ GPUs) are bound by the
+    // per-ray step chain, not by HBM: there the ray-segmented march (4 lanes
+    // per ray, path 7) renders mean / variance row-aligned views ~1.4x faster
+    // than the one-lane march (tools/rank_sim.py).
+    // VR_SEG_RAYS overrides the ray-count threshold.
+    uint64_t seg_rays = 600000;
+    if (const char *e = std::getenv("VR_SEG_RAYS")) seg_rays = std::strtoull(e, nullptr, 10);
+    if (along_rows && d->d_tile_list && (d->query_method == 1 || d->query_method == 2) &&
+        (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= seg_rays)
+        P.path = 7;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
-        if (v >= 0 && v <= 6) P.path = v;
+        if (v >= 0 && v <= 7) P.path = v;
+    }
+    P.seg_lanes = 4;
+    if (const char *e = std::getenv("VR_SEG")) {
+        const int v = std::atoi(e);
+        if (v == 2 || v == 4 || v == 8 || v == -2 || v == -4 || v == -8) P.seg_lanes = v;
     }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {

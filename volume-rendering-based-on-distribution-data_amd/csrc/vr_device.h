@@ -49,6 +49,7 @@ struct Params {
     const float2 *err;
     int ntpl, err_slots;
     int tpl_lds;                 // codec march: template table copied to LDS (bytes, 0 = no)
+    int seg_lanes;               // ray-segmented march (path 7): lanes per ray
 };
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)

@@ -29,6 +29,11 @@ hipError_t launch_march(int nb, int method, const float *vol, const Params &P,
                         uint32_t nslots, bool count, hipStream_t s);
 // name of the march kernel the last non-counting launch_march() chose
 const char *last_march_kernel();
+void note_kernel(const char *kind, int B, int method);
+// ray-segmented march (vr_seg.hip): S lanes per ray; false if (B, S) has no
+// specialisation
+bool launch_march_seg(int nb, int method, int S, const float *vol, const Params &P,
+                      uint32_t nslots, hipStream_t s, hipError_t &err);
 #ifdef VR_WG_PROF
 hipError_t wg_prof_read(unsigned long long *host);   // tooling build only
 #endif

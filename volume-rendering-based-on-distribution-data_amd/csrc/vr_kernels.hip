@@ -18,163 +18,23 @@
 // K = volumeRender_kernel.cu of the reference.
 #include "vr_device.h"
 #include "vr_internal.h"
+#include "vr_march.h"
 
 #include <algorithm>
 #include <cstdio>
 
 namespace vr {
 
-// Blocks are dealt round-robin over the 8 XCDs (blockIdx % 8 = XCD group).
-// Give each group a contiguous run of tiles so neighbouring tiles, which share
-// their apron of voxel records, meet in the same L2.  Bijective for any n.
-__device__ __forceinline__ uint32_t xcd_slot(uint32_t bid, uint32_t n) {
-    const uint32_t q = n >> 3, r = n & 7;
-    const uint32_t g = bid & 7, i = bid >> 3;
-    const uint32_t base = g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q;
-    return base + i;
-}
-
-// Workgroup b runs on XCD b % 8.  Tile lists (multi-GPU) and the host-built
-// full-frame order P.perm are already XCD-interleaved by their producers
-// (tiles.py / frame_order), so workgroup b takes entry b; without either, the
-// raster order is split into one contiguous run per XCD (xcd_slot).
-__device__ __forceinline__ uint32_t launch_slot(const Params &P) {
-    return (P.tile_list || P.perm) ? blockIdx.x : xcd_slot(blockIdx.x, gridDim.x);
-}
-__device__ __forceinline__ uint32_t tile_of(const Params &P, uint32_t slot) {
-    if (P.tile_list) return P.tile_list[slot];
-    if (P.perm) return P.perm[slot];
-    return slot;
-}
 
 static char g_last_kernel[64] = "";
 
-static void note_kernel(const char *kind, int B, int method) {
+void note_kernel(const char *kind, int B, int method) {
     snprintf(g_last_kernel, sizeof g_last_kernel, "%s<B=%d,M=%d>", kind, B, method);
 }
 
 const char *last_march_kernel() { return g_last_kernel; }
 
-struct Ray {
-    float ox, oy, oz, dx, dy, dz, tnear, tfar;
-};
 
-// eye ray + intersectBox, K:288-306
-__device__ __forceinline__ bool make_ray(const Params &P, uint32_t x, uint32_t y, Ray &r) {
-    const float *M = P.m;
-    const float u = ((float)x / (float)P.W) * 2.0f - 1.0f;
-    const float v = ((float)y / (float)P.H) * 2.0f - 1.0f;
-    r.ox = 0.0f * M[0] + 0.0f * M[1] + 0.0f * M[2] + 1.0f * M[3];
-    r.oy = 0.0f * M[4] + 0.0f * M[5] + 0.0f * M[6] + 1.0f * M[7];
-    r.oz = 0.0f * M[8] + 0.0f * M[9] + 0.0f * M[10] + 1.0f * M[11];
-    const float inv = 1.0f / sqrtf(u * u + v * v + (-2.0f) * (-2.0f));
-    const float ax = u * inv, ay = v * inv, az = -2.0f * inv;
-    r.dx = ax * M[0] + ay * M[1] + az * M[2];
-    r.dy = ax * M[4] + ay * M[5] + az * M[6];
-    r.dz = ax * M[8] + ay * M[9] + az * M[10];
-    const float ix = 1.0f / r.dx, iy = 1.0f / r.dy, iz = 1.0f / r.dz;
-    const float bx = ix * (-1.0f - r.ox), by = iy * (-1.0f - r.oy), bz = iz * (-1.0f - r.oz);
-    const float tx = ix * (1.0f - r.ox), ty = iy * (1.0f - r.oy), tz = iz * (1.0f - r.oz);
-    const float mnx = fminf(tx, bx), mny = fminf(ty, by), mnz = fminf(tz, bz);
-    const float mxx = fmaxf(tx, bx), mxy = fmaxf(ty, by), mxz = fmaxf(tz, bz);
-    r.tnear = fmaxf(fmaxf(mnx, mny), fmaxf(mnx, mnz));
-    r.tfar = fminf(fminf(mxx, mxy), fminf(mxx, mxz));
-    if (!(r.tfar > r.tnear)) return false;
-    if (r.tnear < 0.0f) r.tnear = 0.0f;
-    return true;
-}
-
-__device__ __forceinline__ void mark_voxel(unsigned long long *mark, uint64_t idx) {
-    atomicOr(mark + (idx >> 6), 1ull << (idx & 63));
-}
-
-// Pixel of this thread inside its tile: wave w renders tile row w, lane = x.
-// Wide, short tiles: a footprint row of records is x-contiguous, so a tile edge
-// along y (left/right neighbour) splits every 128-B line of the rows it
-// crosses between two workgroups, while an edge along x costs only the records
-// of one voxel row.  64x4 tiles fetch 12 % fewer lines per frame than 16x16
-// (tools/footprint_sim.c, C0 at 1024^3 x 8) and each wave's gathers cover one
-// contiguous x run.
-static_assert(kTileW == 64 && kTileH * kTileW == 256, "one wave per 64-pixel tile row");
-__device__ __forceinline__ void tile_pixel(uint32_t t, uint32_t &lx, uint32_t &ly) {
-    lx = t & (kTileW - 1);
-    ly = t / kTileW;
-}
-
-__device__ __forceinline__ void write_miss(const Params &P, uint64_t o) {
-    if (P.out_n) P.out_n[o] = -1;
-    if (P.tile_list) P.out[o] = 0u;  // packed tile slots are cleared (see write_pixel)
-}
-
-__device__ __forceinline__ void write_pixel(const Params &P, uint64_t o, int n, float r,
-                                            float g, float b, float a) {
-    if (P.out_n) P.out_n[o] = n;
-    if (n < 0) {  // a miss leaves a full frame untouched (K:302-303) but clears a packed
-        if (P.tile_list) P.out[o] = 0u;  // tile slot, so tile buffers need no memset
-        return;
-    }
-    P.out[o] = pack_rgba(r, g, b, a);
-    if (P.out_f) {
-        reinterpret_cast<float4 *>(P.out_f)[o] = make_float4(sat(r), sat(g), sat(b), sat(a));
-    }
-}
-
-// composite one classified sample, K:683-699; returns true on early exit
-__device__ __forceinline__ bool composite(const Params &P, float sample, float &sx, float &sy,
-                                          float &sz, float &sw) {
-    float4 col = transfer((sample - P.toff) * P.tscale);
-    col.w = col.w * P.density;
-    col.x = col.x * col.w;
-    col.y = col.y * col.w;
-    col.z = col.z * col.w;
-    const float om = 1.0f - sw;
-    sx = sx + col.x * om;
-    sy = sy + col.y * om;
-    sz = sz + col.z * om;
-    sw = sw + col.w * om;
-    return sw > kOpacityThreshold;
-}
-
-// ---- wave-level helpers (64 lanes, DPP) ----
-// min over the 64 lanes: row_shr 1/2/4/8 inside each 16-lane row, then
-// row_bcast 15 / 31 across rows; lane 63 holds the result.
-__device__ __forceinline__ int dpp_min(int v, int ident) {
-    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x111, 0xF, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x112, 0xF, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x114, 0xF, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x118, 0xF, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xC, 0xF, false));
-    return __builtin_amdgcn_readlane(v, 63);
-}
-__device__ __forceinline__ int wave_min(int v) { return dpp_min(v, 0x7FFFFFFF); }
-__device__ __forceinline__ int wave_max(int v) { return -dpp_min(-v, 0x7FFFFFFF); }
-
-__device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0; }
-
-// Corners of one sample (K:601 texture footprint): texel indices + 8-bit weights.
-struct Foot {
-    int x0, x1, y0, y1, z0, z1;
-    float ax, ay, az;
-};
-
-__device__ __forceinline__ Foot footprint(const Params &P, float px, float py, float pz) {
-    Foot f;
-    lin_axis(px * 0.5f + 0.5f, P.nx, f.x0, f.x1, f.ax);
-    lin_axis(py * 0.5f + 0.5f, P.ny, f.y0, f.y1, f.ay);
-    lin_axis(pz * 0.5f + 0.5f, P.nz, f.z0, f.z1, f.az);
-    return f;
-}
-
-__device__ __forceinline__ float blend8(const float (&s)[8], const Foot &f) {
-    const float c00 = lerpq(s[0], s[1], f.ax);
-    const float c10 = lerpq(s[2], s[3], f.ax);
-    const float c01 = lerpq(s[4], s[5], f.ax);
-    const float c11 = lerpq(s[6], s[7], f.ax);
-    const float c0 = lerpq(c00, c10, f.ay);
-    const float c1 = lerpq(c01, c11, f.ay);
-    return lerpq(c0, c1, f.az);
-}
 
 // Compile-time tuning knobs (tools/build_variants.sh builds sweeps of them).
 #ifndef VR_DIRECT_CG
@@ -853,31 +713,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
 // The prefetch assumes the ray continues; a ray that terminates early
 // (sum.w > 0.95) wastes one step of gathers.  The loop is unrolled by two so
 // the two register sets swap roles without copies.
-template <int B>
-__device__ __forceinline__ void gather8(const float *__restrict__ vol, const Params &P,
-                                        const Foot &f, float (&rec)[8][B]) {
-    const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
-    const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
-    const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
-    const uint64_t r11 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y1 * P.sy;
-    load_rec<B>(vol, r00 + f.x0, rec[0]);
-    load_rec<B>(vol, r00 + f.x1, rec[1]);
-    load_rec<B>(vol, r10 + f.x0, rec[2]);
-    load_rec<B>(vol, r10 + f.x1, rec[3]);
-    load_rec<B>(vol, r01 + f.x0, rec[4]);
-    load_rec<B>(vol, r01 + f.x1, rec[5]);
-    load_rec<B>(vol, r11 + f.x0, rec[6]);
-    load_rec<B>(vol, r11 + f.x1, rec[7]);
-}
-
-template <int B, int M>
-__device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][B],
-                                         const Foot &f) {
-    float s[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) s[j] = record_stat<B, M>(rec[j], P.enorm);
-    return blend8(s, f);
-}
 
 template <int B, int M>
 __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vol, Params P) {
@@ -1724,6 +1559,11 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     size_t lds = B > 0 ? (size_t)P.box_max * 4u * sizeof(float) : 0;
     if (P.wg_per_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / P.wg_per_cu) & ~(size_t)255);
     if constexpr (!COUNT && B > 0 && B <= 8) {
+        if (P.path == 7) {
+            hipError_t err = hipSuccess;
+            if (launch_march_seg(B, method, P.seg_lanes, vol, P, nslots, s, err)) return err;
+            P.path = 2;
+        }
         if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {
             note_kernel("k_march_quad", B, method);
             switch (method) {

@@ -1,0 +1,220 @@
+// vr_seg.hip -- ray-segmented march: S lanes share one ray (methods 1/2/3).
+//
+// The per-ray march (K:309-707) is a chain of dependent steps: gather the 8
+// corner records, decode, composite, advance.  When a GPU has few rays (a rank
+// of the multi-GPU tile split, small viewports) the frame time is the length
+// of that chain for the longest rays, not HBM bandwidth.  Here a group of S
+// consecutive lanes marches one ray in windows of S steps: lane k samples step
+// base + k, so S steps' gathers are in flight at once, then the group
+// composites the S samples in step order (front to back, K:690-699) with the
+// early exit tested after every step (K:700-705).
+//
+// Bit-identical to the one-lane march: each lane keeps its own copy of the
+// accumulated t and pos (K:701, K:706) and advances it by the same sequence of
+// float additions (lane k starts k additions ahead, then adds S per window),
+// so step s sees exactly the t_s and pos_s of the reference's loop; a step is
+// taken iff s < 500 (K:381) and t_s <= tfar (t is non-decreasing, so that is
+// the reference's "no earlier break"); composite order and expressions are the
+// same.  Samples past an early exit inside a window are gathered but dropped.
+#include "vr_internal.h"
+#include "vr_march.h"
+
+#include <cstdio>
+
+namespace vr {
+
+// value of lane r + J*R of the wave (ds_bpermute; R = 64/S rays per wave)
+template <int S, int J>
+__device__ __forceinline__ float group_bcast(float v, uint32_t r) {
+    constexpr uint32_t R = 64u / S;
+    return __int_as_float(__builtin_amdgcn_ds_bpermute((int)((r + J * R) << 2), __float_as_int(v)));
+}
+
+// front-to-back composite of the group's S samples in step order (K:683-705):
+// every lane of the group classifies and composites the sample of step
+// base + J, taken from the lane that gathered it
+template <int S, int J>
+__device__ __forceinline__ void composite_window(const Params &P, float smp, uint64_t vm,
+                                                 uint32_t r, int base, bool &alive, int &n,
+                                                 float &sx, float &sy, float &sz, float &sw) {
+    if constexpr (J < S) {
+        constexpr uint32_t R = 64u / S;
+        const float sj = group_bcast<S, J>(smp, r);
+        const bool vj = (vm >> (r + J * R)) & 1ull;
+        if (alive) {
+            if (vj) {
+                n = base + J + 1;
+                if (composite(P, sj, sx, sy, sz, sw)) alive = false;  // K:700
+            } else {
+                alive = false;  // t > tfar or 500 steps (K:381, K:703)
+            }
+        }
+        composite_window<S, J + 1>(P, smp, vm, r, base, alive, n, sx, sy, sz, sw);
+    }
+}
+
+// Workgroup b: tile slot (b % 8) + 8 (b / 8S), part (b / 8) % S.  Slot s runs on
+// XCD s % 8 like every other march (the tile lists and the full-frame order
+// are XCD-interleaved by their producers), and the S parts of a tile are
+// consecutive workgroups of the same XCD.
+//
+// PIPE: the next window's corner records are gathered before this window is
+// decoded (one window of gathers always in flight, twice the record
+// registers); a group that exits early wastes one window of gathers.
+template <int B, int M, int S, bool PIPE>
+__global__ __launch_bounds__(256) void k_march_seg(const float *__restrict__ vol, Params P) {
+    constexpr int RPW = 256 / S;  // rays per workgroup
+    const uint32_t b = blockIdx.x;
+    const uint32_t slot = (b & 7u) + 8u * (b / (8u * S));
+    const uint32_t part = (b >> 3) % S;
+    if (slot >= P.n_tiles) return;
+    const uint32_t tile = P.tile_list ? P.tile_list[slot]
+                        : P.perm      ? P.perm[slot]
+                                      : xcd_slot(slot, P.n_tiles);
+    if (tile == kPad) return;
+    // lane = k*R + r: the 4-lane groups the L1 serves together hold adjacent rays
+    // at the same step (adjacent records), as in the one-lane march
+    constexpr uint32_t R = 64u / S;
+    const uint32_t lane = threadIdx.x & 63u, rl = lane % R, k = lane / R;
+    const uint32_t p = part * RPW + (threadIdx.x >> 6) * R + rl;  // pixel inside the 64x4 tile
+    const uint32_t lx = p % kTileW, ly = p / kTileW;
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    if (x >= P.W || y >= P.H) return;  // the whole group leaves
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    if (!make_ray(P, x, y, r)) {
+        if (k == 0) write_miss(P, o);
+        return;
+    }
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+#pragma unroll
+    for (int j = 0; j < S - 1; j++) {
+        if ((uint32_t)j < k) {
+            t = t + kTStep;
+            px = px + stx;
+            py = py + sty;
+            pz = pz + stz;
+        }
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    int n = 0, base = 0;
+    bool alive = true;
+    // step s is taken iff s < 500 and t_s <= tfar (and no early exit before it)
+    auto geom = [&](int s, float ts) { return s < kMaxSteps && (s == 0 || !(ts > r.tfar)); };
+    auto advance = [&](float &tt, float &qx, float &qy, float &qz) {
+#pragma unroll
+        for (int j = 0; j < S; j++) {
+            tt = tt + kTStep;
+            qx = qx + stx;
+            qy = qy + sty;
+            qz = qz + stz;
+        }
+    };
+    if constexpr (!PIPE) {
+        while (true) {
+            const bool valid = alive && geom(base + (int)k, t);
+            float smp = 0.0f;
+            if (valid) {
+                const Foot f = footprint(P, px, py, pz);
+                float rec[8][B];
+                gather8<B>(vol, P, f, rec);
+                smp = decode8<B, M>(P, rec, f);
+            }
+            const uint64_t vm = __ballot(valid);
+            composite_window<S, 0>(P, smp, vm, rl, base, alive, n, sx, sy, sz, sw);
+            if (!__ballot(alive)) break;
+            base += S;
+            advance(t, px, py, pz);
+        }
+    } else {
+        Foot fa, fb;
+        float ra[8][B], rb[8][B];
+        bool va = geom((int)k, t), vb = false;
+        if (va) {
+            fa = footprint(P, px, py, pz);
+            gather8<B>(vol, P, fa, ra);
+        }
+        // one window: gather the next into (fn, rn, vn) while (fc, rc, vc) decodes
+        auto window = [&](const Foot &fc, const float (&rc)[8][B], bool vc, Foot &fn,
+                          float (&rn)[8][B], bool &vn) {
+            float tn = t, nx = px, ny = py, nz = pz;
+            advance(tn, nx, ny, nz);
+            vn = alive && geom(base + S + (int)k, tn);
+            if (vn) {
+                fn = footprint(P, nx, ny, nz);
+                gather8<B>(vol, P, fn, rn);
+            }
+            float smp = 0.0f;
+            if (vc && alive) smp = decode8<B, M>(P, rc, fc);
+            const uint64_t vm = __ballot(vc);
+            composite_window<S, 0>(P, smp, vm, rl, base, alive, n, sx, sy, sz, sw);
+            base += S;
+            t = tn;
+            px = nx;
+            py = ny;
+            pz = nz;
+        };
+        while (true) {
+            window(fa, ra, va, fb, rb, vb);
+            if (!__ballot(alive)) break;
+            window(fb, rb, vb, fa, ra, va);
+            if (!__ballot(alive)) break;
+        }
+    }
+    if (k == 0)
+        write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                    sw * P.brightness);
+}
+
+template <int B, int S, bool PIPE>
+static hipError_t seg_launch(int method, const float *vol, const Params &P, uint32_t nslots,
+                             hipStream_t s) {
+    const dim3 grid(((nslots + 7u) / 8u) * 8u * S), block(256);
+    switch (method) {
+    case 1: hipLaunchKernelGGL((k_march_seg<B, 1, S, PIPE>), grid, block, 0, s, vol, P); break;
+    case 2: hipLaunchKernelGGL((k_march_seg<B, 2, S, PIPE>), grid, block, 0, s, vol, P); break;
+    case 3: hipLaunchKernelGGL((k_march_seg<B, 3, S, PIPE>), grid, block, 0, s, vol, P); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int B>
+static bool seg_b(int method, int S, const float *vol, const Params &P, uint32_t nslots,
+                  hipStream_t s, hipError_t &err) {
+    // S > 0: plain windows; S < 0: pipelined windows of |S| lanes
+    switch (S) {
+    case 2: err = seg_launch<B, 2, false>(method, vol, P, nslots, s); return true;
+    case 4: err = seg_launch<B, 4, false>(method, vol, P, nslots, s); return true;
+    case 8: err = seg_launch<B, 8, false>(method, vol, P, nslots, s); return true;
+    case -2: err = seg_launch<B, 2, true>(method, vol, P, nslots, s); return true;
+    case -4: err = seg_launch<B, 4, true>(method, vol, P, nslots, s); return true;
+    case -8: err = seg_launch<B, 8, true>(method, vol, P, nslots, s); return true;
+    default: return false;
+    }
+}
+
+bool launch_march_seg(int nb, int method, int S, const float *vol, const Params &P,
+                      uint32_t nslots, hipStream_t s, hipError_t &err) {
+    if (method < 1 || method > 3) return false;
+    bool ok = false;
+    switch (nb) {
+    case 1: ok = seg_b<1>(method, S, vol, P, nslots, s, err); break;
+    case 2: ok = seg_b<2>(method, S, vol, P, nslots, s, err); break;
+    case 4: ok = seg_b<4>(method, S, vol, P, nslots, s, err); break;
+    case 8: ok = seg_b<8>(method, S, vol, P, nslots, s, err); break;
+    default: return false;
+    }
+    if (ok) {
+        char kind[32];
+        snprintf(kind, sizeof kind, S < 0 ? "k_march_segp%d" : "k_march_seg%d", S < 0 ? -S : S);
+        note_kernel(kind, nb, method);
+    }
+    return ok;
+}
+
+}  // namespace vr

@@ -149,3 +149,37 @@ def gather_packed(packed, world_size: int, rank: int, group=None):
     else:
         dist.gather(packed, gather_list=None, dst=0, group=group)
     return recv
+
+
+class _Done:
+    """handle of a gather that has already completed on the current stream"""
+
+    def wait(self):
+        return None
+
+
+def gather_packed_into(packed, recv, world_size: int, rank: int, group=None):
+    """Asynchronous gather of every rank's packed tile buffer into ``recv``
+    ((world_size, n_slots*256) on rank 0, None elsewhere), for frame pipelining.
+
+    Issue it under the stream that rendered ``packed``.  With NCCL (= RCCL over
+    xGMI) the collective runs on the process group's own stream after the
+    render; the returned handle's ``wait()`` makes the calling stream wait for
+    it (before ``packed`` is rendered into again, or before rank 0 reads
+    ``recv``).  With gloo (tests) the gather is staged through host memory
+    synchronously and the handle is already complete.
+    """
+    import torch.distributed as dist
+
+    if world_size == 1:
+        recv[0].copy_(packed)
+        return _Done()
+    if packed.is_cuda and dist.get_backend(group) == "gloo":
+        host = gather_packed(packed.cpu(), world_size, rank, group)
+        if rank == 0:
+            recv.copy_(host)
+        return _Done()
+    if rank == 0:
+        return dist.gather(packed, gather_list=list(recv.unbind(0)), dst=0, group=group,
+                           async_op=True)
+    return dist.gather(packed, gather_list=None, dst=0, group=group, async_op=True)
