@@ -228,7 +228,8 @@ def test_errors_do_not_exit(pkg, gpu):
 @pytest.mark.parametrize("path,env", [
     ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}), ("5", {}), ("6", {}),
     ("1", {"VR_BOX_MAX": "0"}), ("1", {"VR_BOX_MAX": "64"}), ("0", {"VR_WG_PER_CU": "1"}),
-    ("7", {"VR_SEG": "2"}), ("7", {"VR_SEG": "4"}), ("7", {"VR_SEG": "8"}),
+    ("7", {"VR_SEG": "2"}), ("7", {"VR_SEG": "4"}), ("7", {"VR_SEG": "8"}), ("7", {"VR_SEG": "-4"}),
+    ("7", {"VR_SEG": "1"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, monkeypatch):

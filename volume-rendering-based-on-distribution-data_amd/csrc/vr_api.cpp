@@ -308,7 +308,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     P.seg_lanes = 4;
     if (const char *e = std::getenv("VR_SEG")) {
         const int v = std::atoi(e);
-        if (v == 2 || v == 4 || v == 8 || v == -2 || v == -4 || v == -8) P.seg_lanes = v;
+        if (v != 0 && v >= -8 && v <= 8 && (abs(v) & (abs(v) - 1)) == 0) P.seg_lanes = v;
     }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {

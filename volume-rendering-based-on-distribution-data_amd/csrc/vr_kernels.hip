@@ -707,68 +707,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
 }
 
 // ---- software-pipelined march (B <= 8) ----
-// Same arithmetic as k_march's direct path, but the 8 corner records of step
-// i+1 are gathered into a second register set BEFORE step i is decoded, so
-// every wave always has a step's gathers in flight while its f64 decode runs.
-// The prefetch assumes the ray continues; a ray that terminates early
-// (sum.w > 0.95) wastes one step of gathers.  The loop is unrolled by two so
-// the two register sets swap roles without copies.
-
 template <int B, int M>
 __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
-    uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;  // no cross-lane work in this kernel
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
-                                   : (uint64_t)y * P.W + x;
-    Ray r;
-    if (!make_ray(P, x, y, r)) {
-        write_miss(P, o);
-        return;
-    }
-    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
-    float t = r.tnear;
-    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
-    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
-    int n = 0;
-    bool alive = true;
-    Foot fa = footprint(P, px, py, pz), fb;
-    float ra[8][B], rb[8][B];
-    gather8<B>(vol, P, fa, ra);
-    // one step: decode (fc, rc) while the gathers of the next step go to (fn, rn)
-    auto step = [&](int i, const Foot &fc, const float (&rc)[8][B], Foot &fn,
-                    float (&rn)[8][B]) {
-        const float tn = t + kTStep;                               // K:701
-        const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, K:381
-        const float nx = px + stx, ny = py + sty, nz = pz + stz;   // K:706
-        if (cont) {
-            fn = footprint(P, nx, ny, nz);
-            gather8<B>(vol, P, fn, rn);
-        }
-        const float sample = decode8<B, M>(P, rc, fc);
-        n = i + 1;
-        if (composite(P, sample, sx, sy, sz, sw) || !cont) {
-            alive = false;
-        } else {
-            t = tn;
-            px = nx;
-            py = ny;
-            pz = nz;
-        }
-    };
-    for (int i = 0; i < kMaxSteps; i += 2) {
-        step(i, fa, ra, fb, rb);
-        if (!alive) break;
-        step(i + 1, fb, rb, fa, ra);
-        if (!alive) break;
-    }
-    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
-                sw * P.brightness);
+    march_pipe_tile<B, M>(vol, P, slot, tile, threadIdx.x);
 }
 
 // ---- neighbour-shared per-ray march (B % 4 == 0, row-aligned views) ----

@@ -61,8 +61,11 @@ __device__ __forceinline__ void composite_window(const Params &P, float smp, uin
 // PIPE: the next window's corner records are gathered before this window is
 // decoded (one window of gathers always in flight, twice the record
 // registers); a group that exits early wastes one window of gathers.
+#ifndef VR_SEG_WAVES
+#define VR_SEG_WAVES 1   // minimum waves per SIMD the register allocation must allow
+#endif
 template <int B, int M, int S, bool PIPE>
-__global__ __launch_bounds__(256) void k_march_seg(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVES, 8))) void k_march_seg(const float *__restrict__ vol, Params P) {
     constexpr int RPW = 256 / S;  // rays per workgroup
     const uint32_t b = blockIdx.x;
     const uint32_t slot = (b & 7u) + 8u * (b / (8u * S));
@@ -188,9 +191,11 @@ static bool seg_b(int method, int S, const float *vol, const Params &P, uint32_t
                   hipStream_t s, hipError_t &err) {
     // S > 0: plain windows; S < 0: pipelined windows of |S| lanes
     switch (S) {
+    case 1: err = seg_launch<B, 1, false>(method, vol, P, nslots, s); return true;
     case 2: err = seg_launch<B, 2, false>(method, vol, P, nslots, s); return true;
     case 4: err = seg_launch<B, 4, false>(method, vol, P, nslots, s); return true;
     case 8: err = seg_launch<B, 8, false>(method, vol, P, nslots, s); return true;
+    case -1: err = seg_launch<B, 1, true>(method, vol, P, nslots, s); return true;
     case -2: err = seg_launch<B, 2, true>(method, vol, P, nslots, s); return true;
     case -4: err = seg_launch<B, 4, true>(method, vol, P, nslots, s); return true;
     case -8: err = seg_launch<B, 8, true>(method, vol, P, nslots, s); return true;
