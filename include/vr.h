@@ -44,9 +44,9 @@ typedef struct { float x, y; } vr_float2;                     /* == float2     *
  * volumeSize is used exactly where the reference uses it: the method-7 corner
  * grid (K:322-352).  queryMethod: 1 mean, 2 variance, 3 entropy,
  * 7 software-interpolated mean, 4/5/6 fractal-codec mean / variance / entropy
- * (needs the codec arrays of initCuda or vr_init_codec).  8/9/0 need the
- * flexible-block pre-pass (out of scope): the call records an error and
- * writes nothing.  Asynchronous on the library stream (default: null stream),
+ * (needs the codec arrays of initCuda or vr_init_codec), 8/9/0 flexible-block
+ * entropy / mean / variance (needs dataProcessing or vr_flex_process after the
+ * span tables of initCuda or vr_init_flex).  Asynchronous on the library stream (default: null stream),
  * like the reference's default-stream launch. */
 void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output,
                    uint32_t imageW, uint32_t imageH, float density, float brightness,
@@ -63,8 +63,10 @@ void copyInvViewMatrix(float *invViewMatrix, size_t sizeofMatrix);
  * histogramSize.height*depth must equal volumeSize.width*height*depth.
  * Args 4-9 (codebook, templates, errorsbook and their sizes) make the codec
  * volume of methods 4/5/6 resident when all three arrays are non-null (see
- * vr_init_codec); the flexible-block arrays (args 10-18) feed methods 8/9/0
- * only and are accepted and ignored. */
+ * vr_init_codec); the flexible-block span tables (args 10-18) are made
+ * resident when all nine are non-null, with the reference's fixed sizes
+ * (64x64x32 fractal and simple entries, 64 bins, 469 templates, 64^3 raw
+ * volume, K:93-106; see vr_init_flex). */
 void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
               vr_int4 *h_codebook, vr_extent codebookSize, float *h_templates,
               vr_extent templatesSize, vr_float2 *h_errorsbook, vr_extent errorsbookSize,
@@ -87,8 +89,9 @@ void setTextureFilterMode(bool bLinearFilter);
  * there is nothing to pre-bake.  Validates that a volume is resident. */
 void basicDataProcessing(void);
 
-/* Replaces dataProcessing, K:1735-1796 (flexible-block pre-pass, methods
- * 8/9/0): out of scope in this build; records an error. */
+/* Replaces dataProcessing, K:1735-1796: the flexible-block pre-pass of
+ * methods 8/9/0 with the reference's block edge of 6 voxels (K:1737), i.e.
+ * vr_flex_process(6). */
 void dataProcessing(void);
 
 /* ---------------- Part 2: extensions ------------------------------------- */
@@ -136,6 +139,48 @@ int vr_synthesize_codec(vr_extent dims, int nbins, int ntemplates, int slots, ui
  * voxel, templates [ntemplates][nbins] fp32, errors [voxel][slots] float2) */
 int vr_codec_info(vr_extent *dims, int *nbins, int *ntemplates, int *slots,
                   const void **codebook, const float **templates, const void **errors);
+
+/* Flexible-block span tables (methods 8/9/0): an integral histogram of a cubic
+ * dim^3 raw volume stored as dyadic spans, as the reference's loaders fill
+ * initCuda's arguments 10-18 (C:709-997):
+ *   fractal_*  spans of >= 8 voxels, 1-based inclusive low/high (x, y, z, -);
+ *              code (template id, shift, flip, NE); errors nbins (bin id,
+ *              value) pairs per entry, the first NE used (C:773-877);
+ *   simple_*   spans of < 8 voxels, 0-based inclusive low/high; count and
+ *              nbins (bin id, frequency) pairs per entry (C:879-949);
+ *   templates  ntemplates x nbins floats (C:951-997).
+ * Entry i of a table stands where the reference's 64x64x32 lookup texture
+ * holds it (x = i % 64, y = i / 64 % 64, z = i / 4096); a span listed twice
+ * resolves like the reference's scan (K:1352-1372: the last 64-entry row
+ * holding it, first entry in that row).  Validated: 1 <= dim <= 126,
+ * 1 <= nbins <= 64, template id < ntemplates, 0 <= shift < nbins,
+ * 0 <= NE <= nbins, 0 <= count <= nbins.  Host arrays, copied. */
+typedef struct {
+    int dim;
+    int nbins;
+    int n_fractal;
+    const vr_int4 *fractal_low, *fractal_high, *fractal_code;
+    const vr_float2 *fractal_errors;
+    int n_simple;
+    const vr_int4 *simple_low, *simple_high;
+    const int32_t *simple_count;
+    const vr_float2 *simple_hist;
+    const float *templates;
+    int ntemplates;
+} vr_flex_tables;
+
+int vr_init_flex(const vr_flex_tables *tables);
+
+/* The dataProcessing pre-pass (K:1735-1796) with blocks of `block` voxels per
+ * axis (the last one cut at dim): per-block mean / variance / entropy of the
+ * span-table histogram (K:1033-1126), resident for methods 8/9/0.  Returns the
+ * blocks per axis, or a negative status (VR_ERR_ARG if some sub-span a block
+ * corner needs has no table entry).  Synchronous. */
+int vr_flex_process(int block);
+
+/* blocks per axis, bins and device array (blocks^3 x float4 (mean, variance,
+ * entropy, 0), block (x, y, z) at x + n*(y + n*z)) of the resident statistics */
+int vr_flex_info(int *nblk, int *nbins, const float **d_blocks);
 
 /* dims, bin count and device pointer of the resident volume */
 int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins);

@@ -69,6 +69,12 @@ def lib():
         L.orc_splitmix64.restype = ctypes.c_uint64
         L.orc_synth_fill.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_uint64, fp, ctypes.c_int]
+        L.orc_flex_corner.argtypes = [ctypes.POINTER(Flex), ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, fp]
+        L.orc_flex_process.argtypes = [ctypes.POINTER(Flex), fp]
+        L.orc_render_flex.argtypes = [fp, ctypes.c_int, ctypes.POINTER(RenderParams), u32p, fp,
+                                      i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_render_flex.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -236,3 +242,158 @@ def transfer(x: float) -> np.ndarray:
 def pack(rgba) -> int:
     a = np.ascontiguousarray(rgba, dtype=np.float32)
     return int(lib().orc_pack(_fp(a)))
+
+
+# ---- flexible blocks (methods 8/9/0): integral-histogram span tables ----
+
+class Flex(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int), ("block", ctypes.c_int), ("nbins", ctypes.c_int),
+                ("n_fractal", ctypes.c_int),
+                ("fractal_low", ctypes.c_void_p), ("fractal_high", ctypes.c_void_p),
+                ("fractal_code", ctypes.c_void_p), ("fractal_err", ctypes.c_void_p),
+                ("n_simple", ctypes.c_int),
+                ("simple_low", ctypes.c_void_p), ("simple_high", ctypes.c_void_p),
+                ("simple_count", ctypes.c_void_p), ("simple_hist", ctypes.c_void_p),
+                ("templates", ctypes.c_void_p), ("ntemplates", ctypes.c_int)]
+
+
+FLEX_KEYS = ("fractal_low", "fractal_high", "fractal_code", "fractal_err", "simple_low",
+             "simple_high", "simple_count", "simple_hist", "templates")
+
+
+def flex_arrays(t: dict) -> dict:
+    """contiguous typed copies of a span-table dict (keys FLEX_KEYS + dim/block/nbins)"""
+    out = dict(t)
+    for k in FLEX_KEYS:
+        dt = np.float32 if k in ("fractal_err", "simple_hist", "templates") else np.int32
+        out[k] = np.ascontiguousarray(t[k], dtype=dt)
+    return out
+
+
+def _flex(t: dict) -> Flex:
+    f = Flex()
+    f.dim, f.block, f.nbins = int(t["dim"]), int(t["block"]), int(t["nbins"])
+    f.n_fractal = t["fractal_low"].shape[0]
+    f.n_simple = t["simple_low"].shape[0]
+    f.ntemplates = t["templates"].shape[0]
+    for k in FLEX_KEYS:
+        setattr(f, k, t[k].ctypes.data)
+    return f
+
+
+def flex_blocks_per_axis(dim, block):
+    return (dim + block - 1) // block
+
+
+def flex_corner(t: dict, x, y, z):
+    t = flex_arrays(t)
+    out = np.zeros(t["nbins"], np.float32)
+    n = lib().orc_flex_corner(ctypes.byref(_flex(t)), int(x), int(y), int(z), _fp(out))
+    return n, out
+
+
+def flex_process(t: dict):
+    """dataProcessing: (nblk, nblk, nblk, 4) float32 block statistics (mean, variance,
+    entropy, 0) indexed [z, y, x]; raises if a sub-span has no table entry"""
+    t = flex_arrays(t)
+    nblk = flex_blocks_per_axis(t["dim"], t["block"])
+    out = np.zeros((nblk, nblk, nblk, 4), np.float32)
+    rc = lib().orc_flex_process(ctypes.byref(_flex(t)), _fp(out))
+    if rc < 0:
+        raise ValueError(f"flex pre-pass failed ({rc})")
+    return out
+
+
+def render_flex(blocks, params, row_start=0, row_stride=1, nthreads=0):
+    """methods 8/9/0 from block statistics (nblk^3, 4).  Returns like render()."""
+    blocks = np.ascontiguousarray(blocks, dtype=np.float32)
+    H, W = params.height, params.width
+    out = np.zeros((H, W), dtype=np.uint32)
+    out_f = np.zeros((H, W, 4), dtype=np.float32)
+    out_n = np.full((H, W), -2, dtype=np.int32)
+    total = lib().orc_render_flex(
+        _fp(blocks), blocks.shape[0], ctypes.byref(params),
+        out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _fp(out_f),
+        out_n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row_start, row_stride, nthreads)
+    return out, out_f, out_n, total
+
+
+def flex_split(x):
+    """[1, x] as the dyadic spans of K:1248-1282, lowest set bit first"""
+    out = []
+    for i in range(7):
+        if x & (1 << i):
+            hi = x
+            x &= ~(1 << i)
+            out.append((x + 1, hi))
+        if x == 0:
+            break
+    return out
+
+
+def flex_needed_spans(dim, block):
+    """every (low, high) 1-based span some block corner's decomposition looks up"""
+    nblk = flex_blocks_per_axis(dim, block)
+    coords = sorted({1 + i * block for i in range(nblk)} |
+                    {min((i + 1) * block, dim) for i in range(nblk)})
+    iv = sorted({s for c in coords for s in flex_split(c)})
+    return [((a[0], b[0], c[0]), (a[1], b[1], c[1])) for a in iv for b in iv for c in iv]
+
+
+def synth_flex(dim, block, nbins=64, ntemplates=40, seed=20261015, extra=50, dup=True):
+    """random span tables (numpy PCG64) covering every span the pre-pass needs:
+    spans of >= 8 voxels fractal-coded (random template, flip, shift, 0-4 errors, some
+    with bin id == nbins), smaller ones as sparse simple histograms (0-based, some bin
+    ids out of range); plus `extra` unreferenced entries and, with dup, duplicated
+    spans placed so the reference's scan order decides which entry wins."""
+    rng = np.random.default_rng(seed)
+    c = (np.arange(nbins) + 0.5) / nbins
+    mu, sig = rng.uniform(0.1, 0.9, ntemplates), rng.uniform(0.05, 0.3, ntemplates)
+    tp = np.exp(-((c[None, :] - mu[:, None]) ** 2) / (2 * sig[:, None] ** 2))
+    templates = (tp / tp.sum(1, keepdims=True)).astype(np.float32)
+    frac, simp = [], []
+    for lo, hi in flex_needed_spans(dim, block):
+        size = (hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1)
+        (frac if size >= 8 else simp).append((lo, hi))
+    for _ in range(extra):  # unreferenced decoys
+        a = rng.integers(1, dim + 1, 3)
+        b = np.minimum(a + rng.integers(0, 4, 3), dim)
+        frac.append((tuple(a), tuple(b)))
+        simp.append((tuple(a - 1), tuple(b - 1)))
+    if dup:  # the same span again, later: the later 64-entry row wins (K:1352-1372)
+        for lst in (frac, simp):
+            k = len(lst)
+            for j in rng.choice(k, size=min(k, 12), replace=False):
+                lst.append(lst[j])
+    rng.shuffle(frac)
+    rng.shuffle(simp)
+    nf, ns = len(frac), len(simp)
+    fl = np.zeros((nf, 4), np.int32)
+    fh = np.zeros((nf, 4), np.int32)
+    for i, (lo, hi) in enumerate(frac):
+        fl[i, :3], fh[i, :3] = lo, hi
+    code = np.zeros((nf, 4), np.int32)
+    code[:, 0] = rng.integers(0, ntemplates, nf)
+    code[:, 1] = rng.integers(0, nbins, nf)
+    code[:, 2] = rng.integers(0, 2, nf)
+    code[:, 3] = rng.integers(0, 5, nf)
+    ferr = np.zeros((nf, nbins, 2), np.float32)
+    ferr[:, :, 0] = rng.integers(0, nbins + 1, (nf, nbins))  # nbins: out of range, skipped
+    ferr[:, :, 1] = rng.uniform(-0.05, 0.05, (nf, nbins))
+    sl = np.zeros((ns, 4), np.int32)
+    sh = np.zeros((ns, 4), np.int32)
+    for i, (lo, hi) in enumerate(simp):
+        sl[i, :3] = np.asarray(lo) - 1
+        sh[i, :3] = np.asarray(hi) - 1
+    cnt = rng.integers(1, min(nbins, 6) + 1, ns).astype(np.int32)
+    shist = np.zeros((ns, nbins, 2), np.float32)
+    for i in range(ns):
+        bins = rng.choice(nbins, size=cnt[i], replace=False)
+        w = rng.uniform(0.1, 1.0, cnt[i])
+        shist[i, :cnt[i], 0] = bins
+        shist[i, :cnt[i], 1] = w / w.sum()
+        if rng.uniform() < 0.05:
+            shist[i, cnt[i] - 1, 0] = nbins  # out of range, skipped
+    return {"dim": dim, "block": block, "nbins": nbins, "fractal_low": fl, "fractal_high": fh,
+            "fractal_code": code, "fractal_err": ferr, "simple_low": sl, "simple_high": sh,
+            "simple_count": cnt, "simple_hist": shist, "templates": templates}

@@ -159,6 +159,8 @@ typedef struct {
     float enorm;
     uint64_t *mark; /* optional footprint bitset */
     const orc_codec *codec; /* methods 4/5/6 */
+    const float *flex;      /* methods 8/9/0: block statistics, nflex^3 float4 */
+    int nflex;
 } vol_t;
 
 static inline const float *rec_at(const vol_t *v, int x, int y, int z) {
@@ -281,6 +283,43 @@ static float sample_stat(const vol_t *v, f3 pos, int comp) {
     return lerpq(c0, c1, az);
 }
 
+/* Flexible-block sample, K:654-680: tex3D(flexBlockTex, (p*0.5+0.5)*nFlexBlock*)
+ * with an unnormalised coordinate, linear filter and clamp addressing on the
+ * 500^3 float4 array of bindToTex (K:1691-1714), which holds the block
+ * statistics at [0, nblk) per axis and zeros elsewhere. */
+#define FLEX_TEX 500 /* nMaxBlockDim, K:93 */
+static inline void lin_axis_unnorm(float u, int *i0, int *i1, float *a) {
+    float xb = u - 0.5f;
+    float fl = floorf(xb);
+    float fr = xb - fl;
+    int i = (int)fl;
+    *a = q8(fr);
+    *i0 = i < 0 ? 0 : (i > FLEX_TEX - 1 ? FLEX_TEX - 1 : i);
+    *i1 = i + 1 < 0 ? 0 : (i + 1 > FLEX_TEX - 1 ? FLEX_TEX - 1 : i + 1);
+}
+
+static inline float flex_texel(const vol_t *v, int x, int y, int z, int comp) {
+    const int n = v->nflex;
+    if (x >= n || y >= n || z >= n) return 0.0f;
+    return v->flex[(((size_t)z * n + y) * n + x) * 4 + comp];
+}
+
+static float sample_flex(const vol_t *v, f3 pos, int comp) {
+    const float nf = (float)v->nflex;
+    int x0, x1, y0, y1, z0, z1;
+    float ax, ay, az;
+    lin_axis_unnorm((pos.x * 0.5f + 0.5f) * nf, &x0, &x1, &ax);
+    lin_axis_unnorm((pos.y * 0.5f + 0.5f) * nf, &y0, &y1, &ay);
+    lin_axis_unnorm((pos.z * 0.5f + 0.5f) * nf, &z0, &z1, &az);
+    float c00 = lerpq(flex_texel(v, x0, y0, z0, comp), flex_texel(v, x1, y0, z0, comp), ax);
+    float c10 = lerpq(flex_texel(v, x0, y1, z0, comp), flex_texel(v, x1, y1, z0, comp), ax);
+    float c01 = lerpq(flex_texel(v, x0, y0, z1, comp), flex_texel(v, x1, y0, z1, comp), ax);
+    float c11 = lerpq(flex_texel(v, x0, y1, z1, comp), flex_texel(v, x1, y1, z1, comp), ax);
+    float c0 = lerpq(c00, c10, ay);
+    float c1 = lerpq(c01, c11, ay);
+    return lerpq(c0, c1, az);
+}
+
 /* method 7 corner state, K:320-367 / K:398-463 */
 typedef struct {
     f3 ip[8];
@@ -391,6 +430,9 @@ static int render_pixel(const vol_t *v, const orc_render_params *p, int x, int y
             sample = sample_stat(v, pos, 2);
         } else if (method >= 4 && method <= 6 && v->codec) {
             sample = sample_stat(v, pos, method - 1);
+        } else if (v->flex && (method == 8 || method == 9 || method == 0)) {
+            /* K:654-680: .z entropy (8), .x mean (9), .y variance (0) */
+            sample = sample_flex(v, pos, method == 8 ? 2 : (method == 9 ? 0 : 1));
         }
         n = i + 1;
         float col[4];
@@ -453,7 +495,7 @@ static void run_rows(const vol_t *v, const orc_render_params *p, uint32_t *out,
 int64_t orc_render(const float *vol, int nx, int ny, int nz, int nbins,
                    const orc_render_params *p, uint32_t *out, float *out_f,
                    int32_t *out_n, int row_start, int row_stride, int nthreads) {
-    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), NULL, NULL};
+    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), NULL, NULL, NULL, 0};
     int64_t total = 0;
     run_rows(&v, p, out, out_f, out_n, row_start, row_stride, nthreads, &total);
     return total;
@@ -462,7 +504,7 @@ int64_t orc_render(const float *vol, int nx, int ny, int nz, int nbins,
 int64_t orc_render_codec(const orc_codec *codec, int nx, int ny, int nz, int nbins,
                          const orc_render_params *p, uint32_t *out, float *out_f,
                          int32_t *out_n, int row_start, int row_stride, int nthreads) {
-    vol_t v = {NULL, nx, ny, nz, nbins, entropy_norm(nbins), NULL, codec};
+    vol_t v = {NULL, nx, ny, nz, nbins, entropy_norm(nbins), NULL, codec, NULL, 0};
     int64_t total = 0;
     run_rows(&v, p, out, out_f, out_n, row_start, row_stride, nthreads, &total);
     return total;
@@ -474,7 +516,7 @@ int64_t orc_count_footprint(const float *vol, int nx, int ny, int nz, int nbins,
     size_t nwords = (nvox + 63) / 64;
     uint64_t *mark = (uint64_t *)calloc(nwords, sizeof(uint64_t));
     if (!mark) return -1;
-    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), mark, NULL};
+    vol_t v = {vol, nx, ny, nz, nbins, entropy_norm(nbins), mark, NULL, NULL, 0};
     int64_t total = 0;
     run_rows(&v, p, NULL, NULL, NULL, 0, 1, nthreads, &total);
     int64_t u = 0;
@@ -634,4 +676,222 @@ void orc_synth_codec(int nx, int ny, int nz, int nbins, int ntpl, int slots, uin
     free(gx);
     free(gy);
     free(gz);
+}
+
+/* ------------------------------------------------------------------------ */
+/* flexible blocks: the dataProcessing pre-pass, K:892-1126, 1142-1544       */
+/* ------------------------------------------------------------------------ */
+/*
+ * Choices for the reference's undefined / unordered behaviour:
+ *  - the per-corner sum runs over the sub-spans in their index order
+ *    i*ny*nz + j*nz + k (the reference adds them with shared-memory float
+ *    atomics in whatever order the threads arrive, K:1402, 1520);
+ *  - a sub-span is looked up as the linear scan of K:1352-1372 finds it: the
+ *    scan's `break` leaves only the x loop, so among equal spans the LAST
+ *    64-entry row holding one wins, and the first entry of that row; a span with
+ *    no entry is an error (the reference reads an uninitialised codebook entry);
+ *  - flexibleFractalDecoding's result is the decoded array (K:249 returns a
+ *    pointer to a local); templates come from layer 0 (K:1389 reads layer 1 of
+ *    a one-layer array); error and simple-histogram bin ids outside [0, nbins)
+ *    are skipped (K:1407 admits == flexNBin, an out-of-bounds write);
+ *  - only cubic volumes (d_divideBlock loops x over nz and z over nx, K:1013-1015,
+ *    and fills the span arrays of all three axes in each pass, K:935-1011).
+ */
+static int flex_find(const int32_t *low, const int32_t *high, int n, const int l[3],
+                     const int h[3]) {
+    int best = -1, best_row = -1;
+    for (int i = 0; i < n; i++) {
+        const int32_t *a = low + 4 * (size_t)i, *b = high + 4 * (size_t)i;
+        if (a[0] == l[0] && a[1] == l[1] && a[2] == l[2] && b[0] == h[0] && b[1] == h[1] &&
+            b[2] == h[2]) {
+            if (i / 64 != best_row) {
+                best = i;
+                best_row = i / 64;
+            }
+        }
+    }
+    return best;
+}
+
+/* K:1248-1282: [1, x] as dyadic spans, lowest set bit first */
+static int flex_split(int x, int lo[8], int hi[8]) {
+    int n = 0;
+    for (int i = 0; i <= 6; i++) {
+        if ((x & ~(1 << i)) != x) {
+            hi[n] = x;
+            x &= ~(1 << i);
+            lo[n] = x + 1;
+            n++;
+        }
+        if (x == 0) break;
+    }
+    return n;
+}
+
+/* histogram of one span (K:1349-1437 fractal, K:1438-1531 simple), unweighted */
+static int flex_span_hist_uncached(const orc_flex *f, const int l[3], const int h[3], float *out);
+
+/* memo of span histograms per (low, high): block corners share most sub-spans,
+ * so each distinct span is looked up (linear scan) and decoded once */
+typedef struct {
+    int key[6];
+    int w;      /* weight, or -1 for a missing span; 0 = empty slot */
+    float *hist;
+} flex_memo_slot;
+static flex_memo_slot *g_memo = NULL;
+static size_t g_memo_cap = 0;
+static const orc_flex *g_memo_f = NULL;
+
+static void flex_memo_reset(const orc_flex *f) {
+    for (size_t i = 0; i < g_memo_cap; i++) free(g_memo[i].hist);
+    free(g_memo);
+    g_memo_cap = 1u << 18;
+    g_memo = calloc(g_memo_cap, sizeof(flex_memo_slot));
+    g_memo_f = f;
+}
+
+static int flex_span_hist(const orc_flex *f, const int l[3], const int h[3], float *out) {
+    if (g_memo_f != f) return flex_span_hist_uncached(f, l, h, out);
+    uint64_t k = 1469598103934665603ull;
+    const int key[6] = {l[0], l[1], l[2], h[0], h[1], h[2]};
+    for (int q = 0; q < 6; q++) k = (k ^ (uint64_t)(uint32_t)key[q]) * 1099511628211ull;
+    size_t i = (size_t)(k & (g_memo_cap - 1));
+    for (;; i = (i + 1) & (g_memo_cap - 1)) {
+        flex_memo_slot *s = &g_memo[i];
+        if (s->w == 0) {
+            memcpy(s->key, key, sizeof key);
+            s->hist = malloc(sizeof(float) * (size_t)f->nbins);
+            s->w = flex_span_hist_uncached(f, l, h, s->hist);
+            if (s->w == 0) s->w = -2; /* cannot happen: spans hold >= 1 voxel */
+            break;
+        }
+        if (memcmp(s->key, key, sizeof key) == 0) break;
+    }
+    if (g_memo[i].w < 0) return -1;
+    memcpy(out, g_memo[i].hist, sizeof(float) * (size_t)f->nbins);
+    return g_memo[i].w;
+}
+
+static int flex_span_hist_uncached(const orc_flex *f, const int l[3], const int h[3], float *out) {
+    const int nb = f->nbins;
+    const int size = (h[0] - l[0] + 1) * (h[1] - l[1] + 1) * (h[2] - l[2] + 1);
+    if (size >= 8) { /* K:1349 */
+        const int e = flex_find(f->fractal_low, f->fractal_high, f->n_fractal, l, h);
+        if (e < 0) return -1;
+        const int32_t *cb = f->fractal_code + 4 * (size_t)e;
+        const int tid = cb[0], shift = cb[1], flip = cb[2] != 0, ne = cb[3];
+        const float *orig = f->templates + (size_t)tid * (size_t)nb;
+        for (int i = 0; i < nb; i++) { /* flexibleFractalDecoding, K:225-250 */
+            int m = i + shift;
+            if (m >= nb) m = m - nb;
+            out[m] = flip ? orig[nb - 1 - i] : orig[i];
+        }
+        const float *err = f->fractal_err + 2 * (size_t)e * (size_t)nb;
+        for (int j = 0; j < ne; j++) { /* K:1400-1418 */
+            int idx = (int)err[2 * j];
+            if (idx < 0 || idx >= nb) continue;
+            out[idx] = out[idx] + err[2 * j + 1];
+            if (out[idx] < 0) out[idx] = 0;
+        }
+        float total = 0.0f; /* K:1420-1431 */
+        for (int i = 0; i < nb; i++) total = total + out[i];
+        for (int i = 0; i < nb; i++) out[i] = out[i] / total;
+    } else {
+        const int l0[3] = {l[0] - 1, l[1] - 1, l[2] - 1}; /* K:1444-1449 */
+        const int h0[3] = {h[0] - 1, h[1] - 1, h[2] - 1};
+        const int e = flex_find(f->simple_low, f->simple_high, f->n_simple, l0, h0);
+        if (e < 0) return -1;
+        for (int i = 0; i < nb; i++) out[i] = 0.0f;
+        const float *pr = f->simple_hist + 2 * (size_t)e * (size_t)nb;
+        for (int j = 0; j < f->simple_count[e]; j++) { /* K:1510-1514 */
+            int idx = (int)pr[2 * j];
+            if (idx < 0 || idx >= nb) continue;
+            out[idx] = pr[2 * j + 1];
+        }
+    }
+    return size;
+}
+
+int orc_flex_corner(const orc_flex *f, int x, int y, int z, float *hist) {
+    int xl[8], xh[8], yl[8], yh[8], zl[8], zh[8];
+    const int nx = flex_split(x, xl, xh), ny = flex_split(y, yl, yh), nz = flex_split(z, zl, zh);
+    float sp[256];
+    for (int b = 0; b < f->nbins; b++) hist[b] = 0.0f;
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < ny; j++)
+            for (int k = 0; k < nz; k++) {
+                const int l[3] = {xl[i], yl[j], zl[k]}, h[3] = {xh[i], yh[j], zh[k]};
+                const int w = flex_span_hist(f, l, h, sp);
+                if (w < 0) return -1 - (i * ny * nz + j * nz + k);
+                for (int b = 0; b < f->nbins; b++) hist[b] = hist[b] + sp[b] * (float)w;
+            }
+    return nx * ny * nz;
+}
+
+int orc_flex_process(const orc_flex *f, float *blocks) {
+    const int D = f->dim, bs = f->block, nb = f->nbins;
+    if (D < 1 || D > 126 || bs < 1 || bs > D || nb < 1 || nb > 256) return -1000000;
+    const int nblk = (D + bs - 1) / bs; /* K:906-931 */
+    flex_memo_reset(f);
+    const float bw = (255.0f - 0.0f) / (float)nb; /* K:1084-1087 */
+    const float enorm = entropy_norm(nb);
+    int rc = nblk;
+    for (int n = 0; n < nblk * nblk * nblk; n++) {
+        const int bx = n % nblk, by = (n / nblk) % nblk, bz = n / (nblk * nblk);
+        /* span of block n, K:935-1024: [1 + i*bs, (i+1)*bs], the last cut at D */
+        const int lo[3] = {1 + bx * bs, 1 + by * bs, 1 + bz * bs};
+        const int hi[3] = {bx == nblk - 1 ? D : (bx + 1) * bs, by == nblk - 1 ? D : (by + 1) * bs,
+                           bz == nblk - 1 ? D : (bz + 1) * bs};
+        float c[8][256];
+        for (int k = 0; k < 8; k++) { /* corners, K:1151-1228 */
+            const int x = (k & 1) ? hi[0] : lo[0], y = (k & 2) ? hi[1] : lo[1],
+                      z = (k & 4) ? hi[2] : lo[2];
+            if (orc_flex_corner(f, x, y, z, c[k]) < 0) rc = -1 - n;
+        }
+        float h[256], total = 0.0f;
+        for (int s = 0; s < nb; s++) { /* K:1041-1051 */
+            h[s] = c[0][s] + c[3][s] + c[4][s] + c[7][s] - c[1][s] - c[2][s] - c[5][s] - c[6][s];
+            if (h[s] < 0) h[s] = 0;
+        }
+        for (int s = 0; s < nb; s++) total += h[s]; /* K:1059-1062 */
+        if (!(total <= 0)) {
+            for (int s = 0; s < nb; s++) { /* K:1072-1080 */
+                h[s] = h[s] / total;
+                if (h[s] < 0) h[s] = 0;
+                if (h[s] > 1) h[s] = 1;
+            }
+        }
+        float mean = 0.0f; /* K:1086-1090 */
+        for (int i = 0; i < nb; i++)
+            mean = (float)((double)mean + (double)h[i] * ((double)(bw * (float)i) + (double)bw / 2.0));
+        float var = 0.0f; /* K:1094-1098 */
+        for (int i = 0; i < nb; i++) {
+            const double d = ((double)(bw * (float)i) + (double)bw / 2.0) - (double)mean;
+            var = (float)((double)var + (double)h[i] * d * d);
+        }
+        float ent = 0.0f; /* K:1106-1115 */
+        for (int i = 0; i < nb; i++) {
+            const float pr = h[i];
+            const double t = pr <= 0 ? 0.0 : ((double)logf_cr(pr) / LN2_D);
+            ent = (float)((double)ent + (double)pr * t);
+        }
+        ent = -ent;
+        ent = ent / enorm;
+        float *o = blocks + 4 * (size_t)n; /* flexBlockData[n], K:1117-1119 */
+        o[0] = mean;
+        o[1] = var;
+        o[2] = ent;
+        o[3] = 0.0f;
+    }
+    g_memo_f = NULL;
+    return rc;
+}
+
+int64_t orc_render_flex(const float *blocks, int nblk, const orc_render_params *p,
+                        uint32_t *out, float *out_f, int32_t *out_n, int row_start,
+                        int row_stride, int nthreads) {
+    vol_t v = {NULL, 1, 1, 1, 1, 0.0f, NULL, NULL, blocks, nblk};
+    int64_t total = 0;
+    run_rows(&v, p, out, out_f, out_n, row_start, row_stride, nthreads, &total);
+    return total;
 }

@@ -56,6 +56,44 @@ int64_t orc_render_codec(const orc_codec *codec, int nx, int ny, int nz, int nbi
                          const orc_render_params *p, uint32_t *out, float *out_f,
                          int32_t *out_n, int row_start, int row_stride, int nthreads);
 
+/* Flexible blocks (methods 8/9/0): the integral-histogram span tables of
+ * initCuda's arguments 10-18 (K:1893-1900, loaders C:709-997) and the
+ * dataProcessing pre-pass (K:1735-1796).
+ *   fractal spans: low/high 4 int32 (x, y, z, 0), 1-based inclusive; code 4
+ *     int32 (template id, shift, flip, NE); err nbins (bin id, value) float
+ *     pairs per entry (C:773-877);
+ *   simple spans: low/high 0-based; count int32; hist nbins (bin id, freq)
+ *     float pairs per entry (C:879-949);
+ *   templates: ntemplates x nbins floats (C:951-997).
+ * Table entry i sits at (i % 64, (i / 64) % 64, i / 4096) of the reference's
+ * 64x64x32 lookup textures (K:1352-1370). */
+typedef struct {
+    int dim;            /* cubic raw volume edge (rawVolumeDim, K:106)          */
+    int block;          /* block edge (dataProcessing's blockSize, K:1737)      */
+    int nbins;          /* flexNBin (K:97)                                      */
+    int n_fractal;
+    const int32_t *fractal_low, *fractal_high, *fractal_code;
+    const float *fractal_err;
+    int n_simple;
+    const int32_t *simple_low, *simple_high, *simple_count;
+    const float *simple_hist;
+    const float *templates;
+    int ntemplates;
+} orc_flex;
+
+/* histogram sum of the integral-histogram corner (x, y, z) (1-based), K:1142-1544;
+ * returns the number of sub-spans, or -1 - k when sub-span k has no table entry */
+int orc_flex_corner(const orc_flex *f, int x, int y, int z, float *hist);
+/* dataProcessing: per block (mean, variance, entropy, 0) in blocks[nblk^3 * 4],
+ * block n = (z * nblk + y) * nblk + x (K:1013-1031, 1033-1126); returns nblk, or
+ * a negative value when a sub-span is missing from the tables */
+int orc_flex_process(const orc_flex *f, float *blocks);
+/* orc_render for methods 8 (entropy), 9 (mean) and 0 (variance) from the block
+ * statistics (flexBlockTex, K:654-680, bound K:1691-1714) */
+int64_t orc_render_flex(const float *blocks, int nblk, const orc_render_params *p,
+                        uint32_t *out, float *out_f, int32_t *out_n, int row_start,
+                        int row_stride, int nthreads);
+
 /* statistic of one B-bin record: d_basicDataProcessing K:736-773 */
 void orc_record_stats(const float *rec, int nbins, float out[3]);
 

@@ -59,6 +59,34 @@ def main_codec(orc, cam):
         print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
 
 
+FLEX_TSCALE = {9: 1.0 / 255.0, 0: 1.0 / 4000.0, 8: 1.0}  # mean ~[0,255], variance, entropy
+
+
+def flex_scenes(cam):
+    c0, c1 = cam.single_test_inv_view(), cam.display_inv_view((30.0, 45.0))
+    return [(f"flex20b6x16_{c}_m{m}", (20, 6, 16), (48, 40), mat, m)
+            for c, mat in (("c0", c0), ("c1", c1)) for m in (8, 9, 0)]
+
+
+def main_flex(orc, cam):
+    """methods 8/9/0: the span tables are stored in the fixture, with the block
+    statistics of the pre-pass"""
+    for name, (dim, block, nb), (W, H), m, method in flex_scenes(cam):
+        t = orc.synth_flex(dim, block, nb, seed=SEED)
+        blocks = orc.flex_process(t)
+        p = orc.make_params(W, H, m, density=0.2, transfer_scale=FLEX_TSCALE[method],
+                            query_method=method)
+        out, f, n, _ = orc.render_flex(blocks, p)
+        arrays = {k: t[k] for k in orc.FLEX_KEYS}
+        np.savez_compressed(
+            os.path.join(HERE, name + ".npz"), flex_dims=np.array([dim, block, nb]), blocks=blocks,
+            image=np.array([W, H]), inv_view=np.asarray(m, np.float32), density=np.float32(0.2),
+            brightness=np.float32(1.0), toff=np.float32(0.0),
+            tscale=np.float32(FLEX_TSCALE[method]), method=np.int32(method), rgba8=out,
+            steps=n.astype(np.int16), rgba_f=f, **arrays)
+        print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
+
+
 def main():
     orc = graft.load_oracle()
     cam = graft.load_package().camera
@@ -78,6 +106,7 @@ def main():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
         print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
     main_codec(orc, cam)
+    main_flex(orc, cam)
 
 
 if __name__ == "__main__":

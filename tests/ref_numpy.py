@@ -1,4 +1,6 @@
-"""Independent numpy restatement of d_render (methods 1/2/3/7) for small cases.
+"""Independent numpy restatement of d_render (methods 1/2/3/7, 4/5/6 from decoded
+codec records, 8/9/0 from flexible-block statistics) and of the flexible-block
+pre-pass, for small cases.
 
 Test infrastructure: a second, separately written reading of the reference
 (volumeRender_kernel.cu = K) used to cross-check the C oracle bit for bit.
@@ -21,6 +23,15 @@ def _clamp01(u):
 def _lin(u, n):
     u = _clamp01(u)
     xb = u * f32(n) - f32(0.5)
+    fl = np.floor(xb)
+    a = np.rint((xb - fl) * f32(256)) * f32(1.0 / 256)
+    i = fl.astype(np.int64)
+    return np.clip(i, 0, n - 1), np.clip(i + 1, 0, n - 1), a.astype(np.float32)
+
+
+def _lin_unnorm(u, n=500):
+    """unnormalised linear fetch on the 500^3 flexBlockTex, clamp (K:1691-1714)"""
+    xb = u - f32(0.5)
     fl = np.floor(xb)
     a = np.rint((xb - fl) * f32(256)) * f32(1.0 / 256)
     i = fl.astype(np.int64)
@@ -169,6 +180,23 @@ def _render(vol, W, H, m, method, density, brightness, toff, tscale, m7_dims, fo
             m0 = bl(m00, m10, yd)
             m1 = bl(m01, m11, yd)
             sample = bl(m0, m1, zd) * f32(50)
+        elif method in (8, 9, 0):  # K:654-680, vol = block statistics (n, n, n, 4)
+            nbk = vol.shape[0]
+            comp = {9: 0, 0: 1, 8: 2}[method]
+            ax = [_lin_unnorm((pos[k] * f32(0.5) + f32(0.5)) * f32(nbk)) for k in range(3)]
+            vals = []
+            for j in range(8):
+                xi = ax[0][1] if j & 1 else ax[0][0]
+                yi = ax[1][1] if j & 2 else ax[1][0]
+                zi = ax[2][1] if j & 4 else ax[2][0]
+                ok = (xi < nbk) & (yi < nbk) & (zi < nbk)
+                vals.append(np.where(ok, vol[np.minimum(zi, nbk - 1), np.minimum(yi, nbk - 1),
+                                             np.minimum(xi, nbk - 1), comp], f32(0)))
+            c00 = _lerp(vals[0], vals[1], ax[0][2])
+            c10 = _lerp(vals[2], vals[3], ax[0][2])
+            c01 = _lerp(vals[4], vals[5], ax[0][2])
+            c11 = _lerp(vals[6], vals[7], ax[0][2])
+            sample = _lerp(_lerp(c00, c10, ax[1][2]), _lerp(c01, c11, ax[1][2]), ax[2][2])
         else:
             comp = method - 1 if method <= 3 else method - 4
             sfun = stat if method <= 3 else codec_stat  # 4/5/6: vol = codec_decode(...)
@@ -251,3 +279,100 @@ def codec_stat(dec, comp):
         d = c - mean.astype(np.float64)
         var = (var.astype(np.float64) + dec[..., i].astype(np.float64) * d * d).astype(np.float32)
     return (var.astype(np.float64) / 0.000021).astype(np.float32)
+
+
+# ---- flexible-block pre-pass (dataProcessing, K:892-1126, 1142-1544) ----
+
+def _split(x):
+    out = []
+    for i in range(7):
+        if x & (1 << i):
+            out.append((x & ~(1 << i)) + 1)
+            out[-1] = (out[-1], x)
+            x &= ~(1 << i)
+        if x == 0:
+            break
+    return out
+
+
+def _table(low, high):
+    """span -> entry the reference's scan returns (last row with a match, first in it)"""
+    best = {}
+    for i in range(low.shape[0]):
+        key = tuple(low[i, :3].tolist()) + tuple(high[i, :3].tolist())
+        if key not in best or best[key] // 64 != i // 64:
+            best[key] = i
+    return best
+
+
+def flex_process(t):
+    """(n, n, n, 4) float32 block statistics, [z, y, x]"""
+    D, bs, nb = t["dim"], t["block"], t["nbins"]
+    ftab = _table(t["fractal_low"], t["fractal_high"])
+    stab = _table(t["simple_low"], t["simple_high"])
+    tp = np.asarray(t["templates"], np.float32)
+
+    def span_hist(lo, hi):
+        size = (hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1)
+        if size >= 8:
+            e = ftab[tuple(lo) + tuple(hi)]
+            tid, shift, flip, ne = t["fractal_code"][e].tolist()
+            src = tp[tid][::-1] if flip else tp[tid]
+            dec = np.roll(src, shift).astype(np.float32)
+            for b, v in t["fractal_err"][e][:ne].tolist():
+                b = int(b)
+                if 0 <= b < nb:
+                    dec[b] = max(f32(dec[b] + f32(v)), f32(0)) if not np.isnan(dec[b] + f32(v)) else dec[b] + f32(v)
+            tot = f32(0)
+            for q in range(nb):
+                tot = f32(tot + dec[q])
+            return (dec / tot).astype(np.float32), size
+        e = stab[tuple(x - 1 for x in lo) + tuple(x - 1 for x in hi)]
+        h = np.zeros(nb, np.float32)
+        for b, v in t["simple_hist"][e][:t["simple_count"][e]].tolist():
+            if 0 <= int(b) < nb:
+                h[int(b)] = f32(v)
+        return h, size
+
+    def corner(x, y, z):
+        acc = np.zeros(nb, np.float32)
+        for xs in _split(x):
+            for ys in _split(y):
+                for zs in _split(z):
+                    h, w = span_hist((xs[0], ys[0], zs[0]), (xs[1], ys[1], zs[1]))
+                    acc = (acc + h * f32(w)).astype(np.float32)
+        return acc
+
+    n = (D + bs - 1) // bs
+    out = np.zeros((n, n, n, 4), np.float32)
+    bw = f32(255) / f32(nb)
+    enorm = f32(np.log(np.float64(f32(nb)))) / f32(np.log(2.0))
+    for bz in range(n):
+        for by in range(n):
+            for bx in range(n):
+                lo = [1 + bx * bs, 1 + by * bs, 1 + bz * bs]
+                hi = [D if b == n - 1 else (b + 1) * bs for b in (bx, by, bz)]
+                c = [corner(hi[0] if k & 1 else lo[0], hi[1] if k & 2 else lo[1],
+                            hi[2] if k & 4 else lo[2]) for k in range(8)]
+                h = c[0] + c[3] + c[4] + c[7] - c[1] - c[2] - c[5] - c[6]
+                h = np.where(h < 0, f32(0), h).astype(np.float32)
+                tot = f32(0)
+                for q in range(nb):
+                    tot = f32(tot + h[q])
+                if not tot <= 0:
+                    h = np.clip(h / tot, f32(0), f32(1)).astype(np.float32)
+                mean = f32(0)
+                for i in range(nb):
+                    mean = f32(np.float64(mean) + np.float64(h[i]) *
+                               (np.float64(bw * f32(i)) + np.float64(bw) / 2.0))
+                var = f32(0)
+                for i in range(nb):
+                    dd = (np.float64(bw * f32(i)) + np.float64(bw) / 2.0) - np.float64(mean)
+                    var = f32(np.float64(var) + np.float64(h[i]) * dd * dd)
+                ent = f32(0)
+                for i in range(nb):
+                    p = h[i]
+                    tt = 0.0 if p <= 0 else np.float64(f32(np.log(np.float64(p)))) / LN2
+                    ent = f32(np.float64(ent) + np.float64(p) * tt)
+                out[bz, by, bx] = (mean, var, f32(-ent) / enorm, 0)
+    return out

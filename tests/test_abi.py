@@ -56,8 +56,8 @@ def test_errors_without_gpu(pkg):
                           (4, 4, 4))
     assert e.value.status == pkg._lib.VR_ERR_STATE
     with pytest.raises(pkg.VRError) as e:
-        pkg.dataProcessing()
-    assert e.value.status == pkg._lib.VR_ERR_UNSUPPORTED
+        pkg.dataProcessing()  # no span tables resident
+    assert e.value.status == pkg._lib.VR_ERR_STATE
     with pytest.raises(pkg.VRError):
         pkg.basicDataProcessing()
     with pytest.raises(pkg.VRError):
@@ -68,3 +68,26 @@ def test_errors_without_gpu(pkg):
     assert pkg._lib.load().vr_tiles_x(1920) == pkg.tiles.tiles_x(1920) == 30
     assert pkg._lib.load().vr_tiles_y(1080) == pkg.tiles.tiles_y(1080) == 270
     assert "gfx950" in pkg.version()
+
+
+def test_flex_table_validation_without_gpu(pkg, orc):
+    """vr_init_flex rejects out-of-range tables before touching the device"""
+    t = orc.synth_flex(12, 5, 16, ntemplates=6, extra=0, dup=False)
+    bad = [("dim", 0), ("dim", 127), ("nbins", 65)]
+    for k, v in bad:
+        u = dict(t)
+        u[k] = v
+        with pytest.raises(pkg.VRError) as e:
+            pkg.init_flex(u)
+        assert e.value.status == pkg._lib.VR_ERR_ARG
+    for col, v in ((0, 6), (0, -1), (1, 16), (3, 17)):  # template id, shift, NE
+        u = dict(t)
+        u["fractal_code"] = t["fractal_code"].copy()
+        u["fractal_code"][3, col] = v
+        with pytest.raises(pkg.VRError, match="fractal entry 3"):
+            pkg.init_flex(u)
+    u = dict(t)
+    u["simple_count"] = t["simple_count"].copy()
+    u["simple_count"][2] = 17
+    with pytest.raises(pkg.VRError, match="simple entry 2"):
+        pkg.init_flex(u)

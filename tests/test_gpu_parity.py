@@ -4,6 +4,7 @@ Bar (BASELINE.json north_star): packed RGBA8 identical, float RGBA within
 1e-4 per channel, samples-per-pixel identical, on the same seeded inputs.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -17,7 +18,7 @@ def gpu_render(pkg, vol_or_none, W, H, m, method, torch, density=0.05, brightnes
                toff=0.0, tscale=1.0, m7=None, tile_list=None):
     if vol_or_none is not None:
         pkg.init_distribution(vol_or_none)
-    dims = pkg.volume_info()[0]
+    dims = (1, 1, 1) if m7 or method in (8, 9, 0) else pkg.volume_info()[0]
     out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     out_f = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
     steps = torch.full((H * W,), -2, dtype=torch.int32, device="cuda")
@@ -446,4 +447,128 @@ def test_large_volume_64bit_offsets(pkg, orc, gpu):
     ref = orc.render(vol, orc.make_params(96, 64, m, query_method=1))[:3]
     del vol
     assert_parity(got, ref, "4096x4096x36x8")
+    pkg.freeCudaBuffers()
+
+
+# ---- flexible blocks (methods 8/9/0) ----
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+def _flex_blocks_from_device(pkg):
+    import ctypes
+    n, nb, ptr = pkg.flex_info()
+    got = np.zeros((n, n, n, 4), np.float32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    assert hip.hipMemcpy(ctypes.c_void_p(got.ctypes.data), ctypes.c_void_p(ptr),
+                         ctypes.c_size_t(got.nbytes), 2) == 0
+    return got
+
+
+@pytest.mark.parametrize("dim,block,nb", [(12, 5, 16), (20, 6, 64), (16, 3, 8), (9, 9, 4),
+                                          (64, 6, 64)])
+def test_flex_prepass_matches_oracle(pkg, orc, gpu, dim, block, nb):
+    """vr_flex_process (sorted-key lookups, one workgroup per corner) == the oracle's
+    linear-scan restatement of dataProcessing, bit for bit; 64^3 with 6-voxel blocks
+    is the reference's own configuration (K:106, 1737)"""
+    t = orc.synth_flex(dim, block, nb, ntemplates=9, seed=dim + 31 * block)
+    ref = orc.flex_process(t)
+    pkg.init_flex(t)
+    assert pkg.flex_process(block) == orc.flex_blocks_per_axis(dim, block)
+    got = _flex_blocks_from_device(pkg)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("method", [8, 9, 0])
+def test_flex_render_matches_oracle(pkg, orc, gpu, method):
+    """methods 8/9/0 through render_kernel after initCuda-free vr_init_flex + the
+    reference entry point dataProcessing (6-voxel blocks), both cameras, early exits"""
+    import torch
+    t = orc.synth_flex(22, 6, 32, ntemplates=11, seed=5)
+    pkg.init_flex(t)
+    pkg.dataProcessing()
+    blocks = orc.flex_process({**t, "block": 6})
+    ts = {9: 1 / 255, 0: 1 / 4000, 8: 1.0}[method]
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),
+                pkg.camera.display_inv_view((-60.0, 110.0))):
+        for density in (0.05, 0.6):
+            got = gpu_render(pkg, None, 72, 56, cam, method, torch, density=density, tscale=ts)
+            ref = orc.render_flex(blocks, orc.make_params(72, 56, cam, density=density,
+                                                          transfer_scale=ts,
+                                                          query_method=method))[:3]
+            assert_parity(got, ref, f"flex m{method} d={density}")
+    assert pkg.last_kernel().startswith("k_march_flex")
+
+
+def test_flex_golden_fixtures(pkg, gpu):
+    """the committed flex fixtures (tables in the fixture, tests/golden/make_golden.py)"""
+    import glob
+    import torch
+    files = sorted(glob.glob(os.path.join(GOLDEN_DIR, "flex*.npz")))
+    assert files
+    for path in files:
+        z = np.load(path, allow_pickle=False)
+        dim, block, nb = (int(v) for v in z["flex_dims"])
+        pkg.init_flex({"dim": dim, "nbins": nb, **{k: z[k] for k in (
+            "fractal_low", "fractal_high", "fractal_code", "fractal_err", "simple_low",
+            "simple_high", "simple_count", "simple_hist", "templates")}})
+        pkg.flex_process(block)
+        assert np.array_equal(_flex_blocks_from_device(pkg).view(np.uint32),
+                              z["blocks"].view(np.uint32)), path
+        W, H = (int(v) for v in z["image"])
+        got = gpu_render(pkg, None, W, H, z["inv_view"], int(z["method"]), torch,
+                         density=float(z["density"]), tscale=float(z["tscale"]))
+        assert_parity(got, (z["rgba8"], z["rgba_f"], z["steps"].astype(np.int32)), path)
+
+
+def test_flex_through_initcuda(pkg, orc, gpu):
+    """initCuda's arguments 10-18 at the reference's fixed sizes (64x64x32 entries,
+    64 bins, 469 templates, 64^3 volume) then dataProcessing, as main() does
+    (C:1200-1221)"""
+    import torch
+    t = orc.synth_flex(64, 6, 64, ntemplates=469, seed=11, extra=0, dup=False)
+    N = 64 * 64 * 32
+
+    def pad(a, fill=0):
+        out = np.full((N,) + a.shape[1:], fill, a.dtype)
+        out[:a.shape[0]] = a
+        return out
+    arrays = [pad(t["fractal_low"], -1), pad(t["fractal_high"], -1), pad(t["fractal_code"]),
+              pad(t["fractal_err"]), pad(t["simple_low"], -1), pad(t["simple_high"], -1),
+              pad(t["simple_count"]), pad(t["simple_hist"]), t["templates"]]
+    vol = orc.synth_volume(8, 8, 8, 4)
+    pkg.initCuda(vol, (8, 8, 8), (4, 512, 1), None, None, None, None, None, None, *arrays)
+    pkg.dataProcessing()
+    n, nb, _ = pkg.flex_info()
+    assert (n, nb) == (11, 64)
+    ref = orc.flex_process(t)
+    assert np.array_equal(_flex_blocks_from_device(pkg).view(np.uint32), ref.view(np.uint32))
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    got = gpu_render(pkg, None, 48, 40, m, 8, torch)
+    assert_parity(got, orc.render_flex(ref, orc.make_params(48, 40, m, query_method=8))[:3],
+                  "flex via initCuda")
+    # the histogram volume initCuda made resident is still there for methods 1/2/3
+    got = gpu_render(pkg, None, 48, 40, m, 1, torch)
+    assert_parity(got, orc.render(vol, orc.make_params(48, 40, m, query_method=1))[:3],
+                  "method 1 next to flex")
+
+
+def test_flex_errors(pkg, orc, gpu):
+    import torch
+    pkg.freeCudaBuffers()
+    out = torch.zeros(16, dtype=torch.int32, device="cuda")
+    for m in (8, 9, 0):
+        with pytest.raises(pkg.VRError):
+            pkg.render_kernel((1, 1, 1), (16, 16, 1), out, 4, 4, 0.05, 1.0, 0.0, 1.0, m,
+                              (4, 4, 4))
+    t = orc.synth_flex(10, 4, 8, dup=False, extra=0)
+    pkg.init_flex(t)
+    with pytest.raises(pkg.VRError):
+        pkg.flex_process(11)  # block > dim
+    with pytest.raises(pkg.VRError):  # tables resident but no statistics yet
+        pkg.render_kernel((1, 1, 1), (16, 16, 1), out, 4, 4, 0.05, 1.0, 0.0, 1.0, 8, (4, 4, 4))
+    for k in ("simple_low", "simple_high", "simple_count", "simple_hist"):
+        t[k] = t[k][1:]
+    pkg.init_flex(t)
+    with pytest.raises(pkg.VRError, match="no table"):
+        pkg.flex_process(4)
     pkg.freeCudaBuffers()

@@ -57,6 +57,20 @@ class RenderDesc(ctypes.Structure):
     ]
 
 
+class FlexTables(ctypes.Structure):
+    """vr_flex_tables (include/vr.h)"""
+    _fields_ = [
+        ("dim", ctypes.c_int), ("nbins", ctypes.c_int),
+        ("n_fractal", ctypes.c_int),
+        ("fractal_low", ctypes.c_void_p), ("fractal_high", ctypes.c_void_p),
+        ("fractal_code", ctypes.c_void_p), ("fractal_errors", ctypes.c_void_p),
+        ("n_simple", ctypes.c_int),
+        ("simple_low", ctypes.c_void_p), ("simple_high", ctypes.c_void_p),
+        ("simple_count", ctypes.c_void_p), ("simple_hist", ctypes.c_void_p),
+        ("templates", ctypes.c_void_p), ("ntemplates", ctypes.c_int),
+    ]
+
+
 # every symbol include/vr.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers",
@@ -64,7 +78,7 @@ EXPORTS = [
     "vr_last_error", "vr_last_status", "vr_clear_error", "vr_init_distribution", "vr_init_codec", "vr_synthesize_codec", "vr_codec_info",
     "vr_synthesize", "vr_volume_info", "vr_footprint_bytes", "vr_volume_layout", "vr_set_stream", "vr_render", "vr_count_footprint",
     "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version", "vr_last_kernel", "vr_selftest_logf", "vr_parse_codebook", "vr_parse_templates",
-    "vr_load_reference_files",
+    "vr_load_reference_files", "vr_init_flex", "vr_flex_process", "vr_flex_info",
 ]
 
 _lib = None
@@ -142,6 +156,12 @@ def load() -> ctypes.CDLL:
     L.vr_codec_info.restype = i32
     L.vr_footprint_bytes.argtypes = [ctypes.POINTER(RenderDesc)]
     L.vr_footprint_bytes.restype = ctypes.c_int64
+    L.vr_init_flex.argtypes = [ctypes.POINTER(FlexTables)]
+    L.vr_init_flex.restype = i32
+    L.vr_flex_process.argtypes = [i32]
+    L.vr_flex_process.restype = i32
+    L.vr_flex_info.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), vp]
+    L.vr_flex_info.restype = i32
     L.vr_last_kernel.argtypes = []
     L.vr_last_kernel.restype = ctypes.c_char_p
     _lib = L

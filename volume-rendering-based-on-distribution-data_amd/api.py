@@ -78,7 +78,10 @@ def initCuda(h_histogram, volumeSize, histogramSize, h_codebook=None, codebookSi
     h_templates (fp32 [T, B]) and h_errorsbook (fp32 [..., slots, 2]) make the
     codec volume of methods 4/5/6 resident (sizes as the reference passes them:
     codebookSize = volumeSize, templatesSize = (B, T, 1), errorsbookSize =
-    (slots, rows, layers)); the flexible-block arrays are accepted and ignored."""
+    (slots, rows, layers)).  flexible_arrays: the nine span-table arrays of
+    arguments 10-18 (codebookSpanLow, codebookSpanHigh, flexibleCodebook,
+    flexibleErrorsbook, simpleLow, simpleHigh, simpleCount, simpleHistogram,
+    flexibleTemplates) at the reference's fixed sizes (vr_init_flex)."""
     h = np.ascontiguousarray(np.asarray(h_histogram, dtype=np.float32))
     L = _lib.load()
     z = Extent(0, 0, 0)
@@ -95,8 +98,53 @@ def initCuda(h_histogram, volumeSize, histogramSize, h_codebook=None, codebookSi
                arr(h_codebook, np.int32), _extent(codebookSize) if codebookSize else z,
                arr(h_templates, np.float32), _extent(templatesSize) if templatesSize else z,
                arr(h_errorsbook, np.float32), _extent(errorsbookSize) if errorsbookSize else z,
-               None, None, None, None, None, None, None, None, None)
+               *_flex_initcuda_args(flexible_arrays, arr))
     check_last()
+
+
+def _flex_initcuda_args(flexible_arrays, arr):
+    if not flexible_arrays:
+        return [None] * 9
+    if len(flexible_arrays) != 9:
+        raise ValueError("initCuda takes all nine flexible-block arrays or none")
+    types = [np.int32] * 3 + [np.float32] + [np.int32] * 3 + [np.float32] * 2
+    return [arr(a, t) for a, t in zip(flexible_arrays, types)]
+
+
+def init_flex(tables: dict) -> None:
+    """Make flexible-block span tables resident (methods 8/9/0; vr_init_flex).
+    tables: dim, nbins, fractal_low/high/code int32 (n, 4), fractal_err float32
+    (n, nbins, 2), simple_low/high int32 (m, 4), simple_count int32 (m,),
+    simple_hist float32 (m, nbins, 2), templates float32 (T, nbins)."""
+    keep = {}
+    for k, dt in (("fractal_low", np.int32), ("fractal_high", np.int32),
+                  ("fractal_code", np.int32), ("fractal_err", np.float32),
+                  ("simple_low", np.int32), ("simple_high", np.int32),
+                  ("simple_count", np.int32), ("simple_hist", np.float32),
+                  ("templates", np.float32)):
+        keep[k] = np.ascontiguousarray(tables[k], dtype=dt)
+    t = _lib.FlexTables()
+    t.dim, t.nbins = int(tables["dim"]), int(tables["nbins"])
+    t.n_fractal, t.n_simple = keep["fractal_low"].shape[0], keep["simple_low"].shape[0]
+    t.ntemplates = keep["templates"].shape[0]
+    t.fractal_low, t.fractal_high = keep["fractal_low"].ctypes.data, keep["fractal_high"].ctypes.data
+    t.fractal_code, t.fractal_errors = keep["fractal_code"].ctypes.data, keep["fractal_err"].ctypes.data
+    t.simple_low, t.simple_high = keep["simple_low"].ctypes.data, keep["simple_high"].ctypes.data
+    t.simple_count, t.simple_hist = keep["simple_count"].ctypes.data, keep["simple_hist"].ctypes.data
+    t.templates = keep["templates"].ctypes.data
+    check(_lib.load().vr_init_flex(ctypes.byref(t)))
+
+
+def flex_process(block: int) -> int:
+    """dataProcessing with `block`-voxel blocks (vr_flex_process); returns blocks per axis."""
+    return int(check(_lib.load().vr_flex_process(int(block))))
+
+
+def flex_info():
+    """(blocks per axis, bins, device pointer of the float4 block statistics)"""
+    n, nb, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_void_p()
+    check(_lib.load().vr_flex_info(ctypes.byref(n), ctypes.byref(nb), ctypes.byref(p)))
+    return n.value, nb.value, p.value
 
 
 def init_codec(codebook, templates, errors) -> None:
@@ -137,7 +185,7 @@ def basicDataProcessing() -> None:
 
 
 def dataProcessing() -> None:
-    """dataProcessing, K:1735-1796: flexible-block pre-pass, out of scope (raises)."""
+    """dataProcessing, K:1735-1796: flexible-block pre-pass with 6-voxel blocks."""
     _lib.load().dataProcessing()
     check_last()
 
@@ -271,7 +319,8 @@ def version() -> str:
 
 __all__ = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers", "setTextureFilterMode",
-    "basicDataProcessing", "dataProcessing", "init_distribution", "init_codec", "synthesize", "synthesize_codec", "codec_info",
+    "basicDataProcessing", "dataProcessing", "init_distribution", "init_codec", "init_flex",
+    "flex_process", "flex_info", "synthesize", "synthesize_codec", "codec_info",
     "volume_info",
     "volume_layout",
     "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "version",

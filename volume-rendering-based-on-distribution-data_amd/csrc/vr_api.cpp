@@ -32,6 +32,17 @@ struct State {
     float *tpl = nullptr;
     float2 *cerr = nullptr;
     int cnx = 0, cny = 0, cnz = 0, cnb = 0, ntpl = 0, err_slots = 0;
+    // flexible blocks (methods 8/9/0): span tables, then the block statistics
+    struct Flex {
+        int dim = 0, nb = 0, ntpl = 0, nf = 0, ns = 0, nfk = 0, nsk = 0;
+        uint64_t *fkeys = nullptr, *skeys = nullptr;
+        int32_t *fidx = nullptr, *sidx = nullptr, *scount = nullptr;
+        int4 *fcode = nullptr;
+        float2 *ferr = nullptr, *shist = nullptr;
+        float *tpl = nullptr;
+        float4 *blocks = nullptr;
+        int nblk = 0;
+    } flex;
     // full-frame workgroup -> tile order (frame_order), cached per frame shape
     uint32_t *perm = nullptr;
     size_t perm_cap = 0;
@@ -105,11 +116,32 @@ void release_codec() {
     g.cnx = g.cny = g.cnz = g.cnb = g.ntpl = g.err_slots = 0;
 }
 
+void release_flex_blocks() {
+    if (g.flex.blocks) (void)hipFree(g.flex.blocks);
+    g.flex.blocks = nullptr;
+    g.flex.nblk = 0;
+}
+
+void release_flex() {
+    release_flex_blocks();
+    void *ptrs[] = {g.flex.fkeys, g.flex.skeys, g.flex.fidx, g.flex.sidx, g.flex.scount,
+                    g.flex.fcode, g.flex.ferr, g.flex.shist, g.flex.tpl};
+    for (void *q : ptrs)
+        if (q) (void)hipFree(q);
+    g.flex = State::Flex();
+}
+
+bool is_flex_method(int m) { return m == 8 || m == 9 || m == 0; }
+
 int check_method(int m) {
     if (m == 1 || m == 2 || m == 3 || m == 7 || m == 4 || m == 5 || m == 6) return VR_OK;
-    if (m == 8 || m == 9 || m == 0)
-        return fail(VR_ERR_UNSUPPORTED,
-                    "queryMethod %d needs the flexible-block pre-pass (out of scope)", m);
+    if (is_flex_method(m)) {
+        if (!g.flex.blocks)
+            return fail(VR_ERR_STATE,
+                        "queryMethod %d needs the flexible-block statistics (span tables via "
+                        "initCuda / vr_init_flex, then dataProcessing / vr_flex_process)", m);
+        return VR_OK;
+    }
     return fail(VR_ERR_ARG, "unknown queryMethod %d", m);
 }
 
@@ -215,7 +247,9 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     if (codec && !g.cb)
         return fail(VR_ERR_STATE, "queryMethod %d needs a codec volume (initCuda's codebook / "
                                   "vr_init_codec)", d->query_method);
-    if (!codec && !g.vol) return fail(VR_ERR_STATE, "no volume resident (initCuda / vr_init_* first)");
+    const bool flex = is_flex_method(d->query_method);
+    if (!codec && !flex && !g.vol)
+        return fail(VR_ERR_STATE, "no volume resident (initCuda / vr_init_* first)");
     if (!d->d_output) return fail(VR_ERR_ARG, "d_output is null");
     if (d->width == 0 || d->height == 0) return fail(VR_ERR_ARG, "empty image");
     int rc = check_method(d->query_method);
@@ -249,6 +283,11 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
         P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
         P.sy = g.sy; P.sz = g.sz;
         P.nb = g.nb;
+    }
+    if (flex) {
+        P.flex = g.flex.blocks;
+        P.nflex = g.flex.nblk;
+        P.nb = g.flex.nb;
     }
     P.m7x = (int)d->volume_size.width;
     P.m7y = (int)d->volume_size.height;
@@ -342,6 +381,43 @@ void blob_axis(int n, double c, double s, float *out) {
 
 namespace vr {
 int record_error(int status, const char *msg) { return fail(status, "%s", msg); }
+// Span index: sorted keys and, per key, the entry the reference's linear scan
+// (K:1352-1372) returns -- its `break` leaves only the x loop, so among equal
+// spans the last 64-entry row holding one wins, and its first entry.  Entries
+// with a coordinate outside [0, 1023] can never match a sub-span and are left out.
+void build_span_index(const vr_int4 *lo, const vr_int4 *hi, int n,
+                             std::vector<uint64_t> &keys, std::vector<int32_t> &idx) {
+    std::vector<std::pair<uint64_t, int32_t>> kv;
+    kv.reserve((size_t)n);
+    for (int i = 0; i < n; i++) {
+        const int c[6] = {lo[i].x, lo[i].y, lo[i].z, hi[i].x, hi[i].y, hi[i].z};
+        bool ok = true;
+        for (int q = 0; q < 6; q++) ok = ok && c[q] >= 0 && c[q] < 1024;
+        if (ok) kv.push_back({vr::span_key(c[0], c[1], c[2], c[3], c[4], c[5]), i});
+    }
+    std::sort(kv.begin(), kv.end());
+    keys.clear();
+    idx.clear();
+    for (size_t a = 0; a < kv.size();) {
+        size_t b = a;
+        while (b < kv.size() && kv[b].first == kv[a].first) b++;
+        const int32_t last_row = kv[b - 1].second / 64;
+        size_t pick = a;
+        while (kv[pick].second / 64 != last_row) pick++;
+        keys.push_back(kv[a].first);
+        idx.push_back(kv[pick].second);
+        a = b;
+    }
+}
+
+template <typename T>
+hipError_t upload(T *&dst, const T *src, size_t n) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipMalloc(&dst, n * sizeof(T));
+    if (e == hipSuccess) e = hipMemcpy(dst, src, n * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+
 }  // namespace vr
 
 extern "C" {
@@ -432,6 +508,125 @@ int vr_init_codec(const vr_int4 *codebook, vr_extent dims, const float *template
     g.ntpl = ntemplates;
     g.err_slots = err_slots;
     return VR_OK;
+}
+
+int vr_init_flex(const vr_flex_tables *t) {
+    if (!t) return fail(VR_ERR_ARG, "vr_init_flex: null tables");
+    if (t->dim < 1 || t->dim > vr::kFlexMaxDim)
+        return fail(VR_ERR_ARG, "vr_init_flex: dim %d outside [1, %d]", t->dim, vr::kFlexMaxDim);
+    if (t->nbins < 1 || t->nbins > vr::kFlexMaxBins)
+        return fail(VR_ERR_ARG, "vr_init_flex: nbins %d outside [1, %d]", t->nbins,
+                    vr::kFlexMaxBins);
+    if (t->n_fractal < 0 || t->n_simple < 0 || (t->n_fractal > 0 && t->ntemplates < 1))
+        return fail(VR_ERR_ARG, "vr_init_flex: bad table sizes");
+    if ((t->n_fractal > 0 && (!t->fractal_low || !t->fractal_high || !t->fractal_code ||
+                              !t->fractal_errors || !t->templates)) ||
+        (t->n_simple > 0 && (!t->simple_low || !t->simple_high || !t->simple_count ||
+                             !t->simple_hist)))
+        return fail(VR_ERR_ARG, "vr_init_flex: null array");
+    const int nb = t->nbins;
+    for (int i = 0; i < t->n_fractal; i++) {  // K:1377-1385 (the reference only prints)
+        const vr_int4 c = t->fractal_code[i];
+        if (c.x < 0 || c.x >= t->ntemplates || c.y < 0 || c.y >= nb || c.w < 0 || c.w > nb)
+            return fail(VR_ERR_ARG,
+                        "vr_init_flex: fractal entry %d out of range (template %d of %d, shift %d, "
+                        "NE %d, %d bins)", i, c.x, t->ntemplates, c.y, c.w, nb);
+    }
+    for (int i = 0; i < t->n_simple; i++)
+        if (t->simple_count[i] < 0 || t->simple_count[i] > nb)
+            return fail(VR_ERR_ARG, "vr_init_flex: simple entry %d has %d bins", i,
+                        t->simple_count[i]);
+    std::vector<uint64_t> fk, sk;
+    std::vector<int32_t> fi, si;
+    vr::build_span_index(t->fractal_low, t->fractal_high, t->n_fractal, fk, fi);
+    vr::build_span_index(t->simple_low, t->simple_high, t->n_simple, sk, si);
+    release_flex();
+    State::Flex &f = g.flex;
+    hipError_t e = vr::upload(f.fkeys, fk.data(), fk.size());
+    if (e == hipSuccess) e = vr::upload(f.fidx, fi.data(), fi.size());
+    if (e == hipSuccess) e = vr::upload(f.skeys, sk.data(), sk.size());
+    if (e == hipSuccess) e = vr::upload(f.sidx, si.data(), si.size());
+    if (e == hipSuccess)
+        e = vr::upload(f.fcode, reinterpret_cast<const int4 *>(t->fractal_code), (size_t)t->n_fractal);
+    if (e == hipSuccess)
+        e = vr::upload(f.ferr, reinterpret_cast<const float2 *>(t->fractal_errors),
+                   (size_t)t->n_fractal * nb);
+    if (e == hipSuccess) e = vr::upload(f.scount, t->simple_count, (size_t)t->n_simple);
+    if (e == hipSuccess)
+        e = vr::upload(f.shist, reinterpret_cast<const float2 *>(t->simple_hist),
+                   (size_t)t->n_simple * nb);
+    if (e == hipSuccess && t->n_fractal > 0)
+        e = vr::upload(f.tpl, t->templates, (size_t)t->ntemplates * nb);
+    if (e != hipSuccess) {
+        release_flex();
+        return hip_fail(e, "vr_init_flex");
+    }
+    f.dim = t->dim;
+    f.nb = nb;
+    f.ntpl = t->ntemplates;
+    f.nf = t->n_fractal;
+    f.ns = t->n_simple;
+    f.nfk = (int)fk.size();
+    f.nsk = (int)sk.size();
+    return VR_OK;
+}
+
+int vr_flex_process(int block) {
+    State::Flex &f = g.flex;
+    if (f.dim == 0) return fail(VR_ERR_STATE, "vr_flex_process: no span tables (vr_init_flex)");
+    if (block < 1 || block > f.dim)
+        return fail(VR_ERR_ARG, "vr_flex_process: block %d outside [1, %d]", block, f.dim);
+    const int nblk = (f.dim + block - 1) / block;  // K:906-931
+    const size_t nblocks = (size_t)nblk * nblk * nblk;
+    release_flex_blocks();
+    vr::FlexTables T;
+    T.dim = f.dim;
+    T.nb = f.nb;
+    T.fkeys = f.fkeys;
+    T.fidx = f.fidx;
+    T.nfk = f.nfk;
+    T.fcode = f.fcode;
+    T.ferr = f.ferr;
+    T.skeys = f.skeys;
+    T.sidx = f.sidx;
+    T.nsk = f.nsk;
+    T.scount = f.scount;
+    T.shist = f.shist;
+    T.tpl = f.tpl;
+    float *ch = nullptr;
+    unsigned int *missing = nullptr, hmiss = 0;
+    float4 *blocks = nullptr;
+    hipError_t e = hipMalloc(&ch, nblocks * 8 * f.nb * sizeof(float) + 256);
+    if (e == hipSuccess) e = hipMalloc(&blocks, nblocks * sizeof(float4));
+    if (e == hipSuccess) {
+        missing = reinterpret_cast<unsigned int *>(ch + nblocks * 8 * f.nb);
+        e = hipMemsetAsync(missing, 0, sizeof(unsigned int), g.stream);
+    }
+    if (e == hipSuccess) e = vr::launch_flex_corners(T, block, nblk, ch, missing, g.stream);
+    if (e == hipSuccess) e = vr::launch_flex_blocks(f.nb, nblk, ch, blocks, g.stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(&hmiss, missing, sizeof hmiss, hipMemcpyDeviceToHost, g.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    if (ch) (void)hipFree(ch);
+    if (e != hipSuccess) {
+        if (blocks) (void)hipFree(blocks);
+        return hip_fail(e, "vr_flex_process");
+    }
+    if (hmiss) {
+        (void)hipFree(blocks);
+        return fail(VR_ERR_ARG, "vr_flex_process: a sub-span of some block corner has no table "
+                                "entry (the reference reads an uninitialised codebook entry)");
+    }
+    f.blocks = blocks;
+    f.nblk = nblk;
+    return nblk;
+}
+
+int vr_flex_info(int *nblk, int *nbins, const float **d_blocks) {
+    if (nblk) *nblk = g.flex.nblk;
+    if (nbins) *nbins = g.flex.nb;
+    if (d_blocks) *d_blocks = reinterpret_cast<const float *>(g.flex.blocks);
+    return g.flex.blocks ? VR_OK : fail(VR_ERR_STATE, "no flexible-block statistics resident");
 }
 
 int vr_init_distribution(const float *bins, vr_extent dims, int nbins, int where) {
@@ -666,7 +861,9 @@ int vr_render(const vr_render_desc *desc) {
     int rc = fill_params(desc, P, nslots);
     if (rc != VR_OK) return rc;
     hipError_t e;
-    if (desc->query_method >= 4 && desc->query_method <= 6) {
+    if (is_flex_method(desc->query_method)) {
+        e = vr::launch_march_flex(desc->query_method, P, nslots, g.stream);
+    } else if (desc->query_method >= 4 && desc->query_method <= 6) {
         e = vr::launch_march_codec(P.nb, desc->query_method, P, nslots, false, g.stream);
         if (e == hipErrorInvalidValue)
             return fail(VR_ERR_UNSUPPORTED, "codec volumes with %d bins (compiled: 1,2,4,8,16,32)",
@@ -784,10 +981,6 @@ void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
               vr_int4 *h_flexibleCodebook, vr_float2 *h_flexibleErrorsbook,
               vr_int4 *h_simpleLow, vr_int4 *h_simpleHigh, int *h_simpleCount,
               vr_float2 *h_simpleHistogram, float *h_flexibleTemplates) {
-    // arrays 10-18 feed the flexible-block methods 8/9/0 only (out of scope)
-    (void)h_codebookSpanLow; (void)h_codebookSpanHigh; (void)h_flexibleCodebook;
-    (void)h_flexibleErrorsbook; (void)h_simpleLow; (void)h_simpleHigh; (void)h_simpleCount;
-    (void)h_simpleHistogram; (void)h_flexibleTemplates;
     const size_t nvox = volumeSize.width * volumeSize.height * volumeSize.depth;
     if (histogramSize.width == 0 || histogramSize.height * histogramSize.depth != nvox) {
         fail(VR_ERR_ARG,
@@ -815,11 +1008,34 @@ void initCuda(void *h_histogram, vr_extent volumeSize, vr_extent histogramSize,
         (void)vr_init_codec(h_codebook, codebookSize, h_templates, (int)templatesSize.height,
                             h_errorsbook, (int)errorsbookSize.width, (int)templatesSize.width, 0);
     }
+    // flexible-block span tables (methods 8/9/0, K:2052-2320) with the
+    // reference's fixed sizes: 64x64x32 fractal and simple entries
+    // (flexibleVolumeSize, K:99), 64 bins, 469 templates (K:98, 101), a 64^3
+    // raw volume (K:106)
+    if (h_codebookSpanLow && h_codebookSpanHigh && h_flexibleCodebook && h_flexibleErrorsbook &&
+        h_simpleLow && h_simpleHigh && h_simpleCount && h_simpleHistogram && h_flexibleTemplates) {
+        vr_flex_tables t;
+        t.dim = 64;
+        t.nbins = 64;
+        t.n_fractal = t.n_simple = 64 * 64 * 32;
+        t.fractal_low = h_codebookSpanLow;
+        t.fractal_high = h_codebookSpanHigh;
+        t.fractal_code = h_flexibleCodebook;
+        t.fractal_errors = h_flexibleErrorsbook;
+        t.simple_low = h_simpleLow;
+        t.simple_high = h_simpleHigh;
+        t.simple_count = h_simpleCount;
+        t.simple_hist = h_simpleHistogram;
+        t.templates = h_flexibleTemplates;
+        t.ntemplates = 469;
+        (void)vr_init_flex(&t);
+    }
 }
 
 void freeCudaBuffers(void) {
     release_volume();
     release_codec();
+    release_flex();
 }
 
 void setTextureFilterMode(bool bLinearFilter) { g.linear_filter = bLinearFilter; }
@@ -829,8 +1045,7 @@ void basicDataProcessing(void) {
 }
 
 void dataProcessing(void) {
-    fail(VR_ERR_UNSUPPORTED,
-         "dataProcessing: flexible-block pre-pass (methods 8/9/0) is out of scope");
+    (void)vr_flex_process(6);  // blockSize = 6, K:1737
 }
 
 }  // extern "C"

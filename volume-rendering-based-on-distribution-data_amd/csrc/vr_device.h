@@ -50,6 +50,9 @@ struct Params {
     int ntpl, err_slots;
     int tpl_lds;                 // codec march: template table copied to LDS (bytes, 0 = no)
     int seg_lanes;               // ray-segmented march (path 7): lanes per ray
+    // flexible blocks (methods 8/9/0): per-block (mean, variance, entropy, 0)
+    const float4 *flex;
+    int nflex;                   // blocks per axis
 };
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)

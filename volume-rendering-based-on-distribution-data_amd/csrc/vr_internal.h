@@ -45,6 +45,33 @@ hipError_t launch_codec_check(const int4 *cb, uint64_t n, int ntpl, int nb, int 
                               unsigned long long *bad, hipStream_t s);
 hipError_t launch_synth_codec(int4 *cb, float2 *err, const SynthArgs &a, int ntpl, int slots,
                               hipStream_t s);
+// ---- flexible blocks (methods 8/9/0, vr_flex.hip) ----
+// span key: six coordinates of 10 bits, low x/y/z then high x/y/z
+__host__ __device__ inline uint64_t span_key(int lx, int ly, int lz, int hx, int hy, int hz) {
+    return (uint64_t)lx | (uint64_t)ly << 10 | (uint64_t)lz << 20 | (uint64_t)hx << 30 |
+           (uint64_t)hy << 40 | (uint64_t)hz << 50;
+}
+constexpr int kFlexMaxBins = 64;     // flexNBin (K:97)
+constexpr int kFlexMaxDim = 126;     // dyadic split of K:1248-1282 stays within 6 spans per axis
+struct FlexTables {                  // device arrays
+    int dim, nb;
+    const uint64_t *fkeys;           // fractal spans: sorted keys -> chosen entry
+    const int32_t *fidx;
+    int nfk;
+    const int4 *fcode;               // template id, shift, flip, NE
+    const float2 *ferr;              // nb (bin, value) pairs per entry
+    const uint64_t *skeys;           // simple spans (0-based keys)
+    const int32_t *sidx;
+    int nsk;
+    const int32_t *scount;
+    const float2 *shist;             // nb (bin, freq) pairs per entry
+    const float *tpl;                // [ntpl][nb]
+};
+hipError_t launch_flex_corners(const FlexTables &t, int block, int nblk, float *corner_hist,
+                               unsigned int *missing, hipStream_t s);
+hipError_t launch_flex_blocks(int nb, int nblk, const float *corner_hist, float4 *blocks,
+                              hipStream_t s);
+hipError_t launch_march_flex(int method, const Params &P, uint32_t nslots, hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,
