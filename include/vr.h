@@ -281,6 +281,33 @@ long long vr_parse_templates(const char *path, int nbins, long long max_template
 int vr_load_reference_files(const char *histogram_path, const char *codebook_path,
                             const char *templates_path, vr_extent dims, int nbins);
 
+/* Flexible-block input files (methods 8/9/0), the formats of loadSpanList,
+ * loadFractalHistogram, loadSimpleHistogram and loadFlexibleTemplates
+ * (C:709-997; layouts in vr_io.cpp).  Each parser writes min(count, max)
+ * entries (outputs may be NULL) and returns the file's entry count, -1 if
+ * unreadable or truncated, -2 if an entry is rejected the way the reference's
+ * loader rejects it, -3 (fractal) if a spanId lies past the span list.
+ *   span list: low/high int4 (x, y, z, 0);
+ *   fractal spans: low/high = the span list's entry spanId, code int4
+ *     (template id, shift, flip, NE), errors nbins (bin, value) float pairs;
+ *   simple spans: low/high int4, count, hist nbins (bin, freq) float pairs. */
+long long vr_parse_span_list(const char *path, long long max, int32_t *low, int32_t *high);
+long long vr_parse_fractal_histogram(const char *path, const int32_t *span_low,
+                                     const int32_t *span_high, long long nspans, int nbins,
+                                     long long max, int32_t *low, int32_t *high, int32_t *code,
+                                     float *errors);
+long long vr_parse_simple_histogram(const char *count_path, const char *binid_path,
+                                    const char *binfreq_path, int nbins, long long max,
+                                    int32_t *low, int32_t *high, int32_t *count, float *hist);
+
+/* Parse all six flexible-block files (flexible templates in the templates
+ * format, values in [0, 1]) and make the span tables resident (vr_init_flex)
+ * for a dim^3 raw volume, as main() does (C:1170-1203). */
+int vr_load_flex_files(const char *span_list_path, const char *fractal_path,
+                       const char *simple_count_path, const char *simple_binid_path,
+                       const char *simple_binfreq_path, const char *templates_path, int dim,
+                       int nbins);
+
 /* library version string */
 const char *vr_version(void);
 

@@ -359,7 +359,7 @@ def synth_flex(dim, block, nbins=64, ntemplates=40, seed=20261015, extra=50, dup
         a = rng.integers(1, dim + 1, 3)
         b = np.minimum(a + rng.integers(0, 4, 3), dim)
         frac.append((tuple(a), tuple(b)))
-        simp.append((tuple(a - 1), tuple(b - 1)))
+        simp.append((tuple(a), tuple(b)))
     if dup:  # the same span again, later: the later 64-entry row wins (K:1352-1372)
         for lst in (frac, simp):
             k = len(lst)

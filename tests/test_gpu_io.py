@@ -93,3 +93,25 @@ def test_single_test_tool(pkg, orc, gpu, tmp_path):
                         "--width=64", "--height=64", f"--out={out}"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+def test_flex_files_render(pkg, orc, gpu, tmp_path):
+    """the six flexible-block files -> vr_load_flex_files -> dataProcessing (6-voxel
+    blocks) -> methods 8/9/0 equal the oracle on the same tables"""
+    import torch
+    t = orc.synth_flex(20, 6, 32, ntemplates=8, seed=9)
+    paths = F.write_flex_files(str(tmp_path), t)
+    pkg.load_flex_files(*paths, dim=20, nbins=32)
+    pkg.dataProcessing()
+    blocks = orc.flex_process(t)
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    for method, ts in ((8, 1.0), (9, 1 / 255), (0, 1 / 4000)):
+        out = torch.zeros(40 * 48, dtype=torch.int32, device="cuda")
+        pkg.render(pkg.make_desc(out, 48, 40, m, density=0.3, transfer_scale=ts,
+                                 query_method=method))
+        torch.cuda.synchronize()
+        ref = orc.render_flex(blocks, orc.make_params(48, 40, m, density=0.3, transfer_scale=ts,
+                                                      query_method=method))[0]
+        assert np.array_equal(out.cpu().numpy().view(np.uint32).reshape(40, 48), ref)
+    pkg.freeCudaBuffers()

@@ -79,6 +79,8 @@ EXPORTS = [
     "vr_synthesize", "vr_volume_info", "vr_footprint_bytes", "vr_volume_layout", "vr_set_stream", "vr_render", "vr_count_footprint",
     "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version", "vr_last_kernel", "vr_selftest_logf", "vr_parse_codebook", "vr_parse_templates",
     "vr_load_reference_files", "vr_init_flex", "vr_flex_process", "vr_flex_info",
+    "vr_parse_span_list", "vr_parse_fractal_histogram", "vr_parse_simple_histogram",
+    "vr_load_flex_files",
 ]
 
 _lib = None
@@ -162,6 +164,15 @@ def load() -> ctypes.CDLL:
     L.vr_flex_process.restype = i32
     L.vr_flex_info.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), vp]
     L.vr_flex_info.restype = i32
+    ll = ctypes.c_longlong
+    L.vr_parse_span_list.argtypes = [ctypes.c_char_p, ll, vp, vp]
+    L.vr_parse_span_list.restype = ll
+    L.vr_parse_fractal_histogram.argtypes = [ctypes.c_char_p, vp, vp, ll, i32, ll, vp, vp, vp, vp]
+    L.vr_parse_fractal_histogram.restype = ll
+    L.vr_parse_simple_histogram.argtypes = [ctypes.c_char_p] * 3 + [i32, ll, vp, vp, vp, vp]
+    L.vr_parse_simple_histogram.restype = ll
+    L.vr_load_flex_files.argtypes = [ctypes.c_char_p] * 6 + [i32, i32]
+    L.vr_load_flex_files.restype = i32
     L.vr_last_kernel.argtypes = []
     L.vr_last_kernel.restype = ctypes.c_char_p
     _lib = L

@@ -14,7 +14,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import Dim3, Extent, RenderDesc, VRError, check, check_last
+from ._lib import VR_ERR_ARG, Dim3, Extent, RenderDesc, VRError, check, check_last
 
 PAD = 0xFFFFFFFF
 
@@ -133,6 +133,56 @@ def init_flex(tables: dict) -> None:
     t.simple_count, t.simple_hist = keep["simple_count"].ctypes.data, keep["simple_hist"].ctypes.data
     t.templates = keep["templates"].ctypes.data
     check(_lib.load().vr_init_flex(ctypes.byref(t)))
+
+
+def load_flex_files(span_list, fractal, simple_counts, simple_bin_ids, simple_bin_freqs,
+                    templates, dim: int = 64, nbins: int = 64) -> None:
+    """The reference's flexible-block files (spanList.bin, codebook0.bin, nzbCounts0.bin,
+    nzbBinIds0.bin, nzbFreqs0.bin, domainList.bin; C:79-84) -> resident span tables."""
+    args = [str(a).encode() for a in (span_list, fractal, simple_counts, simple_bin_ids,
+                                      simple_bin_freqs, templates)]
+    check(_lib.load().vr_load_flex_files(*args, int(dim), int(nbins)))
+
+
+def parse_flex_files(span_list, fractal, simple_counts, simple_bin_ids, simple_bin_freqs,
+                     templates, dim: int = 64, nbins: int = 64) -> dict:
+    """Parse the flexible-block files on the host into the table dict init_flex takes."""
+    L = _lib.load()
+    sp = str(span_list).encode()
+    n = L.vr_parse_span_list(sp, 0, None, None)
+    if n < 0:
+        raise VRError(VR_ERR_ARG, f"span list: {n}")
+    sl, sh = np.zeros((n, 4), np.int32), np.zeros((n, 4), np.int32)
+    L.vr_parse_span_list(sp, n, sl.ctypes.data, sh.ctypes.data)
+    fp = str(fractal).encode()
+    nf = L.vr_parse_fractal_histogram(fp, sl.ctypes.data, sh.ctypes.data, n, nbins, 0,
+                                      None, None, None, None)
+    if nf < 0:
+        raise VRError(VR_ERR_ARG, f"fractal spans: {nf}")
+    t = {"dim": dim, "nbins": nbins,
+         "fractal_low": np.zeros((nf, 4), np.int32), "fractal_high": np.zeros((nf, 4), np.int32),
+         "fractal_code": np.zeros((nf, 4), np.int32),
+         "fractal_err": np.zeros((nf, nbins, 2), np.float32)}
+    L.vr_parse_fractal_histogram(fp, sl.ctypes.data, sh.ctypes.data, n, nbins, nf,
+                                 t["fractal_low"].ctypes.data, t["fractal_high"].ctypes.data,
+                                 t["fractal_code"].ctypes.data, t["fractal_err"].ctypes.data)
+    paths = [str(p).encode() for p in (simple_counts, simple_bin_ids, simple_bin_freqs)]
+    ns = L.vr_parse_simple_histogram(*paths, nbins, 0, None, None, None, None)
+    if ns < 0:
+        raise VRError(VR_ERR_ARG, f"simple spans: {ns}")
+    t.update({"simple_low": np.zeros((ns, 4), np.int32), "simple_high": np.zeros((ns, 4), np.int32),
+              "simple_count": np.zeros(ns, np.int32),
+              "simple_hist": np.zeros((ns, nbins, 2), np.float32)})
+    L.vr_parse_simple_histogram(*paths, nbins, ns, t["simple_low"].ctypes.data,
+                                t["simple_high"].ctypes.data, t["simple_count"].ctypes.data,
+                                t["simple_hist"].ctypes.data)
+    tp = str(templates).encode()
+    nt = L.vr_parse_templates(tp, nbins, 0, None)
+    if nt <= 0:
+        raise VRError(VR_ERR_ARG, f"flexible templates: {nt}")
+    t["templates"] = np.zeros((nt, nbins), np.float32)
+    L.vr_parse_templates(tp, nbins, nt, t["templates"].ctypes.data)
+    return t
 
 
 def flex_process(block: int) -> int:
@@ -320,7 +370,7 @@ def version() -> str:
 __all__ = [
     "render_kernel", "copyInvViewMatrix", "initCuda", "freeCudaBuffers", "setTextureFilterMode",
     "basicDataProcessing", "dataProcessing", "init_distribution", "init_codec", "init_flex",
-    "flex_process", "flex_info", "synthesize", "synthesize_codec", "codec_info",
+    "flex_process", "flex_info", "load_flex_files", "parse_flex_files", "synthesize", "synthesize_codec", "codec_info",
     "volume_info",
     "volume_layout",
     "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "version",
