@@ -11,5 +11,6 @@ for c in C0 C1; do
   for p in 1 2 3; do cp $R/pmc_$c/p$p/p${p}_counter_collection.csv $D/pmc/${c}_p$p.csv; done
 done
 [ -f $R/pytest_gpu.log ] && cp $R/pytest_gpu.log $D/pytest_gpu.log
+for c in C0 C1; do [ -f $R/rank_sim_$c.log ] && grep -v amdgpu.ids $R/rank_sim_$c.log > $D/rank_sim_1024x8_$c.log; done
 cp $R/traffic.json profiles/traffic.json
 ls $D

@@ -22,4 +22,7 @@ for CAM in C0 C1; do
   done
   python tools/pmc_traffic.py $O/traffic.json "1024x8|$CAM|m1" $O/pmc_${CAM}_p1.log $O/pmc_$CAM/p1 $O/pmc_$CAM/p2 $O/pmc_$CAM/p3 || exit 1
 done
+for CAM in C0 C1; do
+  timeout -k 10 300 python -u tools/rank_sim.py --camera $CAM > $O/rank_sim_$CAM.log 2>&1; guard $? rank-sim-$CAM
+done
 echo done
