@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 4, 5, 6, 7])
     ap.add_argument("--camera", default="C0", choices=["C0", "C1"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="N > 1: keep the estimate-dealt tile lists (no measured-cost re-deal)")
     ap.add_argument("--dump-frame", default="",
                     help="rank 0 saves the last assembled frame (.npy) for checks")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -99,6 +101,32 @@ def cpu_baseline(pkg, cfg_name, m, method, row_stride):
     }
 
 
+def balanced_lists(pkg, lists, world, rank, W, H, m, method, dev, stream, backend):
+    """Re-deal the tiles by measured cost (untimed, once per view): every rank
+    renders its estimate-ordered list once with per-pixel sample counts, the
+    per-tile costs are summed over ranks (one all_reduce of a tiles-sized
+    vector, 32 KB at 1080p) and every rank derives the same cost-dealt lists
+    (tiles.tile_lists_by_cost): ranks and their XCDs get equal work, not only
+    equal pixel counts."""
+    import torch
+    import torch.distributed as dist
+    n_slots = lists.shape[1]
+    n_tiles = pkg.tiles.tiles_x(W) * pkg.tiles.tiles_y(H)
+    with torch.cuda.stream(stream):
+        tl = torch.from_numpy(lists[rank].view(np.int32).copy()).to(dev)
+        buf = torch.zeros(n_slots * 256, dtype=torch.int32, device=dev)
+        steps = torch.full((n_slots * 256,), -1, dtype=torch.int32, device=dev)
+        pkg.render(pkg.make_desc(buf, W, H, m, query_method=method, d_tile_list=tl,
+                                 n_tiles=n_slots, d_steps=steps))
+    torch.cuda.synchronize()
+    cost = torch.from_numpy(pkg.tiles.tile_costs_from_steps(steps.cpu().numpy(), lists[rank],
+                                                            n_tiles))
+    if backend == "nccl":
+        cost = cost.to(dev)
+    dist.all_reduce(cost)
+    return pkg.tiles.tile_lists_by_cost(W, H, world, cost.cpu().numpy())
+
+
 def main():
     args = parse()
     import torch
@@ -136,6 +164,9 @@ def main():
         pkg.synthesize((n, n, n), nb, SEED)
 
     lists = pkg.tiles.tile_lists(W, H, world, m)
+    if world > 1 and not args.no_balance:
+        lists = balanced_lists(pkg, lists, world, rank, W, H, m, args.method, dev, stream,
+                               args.dist_backend)
     n_slots = lists.shape[1]
     frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
     with torch.cuda.stream(stream):
@@ -259,6 +290,8 @@ def main():
                             f"{args.camera}, queryMethod {args.method}",
                 "volume": [n, n, n], "bins": nb, "image": [W, H], "camera": args.camera,
                 "query_method": args.method, "density": 0.05,
+                "tile_deal": (None if world == 1 else "estimate" if args.no_balance
+                              else "measured cost (one untimed frame)"),
                 "parallelism": f"image tiles x{world}" + (
                 (" + RCCL gather" if args.dist_backend == "nccl" else " + gloo host gather")
                 if world > 1 else ""),

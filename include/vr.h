@@ -250,6 +250,12 @@ uint32_t vr_tiles_y(uint32_t height);
  * render_kernel call launched (e.g. "k_march_quad<B=8,M=1>"), "" before any */
 const char *vr_last_kernel(void);
 
+/* Tooling: while d_buf is non-null, every launch of the per-ray pipelined
+ * march writes 3 uint64 per wave at d_buf[(slot*4 + wave)*3]: wall clock at
+ * the wave's start and end (100 MHz) and __smid() (CU id, XCC id in the high
+ * bits).  d_buf must hold 12 * n_slots values.  nullptr turns it off. */
+int vr_debug_wave_clock(uint64_t *d_buf);
+
 /* Device self-test: compares the entropy decode's fast float logarithm with
  * (float)log((double)x) for every positive finite float (synchronous, about a
  * second).  counts[0] = mismatches (must be 0), counts[1] = inputs decided by

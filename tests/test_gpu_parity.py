@@ -209,6 +209,77 @@ def test_tile_split_and_unscatter(pkg, orc, gpu, world):
     assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref)
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_cost_dealt_tile_split(pkg, orc, gpu, world):
+    """measured-cost dealing (bench.py at N > 1): per-pixel steps of the estimate
+    split -> summed tile costs -> tile_lists_by_cost; the re-dealt ranks (PAD
+    slots inside the XCD sublists included) assemble the same frame"""
+    import torch
+    vol = orc.synth_volume(32, 32, 32, 8)
+    pkg.init_distribution(vol)
+    W, H = 200, 136
+    m = pkg.camera.display_inv_view()
+    full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    fsteps = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+    pkg.render(pkg.make_desc(full, W, H, m, query_method=1, d_steps=fsteps))
+    lists = pkg.tiles.tile_lists(W, H, world, m)
+    n_slots = lists.shape[1]
+    ntiles = pkg.tiles.tiles_x(W) * pkg.tiles.tiles_y(H)
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    cost = np.zeros(ntiles, np.int64)
+    for r in range(world):
+        buf = torch.zeros(n_slots * 256, dtype=torch.int32, device="cuda")
+        st = torch.full((n_slots * 256,), -1, dtype=torch.int32, device="cuda")
+        pkg.render(pkg.make_desc(buf, W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots, d_steps=st))
+        torch.cuda.synchronize()
+        cost += pkg.tiles.tile_costs_from_steps(st.cpu().numpy(), lists[r], ntiles)
+    torch.cuda.synchronize()
+    # the split's steps are the full frame's steps
+    assert np.array_equal(cost, pkg.tiles.tile_costs_from_frame(fsteps.cpu().numpy(), W, H))
+    lists2 = pkg.tiles.tile_lists_by_cost(W, H, world, cost)
+    n2 = lists2.shape[1]
+    packed = torch.full((world, n2 * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    dl2 = torch.from_numpy(lists2.view(np.int32).copy()).cuda()
+    for r in range(world):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl2[r],
+                                 n_tiles=n2))
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl2, world, n2, frame, W, H)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full)
+
+
+@pytest.mark.parametrize("adapt", [True, False])
+def test_adaptive_frame_order_renders_identical_frames(pkg, orc, gpu, adapt, monkeypatch):
+    """full frames: the 1st render of a view uses the estimate order and records
+    tile costs, the 2nd re-deals the tiles by them; every frame is the oracle's;
+    a new view / new volume starts over"""
+    import torch
+    if not adapt:
+        monkeypatch.setenv("VR_NO_ADAPT", "1")
+    vol = orc.synth_volume(48, 40, 36, 8)
+    pkg.init_distribution(vol)
+    W, H = 320, 200
+    for m in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((10.0, 20.0))):
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=1), want_float=False,
+                         want_steps=False)[0]
+        for _ in range(4):
+            out = torch.full((W * H,), 0, dtype=torch.int32, device="cuda")
+            pkg.render(pkg.make_desc(out, W, H, m, query_method=1))
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32).reshape(H, W), ref)
+    vol2 = orc.synth_volume(48, 40, 36, 8, seed=7)
+    pkg.init_distribution(vol2)
+    ref2 = orc.render(vol2, orc.make_params(W, H, m, query_method=1), want_float=False,
+                      want_steps=False)[0]
+    for _ in range(3):
+        out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        pkg.render(pkg.make_desc(out, W, H, m, query_method=1))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32).reshape(H, W), ref2)
+
+
 def test_errors_do_not_exit(pkg, gpu):
     import torch
     pkg.freeCudaBuffers()  # no codec volume resident either
@@ -230,7 +301,8 @@ def test_errors_do_not_exit(pkg, gpu):
     ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}), ("5", {}), ("6", {}),
     ("1", {"VR_BOX_MAX": "0"}), ("1", {"VR_BOX_MAX": "64"}), ("0", {"VR_WG_PER_CU": "1"}),
     ("7", {"VR_SEG": "2"}), ("7", {"VR_SEG": "4"}), ("7", {"VR_SEG": "8"}), ("7", {"VR_SEG": "-4"}),
-    ("7", {"VR_SEG": "1"}),
+    ("7", {"VR_SEG": "1"}), ("9", {"VR_HYB": "8", "VR_SEG": "4"}),
+    ("9", {"VR_HYB": "16", "VR_SEG": "2"}), ("9", {"VR_HYB": "1000", "VR_SEG": "8"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, monkeypatch):

@@ -148,3 +148,86 @@ def test_lists_longest_first(pkg, world):
                  for t in sub]
             blocks = [max(c[i:i + T.BLOCK_X * T.BLOCK_Y]) for i in range(0, len(c), T.BLOCK_X * T.BLOCK_Y)]
             assert all(a >= b - 1e-6 for a, b in zip(blocks, blocks[1:]))
+
+
+def _synthetic_cost(pkg, W, H, seed=0):
+    """per-tile costs shaped like a real view: the C0 slab-test lengths x noise"""
+    T = pkg.tiles
+    tx, ty = T.tiles_x(W), T.tiles_y(H)
+    gy, gx = np.mgrid[0:ty, 0:tx]
+    c = T.est_steps(pkg.camera.single_test_inv_view(), W, H, gx * T.TILE_W + T.TILE_W // 2,
+                    gy * T.TILE_H + T.TILE_H // 2)
+    rng = np.random.default_rng(seed)
+    return (4 * c * rng.uniform(0.3, 1.0, c.shape) + 4).astype(np.int64).reshape(-1)
+
+
+def _bin_loads(T, lists, cost):
+    """(world, 8) summed cost per (rank, XCD): entry 8k+g of a list runs on XCD g"""
+    out = np.zeros((lists.shape[0], T.XCDS), dtype=np.int64)
+    for r, l in enumerate(lists):
+        for g in range(T.XCDS):
+            t = l[g::T.XCDS]
+            out[r, g] = cost[t[t != T.PAD].astype(np.int64)].sum()
+    return out
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (512, 512), (33, 17), (16, 16)])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_cost_lists_cover_each_tile_once(pkg, W, H, world):
+    T = pkg.tiles
+    cost = _synthetic_cost(pkg, W, H)
+    lists = T.tile_lists_by_cost(W, H, world, cost)
+    real = lists[lists != T.PAD]
+    assert sorted(real.tolist()) == list(range(T.tiles_x(W) * T.tiles_y(H)))
+    assert lists.shape[0] == world and lists.shape[1] % T.XCDS == 0
+    # equal block counts per (rank, XCD) bin, +-1 block
+    nblk = np.array([[len(set((t // T.tiles_x(W)) // T.BLOCK_Y * 100000 + t % T.tiles_x(W)
+                               for t in l[g::T.XCDS][l[g::T.XCDS] != T.PAD].tolist()))
+                      for g in range(T.XCDS)] for l in lists])
+    assert nblk.max() - nblk.min() <= 1
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_cost_lists_balance_ranks_and_xcds(pkg, world):
+    """measured-cost dealing balances every (rank, XCD) bin far better than the
+    estimate lattice, longest blocks first inside each bin"""
+    T = pkg.tiles
+    W, H = 1920, 1080
+    cost = _synthetic_cost(pkg, W, H, seed=world)
+    by_cost = _bin_loads(T, T.tile_lists_by_cost(W, H, world, cost), cost)
+    by_est = _bin_loads(T, T.tile_lists(W, H, world, pkg.camera.single_test_inv_view()), cost)
+    assert by_cost.max() / by_cost.mean() < 1.01
+    assert by_cost.max() <= by_est.max()
+    lists = T.tile_lists_by_cost(W, H, world, cost)
+    for l in lists:
+        for g in range(T.XCDS):
+            t = l[g::T.XCDS]
+            t = t[t != T.PAD].astype(np.int64)
+            blk = cost[t].reshape(-1, T.BLOCK_Y).sum(1) if len(t) % T.BLOCK_Y == 0 else None
+            if blk is not None:
+                assert np.all(np.diff(blk) <= 0)
+
+
+def test_tile_costs_from_steps(pkg):
+    """per wave (64-pixel row): longest ray + 2; misses (-1) cost 1; PAD slots skipped;
+    the full-frame form agrees with the packed form"""
+    T = pkg.tiles
+    W, H = 128, 8
+    rng = np.random.default_rng(3)
+    frame = rng.integers(-1, 300, size=(H, W)).astype(np.int32)
+    frame[0:4, 64:128] = -1
+    c = T.tile_costs_from_frame(frame, W, H)
+    tx = T.tiles_x(W)
+    for t in range(tx * T.tiles_y(H)):
+        y0, x0 = (t // tx) * T.TILE_H, (t % tx) * T.TILE_W
+        rows = frame[y0:y0 + T.TILE_H, x0:x0 + T.TILE_W]
+        assert c[t] == int((rows.max(axis=1) + 2).sum())
+    assert c[1] == 4
+    lst = np.array([3, T.PAD, 0], dtype=np.uint32)
+    packed = np.full((3, T.TILE_H, T.TILE_W), 7, dtype=np.int32)
+    for s, t in enumerate(lst):
+        if t != T.PAD:
+            y0, x0 = (t // tx) * T.TILE_H, (t % tx) * T.TILE_W
+            packed[s] = frame[y0:y0 + T.TILE_H, x0:x0 + T.TILE_W]
+    cp = T.tile_costs_from_steps(packed.reshape(-1), lst, tx * T.tiles_y(H))
+    assert cp[3] == c[3] and cp[0] == c[0] and cp[1] == 0 and cp[2] == 0

@@ -18,6 +18,7 @@
 #define H 1080
 
 static float M[12];
+static int PF = 0;
 static int LAYOUT = 0; /* 0: x-rows (4 records along x per line), 1: 2x2 (x,y) micro-bricks,
                           2: 2x1x2 (x,z) micro-bricks */
 
@@ -50,7 +51,14 @@ static int ray_lines(int x, int y, int nsteps, uint32_t *out /* 8 per step */) {
     float bx = ix * (-1.0f - ox), by = iy * (-1.0f - oy), bz = iz * (-1.0f - oz);
     float tx = ix * (1.0f - ox), ty = iy * (1.0f - oy), tz = iz * (1.0f - oz);
     float tn = fmaxf(fmaxf(fminf(tx, bx), fminf(ty, by)), fmaxf(fminf(tx, bx), fminf(tz, bz)));
+    float tf = fminf(fminf(fmaxf(tx, bx), fmaxf(ty, by)), fminf(fmaxf(tx, bx), fmaxf(tz, bz)));
     if (tn < 0) tn = 0;
+    /* PF=1: also the step the pipelined kernels prefetch after an early exit */
+    if (PF && nsteps < 500) {
+        float t = tn;
+        for (int i = 0; i < nsteps - 1; i++) t += 0.01f;
+        if (!(t + 0.01f > tf)) nsteps++;
+    }
     float px = ox + dx * tn, py = oy + dy * tn, pz = oz + dz * tn;
     float sx = dx * 0.01f, sy = dy * 0.01f, sz = dz * 0.01f;
     int k = 0;
@@ -89,6 +97,7 @@ int main(int argc, char **argv) {
                           0.35355338f, 1.4142135f, 0.61237246f, -0.5f, 0.61237246f, 2.4494898f};
     memcpy(M, strcmp(argv[2], "C0") == 0 ? c0 : c1, sizeof M);
     if (getenv("LAYOUT")) LAYOUT = atoi(getenv("LAYOUT"));
+    if (getenv("PF")) PF = atoi(getenv("PF"));
     FILE *f = fopen(argv[1], "rb");
     if (!f) return 1;
     int32_t *steps = malloc(sizeof(int32_t) * W * H);

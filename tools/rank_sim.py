@@ -35,7 +35,8 @@ def main():
          else pkg.camera.display_inv_view((30.0, 45.0)))
 
     def timed(fn):
-        fn()
+        for _ in range(3):  # a full frame's 2nd render re-deals its tiles (adaptive order)
+            fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(args.reps):
@@ -56,8 +57,17 @@ def main():
         pk = torch.zeros(k * 256, dtype=torch.int32, device="cuda")
         dk = pkg.make_desc(pk, W, H, m, query_method=args.method, d_tile_list=sel, n_tiles=k)
         print(f"  {k:5d} longest tiles alone: {timed(lambda dk=dk: pkg.render(dk)):.3f} ms")
-    for world in (2, 4, 8):
-        lists = pkg.tiles.tile_lists(W, H, world, None if args.no_lpt else m)
+    # measured per-tile costs of this view (steps of the full frame) for the
+    # cost-dealt lists (tiles.tile_lists_by_cost, what bench.py uses at N > 1)
+    steps = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+    pkg.render(pkg.make_desc(full, W, H, m, query_method=args.method, d_steps=steps))
+    cost = pkg.tiles.tile_costs_from_frame(steps.cpu().numpy(), W, H)
+    modes = [("est", w) for w in (2, 4, 8)] + [("cost", w) for w in (2, 4, 8)]
+    for mode, world in modes:
+        if mode == "est":
+            lists = pkg.tiles.tile_lists(W, H, world, None if args.no_lpt else m)
+        else:
+            lists = pkg.tiles.tile_lists_by_cost(W, H, world, cost)
         slots = lists.shape[1]
         packed = torch.zeros((world, slots * 256), dtype=torch.int32, device="cuda")
         dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
@@ -70,7 +80,7 @@ def main():
         tu = timed(lambda: pkg.unscatter_tiles(packed, dl, world, slots, frame, W, H))
         torch.cuda.synchronize()
         ok = torch.equal(frame, full)
-        print(f"  N={world}: per-rank ms {' '.join(f'{x:.3f}' for x in per)}  max {max(per):.3f}"
+        print(f"  {mode:4s} N={world}: per-rank ms {' '.join(f'{x:.3f}' for x in per)}  max {max(per):.3f}"
               f"  unscatter {tu:.3f}  -> est. speedup {t1 / (max(per) + tu):.2f}x"
               f"  frame {'identical' if ok else 'DIFFERS'}")
 

@@ -80,7 +80,7 @@ EXPORTS = [
     "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version", "vr_last_kernel", "vr_selftest_logf", "vr_parse_codebook", "vr_parse_templates",
     "vr_load_reference_files", "vr_init_flex", "vr_flex_process", "vr_flex_info",
     "vr_parse_span_list", "vr_parse_fractal_histogram", "vr_parse_simple_histogram",
-    "vr_load_flex_files",
+    "vr_load_flex_files", "vr_debug_wave_clock",
 ]
 
 _lib = None
@@ -173,6 +173,8 @@ def load() -> ctypes.CDLL:
     L.vr_parse_simple_histogram.restype = ll
     L.vr_load_flex_files.argtypes = [ctypes.c_char_p] * 6 + [i32, i32]
     L.vr_load_flex_files.restype = i32
+    L.vr_debug_wave_clock.argtypes = [ctypes.c_void_p]
+    L.vr_debug_wave_clock.restype = ctypes.c_int
     L.vr_last_kernel.argtypes = []
     L.vr_last_kernel.restype = ctypes.c_char_p
     _lib = L

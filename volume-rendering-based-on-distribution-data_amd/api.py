@@ -363,6 +363,12 @@ def last_kernel() -> str:
     return _lib.load().vr_last_kernel().decode()
 
 
+def debug_wave_clock(d_buf) -> None:
+    """Tooling: per-wave {start, end, __smid} clocks of the per-ray pipelined
+    march into a device uint64 buffer of 12 * n_slots values (None = off)."""
+    check(_lib.load().vr_debug_wave_clock(None if d_buf is None else _ptr(d_buf)))
+
+
 def version() -> str:
     return _lib.load().vr_version().decode()
 
@@ -373,6 +379,6 @@ __all__ = [
     "flex_process", "flex_info", "load_flex_files", "parse_flex_files", "synthesize", "synthesize_codec", "codec_info",
     "volume_info",
     "volume_layout",
-    "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "version",
+    "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "version",
     "VRError", "PAD",
 ]

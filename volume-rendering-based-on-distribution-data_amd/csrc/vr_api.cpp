@@ -46,8 +46,19 @@ struct State {
     // full-frame workgroup -> tile order (frame_order), cached per frame shape
     uint32_t *perm = nullptr;
     size_t perm_cap = 0;
-    uint32_t perm_key[18] = {0};
+    uint32_t perm_key[22] = {0};
     std::vector<uint32_t> perm_host;
+    // adaptive order (frame_order): 0 none, 1 estimate order in use and per-tile
+    // costs to be recorded, 2 final; cost_recorded: a render recorded into tile_cost
+    int order_state = 0;
+    bool cost_recorded = false;
+    uint32_t *tile_cost = nullptr;
+    size_t tile_cost_cap = 0;
+    unsigned long long *wave_clock = nullptr;  // vr_debug_wave_clock (tooling)
+    // bumped whenever a resident volume / codec / flexible-block set is
+    // released, so an order learned on old data is not reused (the order is a
+    // scheduling hint only: any order renders the same image)
+    uint32_t volume_epoch = 0;
 };
 
 State g;
@@ -74,6 +85,7 @@ int hip_fail(hipError_t e, const char *what) {
     } while (0)
 
 void release_volume() {
+    g.volume_epoch++;
     if (g.vol && g.owned) (void)hipFree(g.vol);
     g.vol = nullptr;
     g.owned = false;
@@ -107,6 +119,7 @@ uint32_t tiles_x(uint32_t w) { return (w + vr::kTileW - 1) / vr::kTileW; }
 uint32_t tiles_y(uint32_t h) { return (h + vr::kTileH - 1) / vr::kTileH; }
 
 void release_codec() {
+    g.volume_epoch++;
     if (g.cb) (void)hipFree(g.cb);
     if (g.tpl) (void)hipFree(g.tpl);
     if (g.cerr) (void)hipFree(g.cerr);
@@ -117,6 +130,7 @@ void release_codec() {
 }
 
 void release_flex_blocks() {
+    g.volume_epoch++;
     if (g.flex.blocks) (void)hipFree(g.flex.blocks);
     g.flex.blocks = nullptr;
     g.flex.nblk = 0;
@@ -176,7 +190,77 @@ float est_steps(const float *M, uint32_t W, uint32_t H, float x, float y) {
 // the frame ends no earlier than its longest tile started plus that tile's
 // length.  VR_XBLOCK="bx,by" (default 1,4 = 64x16 pixels; "0" = plain raster
 // order).
-int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_t *&perm) {
+//
+// Adaptive refinement: the estimate ignores early ray termination and the
+// volume's content, so the first render of a view also records every tile's
+// measured cost (per wave: its longest ray's samples + 2, record_tile_cost),
+// and the next render of the same view re-deals the blocks by those costs
+// (lists_from_costs).  VR_NO_ADAPT keeps the estimate order.
+
+// Interleave the 8 per-XCD lists into the workgroup order (entry b runs on
+// XCD b % 8) and upload it as g.perm.
+int upload_perm(const std::vector<std::vector<uint32_t>> &lists) {
+    std::vector<uint32_t> &h = g.perm_host;
+    h.clear();
+    size_t longest = 0;
+    for (auto &l : lists) longest = std::max(longest, l.size());
+    for (size_t i = 0; i < longest; i++)
+        for (auto &l : lists)
+            if (i < l.size()) h.push_back(l[i]);
+    if (h.size() > g.perm_cap) {  // grow; otherwise rewrite in stream order
+        if (g.perm) (void)hipFree(g.perm);
+        g.perm = nullptr;
+        g.perm_cap = 0;
+        VR_HIP(hipMalloc(&g.perm, h.size() * sizeof(uint32_t)));
+        g.perm_cap = h.size();
+    }
+    VR_HIP(hipMemcpyAsync(g.perm, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          g.stream));
+    return VR_OK;
+}
+
+// Measured-cost deal: blocks sorted by total cost, each given to the least
+// loaded XCD that still has room (every XCD keeps the same number of blocks,
+// +-1, so the interleaved order keeps entry b on XCD b % 8); an XCD's blocks
+// stay in dealing order, i.e. most expensive first.
+void lists_from_costs(const std::vector<uint32_t> &cost, uint32_t tx, uint32_t ty, uint32_t bx,
+                      uint32_t by, std::vector<std::vector<uint32_t>> &lists) {
+    const uint32_t nbx = (tx + bx - 1) / bx, nby = (ty + by - 1) / by;
+    struct Blk { uint64_t cost; uint32_t i, j; };
+    std::vector<Blk> blk;
+    blk.reserve((size_t)nbx * nby);
+    for (uint32_t j = 0; j < nby; j++)
+        for (uint32_t i = 0; i < nbx; i++) {
+            uint64_t c = 0;
+            for (uint32_t y = j * by; y < std::min(ty, j * by + by); y++)
+                for (uint32_t x = i * bx; x < std::min(tx, i * bx + bx); x++)
+                    c += cost[(size_t)y * tx + x];
+            blk.push_back({c, i, j});
+        }
+    std::stable_sort(blk.begin(), blk.end(), [](const Blk &a, const Blk &b) { return a.cost > b.cost; });
+    // every XCD ends with lo or lo + 1 blocks, exactly `extra` of them with lo + 1
+    const size_t lo = blk.size() / 8, extra = blk.size() % 8;
+    size_t n_plus = 0;
+    uint64_t load[8] = {0};
+    size_t count[8] = {0};
+    lists.assign(8, {});
+    for (const Blk &b : blk) {
+        int best = -1;
+        for (int x8 = 0; x8 < 8; x8++) {
+            const bool room = count[x8] < lo || (count[x8] == lo && n_plus < extra);
+            if (room && (best < 0 || load[x8] < load[best])) best = x8;
+        }
+        n_plus += count[best] == lo;
+        load[best] += b.cost;
+        count[best]++;
+        for (uint32_t y = b.j * by; y < std::min(ty, b.j * by + by); y++)
+            for (uint32_t x = b.i * bx; x < std::min(tx, b.i * bx + bx); x++)
+                lists[best].push_back(y * tx + x);
+    }
+}
+
+int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_t *&perm,
+                uint32_t **record) {
     uint32_t bx = 1, by = 4;
     if (const char *e = std::getenv("VR_XBLOCK")) {
         char *end = nullptr;
@@ -187,11 +271,40 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
         bx = (uint32_t)std::min(a, 64L);
         by = (uint32_t)std::min(b, 64L);
     }
-    uint32_t key[18] = {d->width, d->height, bx, by};
+    // everything that changes the samples each ray takes keys the order
+    uint32_t key[22] = {d->width, d->height, bx, by};
     std::memcpy(key + 4, d->inv_view, sizeof d->inv_view);
     key[16] = std::getenv("VR_NO_LPT") ? 1u : 0u;
+    key[17] = (uint32_t)d->query_method;
+    std::memcpy(key + 18, &d->density, sizeof(float));
+    std::memcpy(key + 19, &d->transfer_offset, sizeof(float));
+    std::memcpy(key + 20, &d->transfer_scale, sizeof(float));
+    key[21] = g.volume_epoch;
+    const size_t ntile = (size_t)tx * ty;
     if (g.perm && std::memcmp(key, g.perm_key, sizeof key) == 0) {
         perm = g.perm;
+        if (g.order_state == 1 && record) {
+            if (!g.cost_recorded) {  // no frame of this view has recorded yet
+                VR_HIP(hipMemsetAsync(g.tile_cost, 0, ntile * sizeof(uint32_t), g.stream));
+                *record = g.tile_cost;
+                return VR_OK;
+            }
+            // the frame after the recording one: re-deal the tiles by the costs
+            std::vector<uint32_t> cost(ntile);
+            VR_HIP(hipMemcpyAsync(cost.data(), g.tile_cost, ntile * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, g.stream));
+            VR_HIP(hipStreamSynchronize(g.stream));
+            g.order_state = 2;
+            bool any = false;
+            for (uint32_t c : cost) any |= c != 0;
+            if (any) {  // kernels other than the per-ray pipelined march record nothing
+                std::vector<std::vector<uint32_t>> lists;
+                lists_from_costs(cost, tx, ty, bx, by, lists);
+                int rc = upload_perm(lists);
+                if (rc != VR_OK) return rc;
+                perm = g.perm;
+            }
+        }
         return VR_OK;
     }
     const uint32_t nbx = (tx + bx - 1) / bx, nby = (ty + by - 1) / by;
@@ -220,28 +333,31 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
                 for (uint32_t x = b.i * bx; x < std::min(tx, b.i * bx + bx); x++)
                     lists[x8].push_back(y * tx + x);
     }
-    std::vector<uint32_t> &h = g.perm_host;
-    h.clear();
-    size_t longest = 0;
-    for (auto &l : lists) longest = std::max(longest, l.size());
-    for (size_t i = 0; i < longest; i++)
-        for (auto &l : lists)
-            if (i < l.size()) h.push_back(l[i]);
-    if (h.size() > g.perm_cap) {  // grow; otherwise rewrite in stream order
-        if (g.perm) (void)hipFree(g.perm);
-        g.perm = nullptr;
-        g.perm_cap = 0;
-        VR_HIP(hipMalloc(&g.perm, h.size() * sizeof(uint32_t)));
-        g.perm_cap = h.size();
-    }
-    VR_HIP(hipMemcpyAsync(g.perm, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                          g.stream));
+    g.order_state = 0;  // until the new order is in place
+    int rc = upload_perm(lists);
+    if (rc != VR_OK) return rc;
     std::memcpy(g.perm_key, key, sizeof key);
     perm = g.perm;
+    g.order_state = (key[16] || std::getenv("VR_NO_ADAPT")) ? 2 : 1;
+    g.cost_recorded = false;
+    if (g.order_state == 1) {
+        if (ntile > g.tile_cost_cap) {
+            if (g.tile_cost) (void)hipFree(g.tile_cost);
+            g.tile_cost = nullptr;
+            g.tile_cost_cap = 0;
+            VR_HIP(hipMalloc(&g.tile_cost, ntile * sizeof(uint32_t)));
+            g.tile_cost_cap = ntile;
+        }
+        if (record) {
+            VR_HIP(hipMemsetAsync(g.tile_cost, 0, ntile * sizeof(uint32_t), g.stream));
+            *record = g.tile_cost;
+        }
+    }
     return VR_OK;
 }
 
-int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
+int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
+                bool for_render = false) {
     if (!d) return fail(VR_ERR_ARG, "null render descriptor");
     const bool codec = d->query_method >= 4 && d->query_method <= 6;
     if (codec && !g.cb)
@@ -296,8 +412,10 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
     P.tiles_x = tiles_x(d->width);
     P.tile_list = d->d_tile_list;
     P.perm = nullptr;
+    uint32_t *record = nullptr;
     if (!d->d_tile_list) {
-        int rc = frame_order(d, tiles_x(d->width), tiles_y(d->height), P.perm);
+        int rc = frame_order(d, tiles_x(d->width), tiles_y(d->height), P.perm,
+                             for_render ? &record : nullptr);
         if (rc != VR_OK) return rc;
     }
     P.out = d->d_output;
@@ -342,8 +460,11 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
         P.path = 7;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
-        if (v >= 0 && v <= 7) P.path = v;
+        if (v >= 0 && v <= 9) P.path = v;
     }
+    P.wave_clock = g.wave_clock;
+    P.tile_cost = record;
+    P.hyb_tiles = 0;
     P.seg_lanes = 4;
     if (const char *e = std::getenv("VR_SEG")) {
         const int v = std::atoi(e);
@@ -357,6 +478,14 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots) {
         nslots = (uint32_t)all;
     }
     P.n_tiles = nslots;
+    // VR_HYB=K: hybrid march (path 9), the first K slots ray-segmented
+    if (const char *e = std::getenv("VR_HYB")) {
+        const long k = std::atol(e);
+        if (k > 0) {
+            P.path = 9;
+            P.hyb_tiles = (int)std::min<uint64_t>((uint64_t)k & ~7ull, nslots & ~7u);
+        }
+    }
     return VR_OK;
 }
 
@@ -858,7 +987,7 @@ int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins) {
 int vr_render(const vr_render_desc *desc) {
     vr::Params P;
     uint32_t nslots = 0;
-    int rc = fill_params(desc, P, nslots);
+    int rc = fill_params(desc, P, nslots, true);
     if (rc != VR_OK) return rc;
     hipError_t e;
     if (is_flex_method(desc->query_method)) {
@@ -872,6 +1001,12 @@ int vr_render(const vr_render_desc *desc) {
         e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
     }
     if (e != hipSuccess) return hip_fail(e, "launch(k_march)");
+    if (P.tile_cost) g.cost_recorded = true;
+    return VR_OK;
+}
+
+int vr_debug_wave_clock(uint64_t *d_buf) {
+    g.wave_clock = reinterpret_cast<unsigned long long *>(d_buf);
     return VR_OK;
 }
 

@@ -50,9 +50,16 @@ struct Params {
     int ntpl, err_slots;
     int tpl_lds;                 // codec march: template table copied to LDS (bytes, 0 = no)
     int seg_lanes;               // ray-segmented march (path 7): lanes per ray
+    int hyb_tiles;               // hybrid march (path 9): leading slots ray-segmented
     // flexible blocks (methods 8/9/0): per-block (mean, variance, entropy, 0)
     const float4 *flex;
     int nflex;                   // blocks per axis
+    // tooling (vr_debug_wave_clock): per wave {start, end, hw id} of the
+    // per-ray pipelined march, nullptr = off
+    unsigned long long *wave_clock;
+    // adaptive tile order: per-tile cost record of the pipelined march
+    // (record_tile_cost), indexed by tile id, nullptr = off
+    uint32_t *tile_cost;
 };
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)

@@ -712,7 +712,16 @@ __global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vo
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
-    march_pipe_tile<B, M>(vol, P, slot, tile, threadIdx.x);
+    unsigned long long t0 = 0;
+    if (P.wave_clock) t0 = wall_clock64();
+    const int n = march_pipe_tile<B, M>(vol, P, slot, tile, threadIdx.x);
+    if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
+    if (P.wave_clock && (threadIdx.x & 63) == 0) {
+        unsigned long long *w = P.wave_clock + ((uint64_t)slot * 4u + threadIdx.x / 64u) * 3u;
+        w[0] = t0;
+        w[1] = wall_clock64();
+        w[2] = __smid();  // XCC id in the high bits on gfx94x/gfx950
+    }
 }
 
 // ---- neighbour-shared per-ray march (B % 4 == 0, row-aligned views) ----
@@ -1506,6 +1515,11 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         if (P.path == 7) {
             hipError_t err = hipSuccess;
             if (launch_march_seg(B, method, P.seg_lanes, vol, P, nslots, s, err)) return err;
+            P.path = 2;
+        }
+        if (P.path == 9) {
+            hipError_t err = hipSuccess;
+            if (launch_march_hyb(B, method, P.seg_lanes, vol, P, nslots, s, err)) return err;
             P.path = 2;
         }
         if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {

@@ -183,19 +183,19 @@ __device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][
 // the two register sets swap roles without copies.  t: thread index inside
 // the 256-thread tile; slot: the tile's launch slot (packed output position).
 template <int B, int M>
-__device__ __forceinline__ void march_pipe_tile(const float *__restrict__ vol, const Params &P,
-                                                uint32_t slot, uint32_t tile, uint32_t tid) {
+__device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, const Params &P,
+                                               uint32_t slot, uint32_t tile, uint32_t tid) {
     uint32_t lx, ly;
     tile_pixel(tid, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;  // no cross-lane work in this kernel
+    if (x >= P.W || y >= P.H) return -1;  // no cross-lane work in this kernel
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
     if (!make_ray(P, x, y, r)) {
         write_miss(P, o);
-        return;
+        return -1;
     }
     float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
     float t = r.tnear;
@@ -235,6 +235,16 @@ __device__ __forceinline__ void march_pipe_tile(const float *__restrict__ vol, c
     }
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
                 sw * P.brightness);
+    return n;
+}
+
+// Cost record of the adaptive tile order (vr_api.cpp frame_order): every wave
+// adds (its longest ray's samples + 2) to its tile's entry, i.e. the wave's
+// step-chain length plus a fixed launch/ray-setup share.  n = this lane's
+// samples (-1: miss or outside the image); call with all 64 lanes converged.
+__device__ __forceinline__ void record_tile_cost(const Params &P, uint32_t tile, int n) {
+    const int mx = wave_max(n);
+    if ((threadIdx.x & 63u) == 0) atomicAdd(P.tile_cost + tile, (uint32_t)(mx + 2));
 }
 
 }  // namespace vr

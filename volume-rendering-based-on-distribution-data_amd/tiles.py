@@ -125,6 +125,91 @@ def tile_lists(width: int, height: int, world_size: int, inv_view=None) -> np.nd
     return out
 
 
+def tile_costs_from_steps(steps, tile_list, n_tiles_total: int) -> np.ndarray:
+    """Per-tile march cost from a render's per-pixel sample counts (d_steps).
+
+    steps: (n_slots*256,) int32 packed like the tile buffer (-1 = miss / no
+    ray), tile_list: the (n_slots,) uint32 list it was rendered with.  A tile's
+    cost is what its four waves spend: per 64-pixel row (one wave), the row's
+    longest ray's samples + 2 (the wave loops while any lane is live; +2 for
+    ray setup and the store) -- the measure the library's own adaptive
+    full-frame order records (record_tile_cost, vr_march.h).  Returns a
+    (n_tiles_total,) int64 vector, zero for tiles not in the list, so ranks can
+    sum their vectors into the whole frame's."""
+    tl = np.asarray(tile_list, dtype=np.uint32)
+    s = np.asarray(steps, dtype=np.int64).reshape(len(tl), TILE_H, TILE_W)
+    row = s.max(axis=2) + 2                       # (n_slots, 4)
+    cost = np.zeros(n_tiles_total, dtype=np.int64)
+    ok = tl != PAD
+    cost[tl[ok].astype(np.int64)] = row[ok].sum(axis=1)
+    return cost
+
+
+def tile_costs_from_frame(steps, width: int, height: int) -> np.ndarray:
+    """tile_costs_from_steps for a full-frame render's (height, width) step map"""
+    tx, ty = tiles_x(width), tiles_y(height)
+    s = np.full((ty * TILE_H, tx * TILE_W), -1, dtype=np.int64)
+    s[:height, :width] = np.asarray(steps, dtype=np.int64).reshape(height, width)
+    packed = s.reshape(ty, TILE_H, tx, TILE_W).transpose(0, 2, 1, 3).reshape(-1)
+    return tile_costs_from_steps(packed, np.arange(tx * ty, dtype=np.uint32), tx * ty)
+
+
+def tile_lists_by_cost(width: int, height: int, world_size: int, cost) -> np.ndarray:
+    """Like tile_lists, but dealt by measured per-tile costs (tile_costs_from_steps
+    summed over the ranks of a previous frame of the same view).
+
+    Blocks (1x4 tiles, as in tile_lists) are taken most expensive first and each
+    goes to the least loaded (rank, XCD) bin that still has room; every bin
+    ends with the same number of blocks (+-1), so ranks get equal pixel counts
+    (equal-size gathers) and work is balanced over all 8*world XCDs, not only
+    over ranks.  A bin's blocks stay in dealing order, i.e. longest first.
+    Each rank's 8 XCD sublists are PAD-padded to one length before they are
+    interleaved, so list entry 8*k + g is always the k-th tile of XCD g."""
+    tx, ty = tiles_x(width), tiles_y(height)
+    cost = np.asarray(cost, dtype=np.int64).reshape(ty, tx)
+    nbx, nby = (tx + BLOCK_X - 1) // BLOCK_X, (ty + BLOCK_Y - 1) // BLOCK_Y
+    pad = np.zeros((nby * BLOCK_Y, nbx * BLOCK_X), dtype=np.int64)
+    pad[:ty, :tx] = cost
+    bcost = pad.reshape(nby, BLOCK_Y, nbx, BLOCK_X).sum(axis=(1, 3)).reshape(-1)
+    nbins = XCDS * world_size
+    # every bin ends with lo or lo + 1 blocks, exactly `extra` of them with lo + 1
+    lo, extra = divmod(len(bcost), nbins)
+    order = np.argsort(-bcost, kind="stable")
+    load = np.zeros(nbins, dtype=np.int64)
+    count = np.zeros(nbins, dtype=np.int64)
+    members = [[] for _ in range(nbins)]
+    big = np.iinfo(np.int64).max
+    n_plus = 0
+    for b in order:
+        room = (count < lo) | ((count == lo) & (n_plus < extra))
+        best = int(np.argmin(np.where(room, load, big)))
+        n_plus += int(count[best] == lo)
+        load[best] += bcost[b]
+        count[best] += 1
+        members[best].append(int(b))
+    ids = []
+    for r in range(world_size):
+        lists = []
+        for g in range(XCDS):
+            lst = []
+            for b in members[g * world_size + r]:
+                by, bx = divmod(b, nbx)
+                for y in range(by * BLOCK_Y, min(ty, by * BLOCK_Y + BLOCK_Y)):
+                    for x in range(bx * BLOCK_X, min(tx, bx * BLOCK_X + BLOCK_X)):
+                        lst.append(y * tx + x)
+            lists.append(lst)
+        longest = max(len(l) for l in lists)
+        inter = np.full((longest, XCDS), PAD, dtype=np.uint32)
+        for g, l in enumerate(lists):
+            inter[:len(l), g] = l
+        ids.append(inter.reshape(-1))
+    n_slots = max(len(i) for i in ids)
+    out = np.full((world_size, n_slots), PAD, dtype=np.uint32)
+    for r, i in enumerate(ids):
+        out[r, :len(i)] = i
+    return out
+
+
 def gather_packed(packed, world_size: int, rank: int, group=None):
     """Gather every rank's packed tile buffer to rank 0.
 
