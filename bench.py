@@ -230,6 +230,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
+    t_enq = time.perf_counter()  # host time to issue the K steps (host-bound if ~ t1 - t0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -280,6 +281,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(1e3 / ms_per_step, 2),
+            "host_issue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

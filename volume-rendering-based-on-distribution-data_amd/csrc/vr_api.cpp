@@ -448,12 +448,13 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // 7 ray-segmented (VR_SEG lanes per ray).
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
-    // Launches of few rays (a rank's tile list at 4+ GPUs) are bound by the
-    // per-ray step chain, not by HBM: there the ray-segmented march (4 lanes
-    // per ray, path 7) renders mean / variance row-aligned views ~1.4x faster
-    // than the one-lane march (tools/rank_sim.py).
-    // VR_SEG_RAYS overrides the ray-count threshold.
-    uint64_t seg_rays = 600000;
+    // Launches of few rays (a rank's tile list at 8 GPUs, 1080p) are bound by
+    // the per-ray step chain, not by HBM: there the ray-segmented march (4
+    // lanes per ray, path 7) renders mean / variance row-aligned views ~1.3x
+    // faster than the one-lane march; with cost-dealt lists the one-lane march
+    // still wins at 4 GPUs (~524 K rays per rank) (tools/rank_sim.py, DESIGN.md
+    // section 7).  VR_SEG_RAYS overrides the ray-count threshold.
+    uint64_t seg_rays = 400000;
     if (const char *e = std::getenv("VR_SEG_RAYS")) seg_rays = std::strtoull(e, nullptr, 10);
     if (along_rows && d->d_tile_list && (d->query_method == 1 || d->query_method == 2) &&
         (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= seg_rays)
