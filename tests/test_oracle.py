@@ -263,3 +263,24 @@ def test_codec_render_matches_numpy(orc, cams, method, cam):
     assert np.array_equal(n, on)
     assert np.array_equal(f, of)
     assert np.array_equal(np.where(n >= 0, R.pack(f), 0), o8)
+
+
+def _sig_bits(x: float) -> int:
+    import math
+    if x == 0:
+        return 0
+    m, _ = math.frexp(abs(x))
+    n = int(m * 2 ** 53)
+    return 53 - ((n & -n).bit_length() - 1)
+
+
+@pytest.mark.parametrize("nb", [1, 2, 3, 4, 5, 8, 16])
+def test_bin_centres_fit_29_bits(nb):
+    """the HIP mean decode uses fma(p, c_i, mean) for B <= 16 (vr_device.h raw_mean):
+    exact only if every bin centre c_i = (double)(bw*i) + bw/2.0 (K:742-747) has
+    <= 29 significant bits, so the double product with a 24-bit float is exact"""
+    bw = np.float32(np.float32(0.0217) - np.float32(0.0)) / np.float32(nb)
+    half = float(bw) / 2.0
+    for i in range(nb):
+        c = float(np.float32(bw * np.float32(i))) + half
+        assert _sig_bits(c) <= 29, (nb, i, c)

@@ -144,12 +144,36 @@ __device__ __forceinline__ float bin_width(int nb) {
     return (maxh - 0.0f) / (float)nb;
 }
 
-// K:742-747: mean += p * (binWidth * i + binWidth / 2.0), float accumulator
+// K:742-747: mean += p * (binWidth * i + binWidth / 2.0), float accumulator.
+// The bin centre c_i = (double)(bw * i) + bw / 2.0 is a sum of two floats a
+// few binades apart, so it has at most 29 significant bits for B <= 16
+// (tests/test_oracle.py::test_bin_centres_fit_29_bits); the double product
+// (double)p * c_i of a 24-bit float is then exact, and
+// (double)mean + p * c_i rounded once is exactly fma(p, c_i, mean): one f64
+// op per bin fewer, bit-identical.  B = 32 centres reach 30 bits: mul + add.
 template <int B>
 __device__ __forceinline__ float raw_mean(const float (&p)[B]) {
     const float bw = bin_width(B);
     const double half = (double)bw / 2.0;
     float mean = 0.0f;
+#ifndef VR_NO_FMA_MEAN  // A/B builds only
+    if constexpr (B <= 16) {
+#else
+    if constexpr (false) {
+#endif
+#pragma unroll
+        for (int i = 0; i < B; i++) {
+            const double c = (double)(bw * (float)i) + half;
+            mean = (float)__builtin_fma((double)p[i], c, (double)mean);
+        }
+        return mean;
+    }
+#if defined(VR_ABL) && (VR_ABL & 1)
+    // timing ablation only (tools/build_variants.sh): f32 decode, NOT the reference's
+#pragma unroll
+    for (int i = 0; i < B; i++) mean = mean + p[i] * (float)((double)(bw * (float)i) + half);
+    return mean;
+#endif
 #pragma unroll
     for (int i = 0; i < B; i++) {
         const double c = (double)(bw * (float)i) + half;
@@ -235,6 +259,9 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
 template <int B, int M>
 __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
     if constexpr (M == 1) {
+#if defined(VR_ABL) && (VR_ABL & 2)
+        return raw_mean<B>(p) * (float)kMeanR;  // timing ablation only
+#endif
         return (float)div_const((double)raw_mean<B>(p), kMeanD, kMeanR);
     } else if constexpr (M == 2) {
         const float mean = raw_mean<B>(p);
