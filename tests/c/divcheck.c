@@ -10,7 +10,8 @@
  * R = 1/D rounded to nearest (Markstein's correction step), returning q0 itself
  * when it is +-0 or +-inf.  This program
  * checks every one of the 2^32 float inputs for each divisor and prints the
- * number of mismatches (0 expected), comparing the float result for the first
+ * number of mismatches (0 expected) -- and the same for the float-only
+ * variance division div_var_f32 and the multiply-only div_to_float below -- comparing the float result for the first
  * two and the full double result for the third.
  *
  *   gcc -O2 -fopenmp -ffp-contract=off divcheck.c -lm && ./a.out
@@ -29,6 +30,19 @@ static inline double fast_div(double m, double D, double R) {
     if (q0 == 0.0 || isinf(q0)) return q0;  /* +-0, +-inf: keep the sign / infinity */
     const double e = fma(-q0, D, m);
     return fma(e, R, q0);
+}
+
+/* float-only division by 0.000021 (vr_device.h div_var_f32): one FMA against
+ * the reciprocal split in two floats, for |m| in [2^-100, FLT_MAX]; zeros and
+ * infinities return m * Ch; NaN propagates; the remaining tiny inputs (whose
+ * quotients are subnormal) take the double path */
+static inline float div_var_f32(float m) {
+    const double R = 1.0 / 0.000021;
+    const float Ch = (float)R, Cl = (float)(R - (double)Ch);
+    const float am = fabsf(m);
+    if (am >= 0x1p-100f && am <= 0x1.fffffep127f) return fmaf(m, Ch, m * Cl);
+    if (m == 0.0f || !(am <= 0x1.fffffep127f)) return m * Ch;
+    return (float)fast_div((double)m, 0.000021, R);
 }
 
 int main(void) {
@@ -51,6 +65,31 @@ int main(void) {
             }
         }
         printf("%-28s mismatches: %lld\n", names[k], bad);
+        total_bad += bad;
+    }
+    {
+        long long bad = 0;
+#pragma omp parallel for reduction(+ : bad) schedule(static)
+        for (int64_t i = 0; i <= 0xFFFFFFFFll; i++) {
+            const float m = bits_f((uint32_t)i);
+            const float a = (float)((double)m / 0.000021), b = div_var_f32(m);
+            if (f_bits(a) != f_bits(b) && !(isnan(a) && isnan(b))) bad++;
+        }
+        printf("%-28s mismatches: %lld\n", "0.000021 float-only (var)", bad);
+        total_bad += bad;
+    }
+    /* rounded to float, the reciprocal multiply alone suffices (vr_device.h
+     * div_to_float): (float)((double)m * (1/D)) == (float)((double)m / D) */
+    for (int k = 0; k < 2; k++) {
+        const double D = Ds[k], R = 1.0 / D;
+        long long bad = 0;
+#pragma omp parallel for reduction(+ : bad) schedule(static)
+        for (int64_t i = 0; i <= 0xFFFFFFFFll; i++) {
+            const float m = bits_f((uint32_t)i);
+            const float a = (float)((double)m / D), b = (float)((double)m * R);
+            if (f_bits(a) != f_bits(b) && !(isnan(a) && isnan(b))) bad++;
+        }
+        printf("%-28s mismatches: %lld\n", k ? "0.000021 multiply-only" : "0.0217 multiply-only", bad);
         total_bad += bad;
     }
     return total_bad != 0;

@@ -138,6 +138,31 @@ constexpr double kMeanD = 0.0217, kMeanR = 1.0 / 0.0217;          // K:758
 constexpr double kVarD = 0.000021, kVarR = 1.0 / 0.000021;        // K:759
 constexpr double kLn2R = 1.0 / VR_LN2_D;                          // K:766
 
+// (float)((double)m / D) for a float m when only the float rounding is kept:
+// the reciprocal multiply (float)((double)m * (1/D)) is bit-identical for
+// every one of the 2^32 float inputs for D = 0.0217 and 0.000021
+// (tests/c/divcheck.c) -- no Markstein correction, no 0 / inf selects.
+// (The mean keeps div_const: equally exact, and the per-ray march it sits in
+// measured 1.45 ms with it against 1.97 ms with the shorter form, whose
+// different register allocation serialised the next step's gathers.)
+__device__ __forceinline__ float div_to_float(float m, double R) {
+    return (float)((double)m * R);
+}
+
+// (float)((double)v / 0.000021) (K:759) without f64 in the common case: one
+// FMA against the reciprocal split in two floats for |v| in [2^-100, FLT_MAX];
+// zeros and infinities give v * Ch, NaN propagates, and the tiny inputs with
+// subnormal quotients take div_to_float.  Bit-identical for every one of the 2^32
+// float inputs (tests/c/divcheck.c, div_var_f32).
+__device__ __forceinline__ float div_var_f32(float v) {
+    constexpr float Ch = (float)kVarR;
+    constexpr float Cl = (float)(kVarR - (double)Ch);
+    const float av = __builtin_fabsf(v);
+    if (av >= 0x1p-100f && av <= 0x1.fffffep127f) return __builtin_fmaf(v, Ch, v * Cl);
+    if (v == 0.0f || !(av <= 0x1.fffffep127f)) return v * Ch;
+    return div_to_float(v, kVarR);
+}
+
 // binWidth, K:736-738
 __device__ __forceinline__ float bin_width(int nb) {
     const float maxh = (float)0.0217;
@@ -168,12 +193,6 @@ __device__ __forceinline__ float raw_mean(const float (&p)[B]) {
         }
         return mean;
     }
-#if defined(VR_ABL) && (VR_ABL & 1)
-    // timing ablation only (tools/build_variants.sh): f32 decode, NOT the reference's
-#pragma unroll
-    for (int i = 0; i < B; i++) mean = mean + p[i] * (float)((double)(bw * (float)i) + half);
-    return mean;
-#endif
 #pragma unroll
     for (int i = 0; i < B; i++) {
         const double c = (double)(bw * (float)i) + half;
@@ -259,13 +278,10 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
 template <int B, int M>
 __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
     if constexpr (M == 1) {
-#if defined(VR_ABL) && (VR_ABL & 2)
-        return raw_mean<B>(p) * (float)kMeanR;  // timing ablation only
-#endif
         return (float)div_const((double)raw_mean<B>(p), kMeanD, kMeanR);
     } else if constexpr (M == 2) {
         const float mean = raw_mean<B>(p);
-        return (float)div_const((double)raw_variance<B>(p, mean), kVarD, kVarR);
+        return div_var_f32(raw_variance<B>(p, mean));
     } else {
         return entropy<B>(p, enorm);
     }
@@ -345,7 +361,7 @@ __device__ __forceinline__ float codec_stat_of(const float (&dec)[B], float enor
             const double d = ((double)(bw * (float)i) + half) - (double)mean;
             var = (float)((double)var + (double)dec[i] * d * d);
         }
-        return (float)div_const((double)var, kVarD, kVarR);
+        return div_var_f32(var);
     } else {
         return entropy<B>(dec, enorm);
     }
@@ -383,7 +399,7 @@ __device__ __forceinline__ float record_stat_rt(const float *__restrict__ p, int
             const float d = ((float)i / (float)nb) * maxh - mean;
             var = var + p[i] * d * d;
         }
-        return (float)div_const((double)var, kVarD, kVarR);
+        return div_var_f32(var);
     } else {
         float ent = 0.0f;
         for (int i = 0; i < nb; i++) {

@@ -707,8 +707,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
 }
 
 // ---- software-pipelined march (B <= 8) ----
+#ifndef VR_PIPE_WAVES
+#define VR_PIPE_WAVES 1     // minimum waves per SIMD the register allocation must allow
+#endif
 template <int B, int M>
-__global__ __launch_bounds__(256) void k_march_pipe(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_PIPE_WAVES, 8))) void k_march_pipe(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
