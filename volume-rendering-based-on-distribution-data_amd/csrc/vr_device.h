@@ -142,9 +142,6 @@ constexpr double kLn2R = 1.0 / VR_LN2_D;                          // K:766
 // the reciprocal multiply (float)((double)m * (1/D)) is bit-identical for
 // every one of the 2^32 float inputs for D = 0.0217 and 0.000021
 // (tests/c/divcheck.c) -- no Markstein correction, no 0 / inf selects.
-// (The mean keeps div_const: equally exact, and the per-ray march it sits in
-// measured 1.45 ms with it against 1.97 ms with the shorter form, whose
-// different register allocation serialised the next step's gathers.)
 __device__ __forceinline__ float div_to_float(float m, double R) {
     return (float)((double)m * R);
 }
@@ -278,7 +275,7 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
 template <int B, int M>
 __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
     if constexpr (M == 1) {
-        return (float)div_const((double)raw_mean<B>(p), kMeanD, kMeanR);
+        return div_to_float(raw_mean<B>(p), kMeanR);
     } else if constexpr (M == 2) {
         const float mean = raw_mean<B>(p);
         return div_var_f32(raw_variance<B>(p, mean));

@@ -178,8 +178,8 @@ __device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][
 // Same arithmetic as k_march's direct path, but the 8 corner records of step
 // i+1 are gathered into a second register set BEFORE step i is decoded, so
 // every wave always has a step's gathers in flight while its f64 decode runs.
-// The prefetch assumes the ray continues; a ray that terminates early
-// (sum.w > 0.95) wastes one step of gathers.  The loop is unrolled by two so
+// The prefetch assumes the ray continues; a ray that terminates (early, or at
+// tfar) wastes one step of gathers.  The loop is unrolled by two so
 // the two register sets swap roles without copies.  t: thread index inside
 // the 256-thread tile; slot: the tile's launch slot (packed output position).
 template <int B, int M>
@@ -212,15 +212,13 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
         const float tn = t + kTStep;                               // K:701
         const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, K:381
         const float nx = px + stx, ny = py + sty, nz = pz + stz;   // K:706
-        // Variance (M = 2) gathers unconditionally: the footprint's indices are
-        // clamped, so a ray past tfar just reads one valid step it discards,
-        // and without the divergent branch the compiler keeps the march at
-        // <= 168 VGPRs (3 waves/SIMD): 1.25 -> 1.13 ms at 1024^3 x 8, C0.  For
-        // the mean the branchy form schedules better (1.45 vs 1.55 ms).
-        if (M == 2 || cont) {
-            fn = footprint(P, nx, ny, nz);
-            gather8<B>(vol, P, fn, rn);
-        }
+        // The next step is gathered unconditionally: the footprint's indices
+        // are clamped, so a ray past tfar reads one valid step it discards
+        // (early-terminated rays already did).  Without the divergent branch
+        // the loads need no copies at the join and the compiler keeps the
+        // march small (B = 8: 107 VGPRs for the mean, 168 for the variance).
+        fn = footprint(P, nx, ny, nz);
+        gather8<B>(vol, P, fn, rn);
         const float sample = decode8<B, M>(P, rc, fc);
         n = i + 1;
         if (composite(P, sample, sx, sy, sz, sw) || !cont) {
