@@ -214,9 +214,12 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
         const float nx = px + stx, ny = py + sty, nz = pz + stz;   // K:706
         // The next step is gathered unconditionally: the footprint's indices
         // are clamped, so a ray past tfar reads one valid step it discards
-        // (early-terminated rays already did).  Without the divergent branch
-        // the loads need no copies at the join and the compiler keeps the
-        // march small (B = 8: 107 VGPRs for the mean, 168 for the variance).
+        // (early-terminated rays already did).  Without a divergent branch
+        // around the loads they need no copies at the join and the compiler
+        // keeps the march small (B = 8: 107 VGPRs for the mean, 168 for the
+        // variance) with all 16 in flight.  (Re-gathering the current
+        // footprint instead -- cache hits -- measured 2.4 ms against 1.36:
+        // the select changed the schedule again.)
         fn = footprint(P, nx, ny, nz);
         gather8<B>(vol, P, fn, rn);
         const float sample = decode8<B, M>(P, rc, fc);
