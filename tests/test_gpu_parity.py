@@ -301,7 +301,7 @@ def test_errors_do_not_exit(pkg, gpu):
     ("0", {}), ("1", {}), ("2", {}), ("3", {}), ("4", {}), ("5", {}), ("6", {}),
     ("1", {"VR_BOX_MAX": "0"}), ("1", {"VR_BOX_MAX": "64"}), ("0", {"VR_WG_PER_CU": "1"}),
     ("7", {"VR_SEG": "2"}), ("7", {"VR_SEG": "4"}), ("7", {"VR_SEG": "8"}), ("7", {"VR_SEG": "-4"}),
-    ("7", {"VR_SEG": "1"}), ("9", {"VR_HYB": "8", "VR_SEG": "4"}),
+    ("7", {"VR_SEG": "-2"}), ("7", {"VR_SEG": "1"}), ("9", {"VR_HYB": "8", "VR_SEG": "4"}),
     ("9", {"VR_HYB": "16", "VR_SEG": "2"}), ("9", {"VR_HYB": "1000", "VR_SEG": "8"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
@@ -322,7 +322,7 @@ def test_every_kernel_path(pkg, orc, gpu, path, env, nb, monkeypatch):
             assert_parity(got, ref, f"path {path} {env} nb={nb} m{method}")
 
 
-@pytest.mark.parametrize("seg", ["2", "4", "8"])
+@pytest.mark.parametrize("seg", ["2", "4", "8", "-2", "-4"])
 @pytest.mark.parametrize("nb", [1, 2, 8])
 def test_segmented_march_early_exit(pkg, orc, gpu, seg, nb, monkeypatch):
     """ray-segmented march (S lanes per ray): early exits inside a window, rays that end
@@ -356,7 +356,8 @@ def test_segmented_march_early_exit(pkg, orc, gpu, seg, nb, monkeypatch):
     for r in range(world):
         pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
                                  n_tiles=n_slots))
-    assert pkg.last_kernel().startswith(f"k_march_seg{seg}")
+    name = f"k_march_segp{seg[1:]}" if seg.startswith("-") else f"k_march_seg{seg}"
+    assert pkg.last_kernel().startswith(name)
     frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
     torch.cuda.synchronize()

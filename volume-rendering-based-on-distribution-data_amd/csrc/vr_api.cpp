@@ -448,13 +448,16 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // 7 ray-segmented (VR_SEG lanes per ray).
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
-    // Launches of few rays (a rank's tile list at 8 GPUs, 1080p) are bound by
-    // the per-ray step chain, not by HBM: there the ray-segmented march (4
-    // lanes per ray, path 7) renders mean / variance row-aligned views ~1.3x
-    // faster than the one-lane march; with cost-dealt lists the one-lane march
-    // still wins at 4 GPUs (~524 K rays per rank) (tools/rank_sim.py, DESIGN.md
-    // section 7).  VR_SEG_RAYS overrides the ray-count threshold.
-    uint64_t seg_rays = 400000;
+    // Launches of few rays (a rank's tile list at 4 or 8 GPUs, 1080p) are bound
+    // by the per-ray step chain, not by HBM: there the pipelined ray-segmented
+    // march (2 lanes per ray, next window gathered before this one decodes,
+    // path 7) renders mean / variance row-aligned views faster than the
+    // one-lane march (cost-dealt 1024^3x8 C0 lists, max over ranks: N = 8
+    // 0.217 ms vs 0.265 for plain 4-lane windows, N = 4 0.410 vs 0.44 one-lane);
+    // at 2 GPUs (~1.04 M rays per rank) the one-lane march still wins (0.70 vs
+    // 0.81 ms) (tools/rank_sim.py, tools/gpu_seg4.sh).
+    // VR_SEG_RAYS overrides the ray-count threshold.
+    uint64_t seg_rays = 700000;
     if (const char *e = std::getenv("VR_SEG_RAYS")) seg_rays = std::strtoull(e, nullptr, 10);
     if (along_rows && d->d_tile_list && (d->query_method == 1 || d->query_method == 2) &&
         (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= seg_rays)
@@ -466,7 +469,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     P.wave_clock = g.wave_clock;
     P.tile_cost = record;
     P.hyb_tiles = 0;
-    P.seg_lanes = 4;
+    P.seg_lanes = -2;  // VR_SEG=S: S lanes per ray, negative = pipelined windows
     if (const char *e = std::getenv("VR_SEG")) {
         const int v = std::atoi(e);
         if (v != 0 && v >= -8 && v <= 8 && (abs(v) & (abs(v) - 1)) == 0) P.seg_lanes = v;
