@@ -1064,8 +1064,11 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
     return qc_blend<G>(fc, s0, s1);
 }
 
+#ifndef VR_QUAD_WAVES
+#define VR_QUAD_WAVES 1  // minimum waves per SIMD the register allocation must allow
+#endif
 template <int M>
-__global__ __launch_bounds__(256) void k_march_quad(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAVES, 8))) void k_march_quad(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // uniform per workgroup
@@ -1534,10 +1537,15 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         }
         if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {
             note_kernel("k_march_quad", B, method);
+            // The quad march uses no LDS; an LDS request caps it at 2 workgroups
+            // (2 waves per SIMD) per CU, which trims the oblique view's line
+            // re-reads: 1024^3x8 C1 3.73 -> 3.52 ms (3 per CU by registers, 1 per
+            // CU 3.91).  VR_WG_PER_CU overrides.
+            const size_t qlds = (size_t)(160 * 1024 / (P.wg_per_cu > 0 ? P.wg_per_cu : 2)) & ~(size_t)255;
             switch (method) {
-            case 1: hipLaunchKernelGGL((k_march_quad<1>), grid, block, 0, s, vol, P); break;
-            case 2: hipLaunchKernelGGL((k_march_quad<2>), grid, block, 0, s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_quad<3>), grid, block, 0, s, vol, P); break;
+            case 1: hipLaunchKernelGGL((k_march_quad<1>), grid, block, qlds, s, vol, P); break;
+            case 2: hipLaunchKernelGGL((k_march_quad<2>), grid, block, qlds, s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_quad<3>), grid, block, qlds, s, vol, P); break;
             }
             return hipGetLastError();
         }
