@@ -1591,9 +1591,9 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         if (P.path == 2 && method >= 1 && method <= 3) {
             note_kernel("k_march_pipe", B, method);
             switch (method) {
-            case 1: hipLaunchKernelGGL((k_march_pipe<B, 1>), grid, block, 0, s, vol, P); break;
-            case 2: hipLaunchKernelGGL((k_march_pipe<B, 2>), grid, block, 0, s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3>), grid, block, 0, s, vol, P); break;
+            case 1: hipLaunchKernelGGL((k_march_pipe<B, 1>), grid, block, occupancy_lds(P), s, vol, P); break;
+            case 2: hipLaunchKernelGGL((k_march_pipe<B, 2>), grid, block, occupancy_lds(P), s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3>), grid, block, occupancy_lds(P), s, vol, P); break;
             }
             return hipGetLastError();
         }
@@ -1605,7 +1605,14 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     case 3: hipLaunchKernelGGL((k_march<B, 3, COUNT>), grid, block, lds, s, vol, P); break;
     case 7:
         if (COUNT) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_march_m7<B>), grid, block, 0, s, vol, P);
+        // oblique views (path 0) run method 7 at 3 workgroups per CU: fewer
+        // corner-mean refreshes in flight, fewer L2 re-reads (1024^3x8 C1
+        // 9.94 -> 8.29 ms; row-aligned C0 is fastest uncapped)
+        {
+            Params Q = P;
+            if (Q.wg_per_cu == 0 && Q.path == 0) Q.wg_per_cu = 3;
+            hipLaunchKernelGGL((k_march_m7<B>), grid, block, occupancy_lds(Q), s, vol, P);
+        }
         break;
     default: return hipErrorInvalidValue;
     }

@@ -253,4 +253,11 @@ __device__ __forceinline__ void record_tile_cost(const Params &P, uint32_t tile,
     if ((threadIdx.x & 63u) == 0) atomicAdd(P.tile_cost + tile, (uint32_t)(mx + 2));
 }
 
+// Dynamic LDS request that caps resident workgroups per CU at P.wg_per_cu
+// (VR_WG_PER_CU, 160 KiB of LDS per CU); 0 = no cap.  Host-side helper, only
+// for kernels without static LDS (static + dynamic must fit in 160 KiB).
+inline size_t occupancy_lds(const Params &P) {
+    return P.wg_per_cu > 0 ? (size_t)(160 * 1024 / P.wg_per_cu) & ~(size_t)255 : 0;
+}
+
 }  // namespace vr

@@ -259,9 +259,9 @@ static hipError_t seg_launch(int method, const float *vol, const Params &P, uint
                              hipStream_t s) {
     const dim3 grid(((nslots + 7u) / 8u) * 8u * S), block(256);
     switch (method) {
-    case 1: hipLaunchKernelGGL((k_march_seg<B, 1, S, PIPE>), grid, block, 0, s, vol, P); break;
-    case 2: hipLaunchKernelGGL((k_march_seg<B, 2, S, PIPE>), grid, block, 0, s, vol, P); break;
-    case 3: hipLaunchKernelGGL((k_march_seg<B, 3, S, PIPE>), grid, block, 0, s, vol, P); break;
+    case 1: hipLaunchKernelGGL((k_march_seg<B, 1, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P); break;
+    case 2: hipLaunchKernelGGL((k_march_seg<B, 2, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P); break;
+    case 3: hipLaunchKernelGGL((k_march_seg<B, 3, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
