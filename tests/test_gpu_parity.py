@@ -303,6 +303,9 @@ def test_errors_do_not_exit(pkg, gpu):
     ("7", {"VR_SEG": "2"}), ("7", {"VR_SEG": "4"}), ("7", {"VR_SEG": "8"}), ("7", {"VR_SEG": "-4"}),
     ("7", {"VR_SEG": "-2"}), ("7", {"VR_SEG": "1"}), ("9", {"VR_HYB": "8", "VR_SEG": "4"}),
     ("9", {"VR_HYB": "16", "VR_SEG": "2"}), ("9", {"VR_HYB": "1000", "VR_SEG": "8"}),
+    # occupancy caps (LDS requests) on the ray-segmented, LDS-box and pipelined launches
+    ("7", {"VR_SEG": "-2", "VR_WG_PER_CU": "3"}), ("1", {"VR_BOX_MAX": "64", "VR_WG_PER_CU": "3"}),
+    ("2", {"VR_WG_PER_CU": "2"}), ("0", {"VR_WG_PER_CU": "3"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, monkeypatch):
@@ -414,6 +417,23 @@ def test_codec_methods(pkg, orc, gpu, method, nb):
         ref = orc.render_codec(cb, t, e, orc.make_params(72, 56, cam, query_method=method))[:3]
         assert_parity(got, ref, f"codec nb={nb} m{method}")
     assert pkg.last_kernel().startswith("k_march_codec")
+
+
+@pytest.mark.parametrize("cap", ["1", "3"])
+def test_codec_occupancy_cap(pkg, orc, gpu, cap, monkeypatch):
+    """VR_WG_PER_CU reaches the codec march (its LDS request holds the template table at
+    the front): results stay bit-identical, with and without the staged table"""
+    import torch
+    monkeypatch.setenv("VR_WG_PER_CU", cap)
+    cb, t, e = orc.synth_codec(20, 16, 12, 8, seed=7)
+    pkg.init_codec(cb, t, e)
+    for lds in ("1", "0"):
+        monkeypatch.setenv("VR_CODEC_LDS", lds)
+        for method in (4, 5, 6):
+            cam = pkg.camera.display_inv_view((30.0, 45.0))
+            got = codec_render(pkg, 64, 48, cam, method, torch)
+            ref = orc.render_codec(cb, t, e, orc.make_params(64, 48, cam, query_method=method))[:3]
+            assert_parity(got, ref, f"codec cap {cap} lds {lds} m{method}")
 
 
 def test_codec_via_reference_initCuda(pkg, orc, gpu):

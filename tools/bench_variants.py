@@ -100,9 +100,14 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
+            bad = 0
             for _ in range(args.reps):
-                L.vr_render(ctypes.byref(d))
+                bad += L.vr_render(ctypes.byref(d)) != 0
             e1.record()
+            torch.cuda.synchronize()
+            # a launch failing only under some env setting must not be logged as fast
+            assert bad == 0, f"{name} {env}: {bad} failed renders: {L.vr_last_error()}"
+            assert L.vr_render(ctypes.byref(d)) == 0, L.vr_last_error()
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / args.reps)
         print(f"round {rnd} done", file=sys.stderr, flush=True)

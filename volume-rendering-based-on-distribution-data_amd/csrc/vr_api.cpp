@@ -356,6 +356,26 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
     return VR_OK;
 }
 
+// LDS bytes per CU and per workgroup of the current device (160 KiB each on
+// gfx950), read once per device; the occupancy caps are sized from them
+// (vr_march.h cap_lds).
+void device_lds(int &per_cu, int &per_wg) {
+    static int cached_dev = -1, cu = 160 * 1024, wg = 64 * 1024;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev != cached_dev) {
+        int a = 0, b = 0;
+        if (hipDeviceGetAttribute(&a, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) ==
+                hipSuccess && a > 0)
+            cu = a;
+        if (hipDeviceGetAttribute(&b, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) ==
+                hipSuccess && b > 0)
+            wg = b;
+        cached_dev = dev;
+    }
+    per_cu = cu;
+    per_wg = wg;
+}
+
 int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
                 bool for_render = false) {
     if (!d) return fail(VR_ERR_ARG, "null render descriptor");
@@ -448,6 +468,8 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // 7 ray-segmented (VR_SEG lanes per ray).
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
+    P.oblique = along_rows ? 0 : 1;
+    device_lds(P.lds_cu, P.lds_wg);
     // Launches of few rays (a rank's tile list at 4 or 8 GPUs, 1080p) are bound
     // by the per-ray step chain, not by HBM: there the pipelined ray-segmented
     // march (2 lanes per ray, next window gathered before this one decodes,

@@ -41,6 +41,8 @@ struct Params {
     unsigned long long *mark;    // footprint bitset (count mode only)
     int box_max;                 // LDS-staged footprint box capacity (voxels per wave), 0 = off
     int wg_per_cu;               // occupancy cap through the LDS request (0 = none)
+    int lds_cu, lds_wg;          // LDS bytes per CU / per workgroup (device attributes)
+    int oblique;                 // view's screen x does not run along voxel rows
     int path;                    // kernel variant (vr_api.cpp fill_params)
     // fractal/template codec (methods 4/5/6): codebook int4 per voxel, templates
     // [ntpl][nb], (bin, value) errors [voxel][err_slots]

@@ -1255,7 +1255,8 @@ template <int B, bool COUNT>
 static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream_t s) {
     const dim3 grid(nslots), block(256);
     if (!COUNT) note_kernel("k_march_codec", B, method);
-    const size_t lds = (size_t)P.tpl_lds;
+    // template table (if staged) at the front of the request; VR_WG_PER_CU caps
+    const size_t lds = cap_lds(P, P.wg_per_cu, (size_t)P.tpl_lds);
     switch (method) {
     case 4: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT>), grid, block, lds, s, nullptr, P); break;
     case 5: hipLaunchKernelGGL((k_march_codec<B, 1, COUNT>), grid, block, lds, s, nullptr, P); break;
@@ -1522,8 +1523,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     const dim3 grid(nslots), block(256);
     // one f32 box slice of box_max voxels per wave (4 waves); a larger request
     // caps the workgroups resident per CU (160 KiB of LDS per CU)
-    size_t lds = B > 0 ? (size_t)P.box_max * 4u * sizeof(float) : 0;
-    if (P.wg_per_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / P.wg_per_cu) & ~(size_t)255);
+    const size_t lds = cap_lds(P, P.wg_per_cu, B > 0 ? (size_t)P.box_max * 4u * sizeof(float) : 0);
     if constexpr (!COUNT && B > 0 && B <= 8) {
         if (P.path == 7) {
             hipError_t err = hipSuccess;
@@ -1541,7 +1541,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // (2 waves per SIMD) per CU, which trims the oblique view's line
             // re-reads: 1024^3x8 C1 3.73 -> 3.52 ms (3 per CU by registers, 1 per
             // CU 3.91).  VR_WG_PER_CU overrides.
-            const size_t qlds = (size_t)(160 * 1024 / (P.wg_per_cu > 0 ? P.wg_per_cu : 2)) & ~(size_t)255;
+            const size_t qlds = cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2);
             switch (method) {
             case 1: hipLaunchKernelGGL((k_march_quad<1>), grid, block, qlds, s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_quad<2>), grid, block, qlds, s, vol, P); break;
@@ -1605,14 +1605,14 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     case 3: hipLaunchKernelGGL((k_march<B, 3, COUNT>), grid, block, lds, s, vol, P); break;
     case 7:
         if (COUNT) return hipErrorInvalidValue;
-        // oblique views (path 0) run method 7 at 3 workgroups per CU: fewer
-        // corner-mean refreshes in flight, fewer L2 re-reads (1024^3x8 C1
-        // 9.94 -> 8.29 ms; row-aligned C0 is fastest uncapped)
-        {
-            Params Q = P;
-            if (Q.wg_per_cu == 0 && Q.path == 0) Q.wg_per_cu = 3;
-            hipLaunchKernelGGL((k_march_m7<B>), grid, block, occupancy_lds(Q), s, vol, P);
-        }
+        // oblique views run method 7 at 3 workgroups per CU when B = 8 (the
+        // measured case): fewer corner-mean refreshes in flight, fewer L2
+        // re-reads (1024^3x8 C1 9.94 -> 8.29 ms; row-aligned C0 is fastest
+        // uncapped).  Keyed on the view, not on P.path, which
+        // the B < 8 rewrite above has already changed.
+        hipLaunchKernelGGL((k_march_m7<B>), grid, block,
+                           cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : (P.oblique && B == 8 ? 3 : 0)),
+                           s, vol, P);
         break;
     default: return hipErrorInvalidValue;
     }

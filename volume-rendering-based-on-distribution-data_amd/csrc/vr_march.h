@@ -253,11 +253,20 @@ __device__ __forceinline__ void record_tile_cost(const Params &P, uint32_t tile,
     if ((threadIdx.x & 63u) == 0) atomicAdd(P.tile_cost + tile, (uint32_t)(mx + 2));
 }
 
-// Dynamic LDS request that caps resident workgroups per CU at P.wg_per_cu
-// (VR_WG_PER_CU, 160 KiB of LDS per CU); 0 = no cap.  Host-side helper, only
-// for kernels without static LDS (static + dynamic must fit in 160 KiB).
-inline size_t occupancy_lds(const Params &P) {
-    return P.wg_per_cu > 0 ? (size_t)(160 * 1024 / P.wg_per_cu) & ~(size_t)255 : 0;
+// Dynamic LDS request that caps resident workgroups per CU at `cap` (0 = no
+// cap) and is never below `need` (the kernel's own dynamic LDS, kept at the
+// front of the buffer).  P.lds_cu / P.lds_wg are the device's LDS per CU and
+// per workgroup (160 KiB each on gfx950, read once by vr_api.cpp); the request
+// is clamped to the per-workgroup limit minus the kernel's static LDS.
+// Host-side helper.
+inline size_t cap_lds(const Params &P, int cap, size_t need = 0, size_t static_lds = 0) {
+    size_t r = cap > 0 ? (size_t)(P.lds_cu / cap) & ~(size_t)255 : 0;
+    if (r < need) r = need;
+    const size_t room = (size_t)P.lds_wg > static_lds ? (size_t)P.lds_wg - static_lds : 0;
+    return r > room && need <= room ? room : r;
 }
+
+// The VR_WG_PER_CU cap (P.wg_per_cu) for kernels without static LDS.
+inline size_t occupancy_lds(const Params &P) { return cap_lds(P, P.wg_per_cu); }
 
 }  // namespace vr
