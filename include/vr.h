@@ -314,6 +314,59 @@ int vr_load_flex_files(const char *span_list_path, const char *fractal_path,
                        const char *simple_binfreq_path, const char *templates_path, int dim,
                        int nbins);
 
+/* ---- GMM distribution volumes (BASELINE config 5) ----
+ * An extension: the reference holds histograms only.  Each voxel is a K-component
+ * Gaussian mixture in two planes:
+ *   wm     (w_k, mu_k) float pairs, [voxel][K][2]  (8K bytes per voxel)
+ *   sigma  sigma_k floats,          [voxel][K]     (4K bytes per voxel)
+ * voxel order x + X*(y + Y*(z - z_base)) over the resident slices
+ * [z_base, z_base + nslices) of an X x Y x Z volume (dims).  K: 8, 16 or 32.
+ * The march is the reference's (K:282-717) with the per-step statistic decoded
+ * from the 8 corner mixtures: queryMethod 1 samples the mean sum w mu,
+ * queryMethod 2 samples 16 x the variance sum w (sigma^2 + mu^2) - mean^2
+ * (canonical evaluation order in vr_gmm.hip).  where: 0 host, 1 device (copied),
+ * 2 device (adopted, not freed).  A new GMM volume replaces the previous one. */
+int vr_init_gmm(const float *wm, const float *sigma, vr_extent dims, int ncomp, int z_base,
+                int nslices, int where);
+
+/* Generate slices [z_base, z_base + nslices) of the seeded synthetic GMM volume
+ * of DESIGN.md 11.1 (a dims-sized volume) directly in HBM. */
+int vr_synthesize_gmm(vr_extent dims, int ncomp, uint64_t seed, int z_base, int nslices);
+
+int vr_gmm_info(vr_extent *dims, int *ncomp, int *z_base, int *nslices, const float **d_wm,
+                const float **d_sigma);
+int vr_free_gmm(void);
+
+/* Slab of a slab-chained render (out-of-core and multi-GPU sort-last, DESIGN.md
+ * 11.2).  The launch takes the samples whose trilinear footprint starts in
+ * slices [z_lo, z_hi) (it reads slices z_lo .. min(z_hi, Z-1), which must be
+ * resident).  Rays come from the camera (d_rays_in == NULL: whole frame) or
+ * from the alive list of the previous slab (n_rays_in entries of 48 bytes:
+ * float sum[4], t, pos[3]; uint32 pixel, samples taken, 0, 0).  Rays that end in
+ * the slab are written to the frame (d_output etc., pixel y*width + x); rays that
+ * leave it alive are appended to d_rays_out (capacity: n_rays_in, or
+ * width*height) and counted in *d_n_rays_out (caller-zeroed, device memory).
+ * Slabs must be rendered in the order the view's rays cross them (every ray of
+ * the frame must step the same way in z, else VR_ERR_UNSUPPORTED); the chain
+ * then reproduces the whole-volume render bit for bit. */
+typedef struct {
+    int z_lo, z_hi;
+    const void *d_rays_in;
+    uint32_t n_rays_in;
+    void *d_rays_out;
+    uint32_t *d_n_rays_out;
+} vr_gmm_slab;
+
+/* Render the resident GMM volume: slab == NULL renders the whole frame (all
+ * slices must be resident); otherwise one slab of a chain.  desc: as for
+ * vr_render (d_tile_list must be NULL). */
+int vr_render_gmm(const vr_render_desc *desc, const vr_gmm_slab *slab);
+
+/* U for a whole-volume GMM render: distinct voxels in the union of the
+ * footprints of all samples taken (algorithmic bytes = U * 8K for the mean,
+ * U * 12K for the variance).  Synchronous. */
+int64_t vr_gmm_count_footprint(const vr_render_desc *desc);
+
 /* library version string */
 const char *vr_version(void);
 

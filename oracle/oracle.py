@@ -75,6 +75,15 @@ def lib():
         L.orc_render_flex.argtypes = [fp, ctypes.c_int, ctypes.POINTER(RenderParams), u32p, fp,
                                       i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.orc_render_flex.restype = ctypes.c_int64
+        L.orc_gmm_stat.argtypes = [fp, fp, ctypes.c_int, ctypes.c_int]
+        L.orc_gmm_stat.restype = ctypes.c_float
+        L.orc_synth_gmm.argtypes = [ctypes.c_int] * 4 + [ctypes.c_uint64, ctypes.c_int,
+                                                         ctypes.c_int, fp, fp, ctypes.c_int]
+        L.orc_render_gmm.argtypes = [ctypes.POINTER(Gmm), ctypes.POINTER(RenderParams),
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_uint32, ctypes.c_void_p, u32p, u32p, fp, i32p,
+                                     ctypes.c_void_p]
+        L.orc_render_gmm.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -397,3 +406,67 @@ def synth_flex(dim, block, nbins=64, ntemplates=40, seed=20261015, extra=50, dup
     return {"dim": dim, "block": block, "nbins": nbins, "fractal_low": fl, "fractal_high": fh,
             "fractal_code": code, "fractal_err": ferr, "simple_low": sl, "simple_high": sh,
             "simple_count": cnt, "simple_hist": shist, "templates": templates}
+
+
+# ---- GMM volumes (config 5) ----
+
+class Gmm(ctypes.Structure):
+    _fields_ = [("wm", ctypes.POINTER(ctypes.c_float)), ("sg", ctypes.POINTER(ctypes.c_float)),
+                ("nx", ctypes.c_int), ("ny", ctypes.c_int), ("nz", ctypes.c_int),
+                ("K", ctypes.c_int), ("z_base", ctypes.c_int), ("nzs", ctypes.c_int)]
+
+
+GMM_RAY_WORDS = 12  # 48-byte alive-list entry as uint32 words
+
+
+def synth_gmm(nx, ny, nz, K=16, seed=20261015, z_base=0, nslices=None, nthreads=0):
+    """slices [z_base, z_base + nslices) of the synthetic GMM volume:
+    (wm (nzs, ny, nx, K, 2), sigma (nzs, ny, nx, K)) float32"""
+    if nslices is None:
+        nslices = nz - z_base
+    wm = np.zeros((nslices, ny, nx, K, 2), np.float32)
+    sg = np.zeros((nslices, ny, nx, K), np.float32)
+    lib().orc_synth_gmm(nx, ny, nz, K, seed, z_base, nslices, _fp(wm), _fp(sg), nthreads)
+    return wm, sg
+
+
+def gmm_stat(wm_rec, sg_rec, method):
+    a = np.ascontiguousarray(wm_rec, dtype=np.float32).reshape(-1)
+    b = np.ascontiguousarray(sg_rec, dtype=np.float32).reshape(-1)
+    return float(lib().orc_gmm_stat(_fp(a), _fp(b), b.size, int(method)))
+
+
+def render_gmm(wm, sg, dims, params, z_base=0, slab=None, rays_in=None, want_mark=False):
+    """GMM render (whole volume when slab is None, else slab = (z_lo, z_hi)).
+    rays_in: (n, 12) uint32 alive-list entries or None (camera rays).
+    Returns dict: out (H, W) uint32, out_f (H, W, 4), out_n (H, W) int32 (-2 where
+    not written), rays_out (m, 12) uint32 or None, samples, U (with want_mark)."""
+    wm = np.ascontiguousarray(wm, dtype=np.float32)
+    sg = np.ascontiguousarray(sg, dtype=np.float32)
+    nx, ny, nz = (int(v) for v in dims)
+    g = Gmm(_fp(wm), _fp(sg), nx, ny, nz, int(sg.shape[-1]), int(z_base), int(sg.shape[0]))
+    W, H = params.width, params.height
+    out = np.zeros((H, W), np.uint32)
+    out_f = np.zeros((H, W, 4), np.float32)
+    out_n = np.full((H, W), -2, np.int32)
+    n_in = 0 if rays_in is None else int(rays_in.shape[0])
+    cap = n_in if rays_in is not None else W * H
+    rays_out = np.zeros((max(cap, 1), GMM_RAY_WORDS), np.uint32) if slab is not None else None
+    n_out = ctypes.c_uint32(0)
+    mark = None
+    if want_mark:
+        mark = np.zeros((nx * ny * nz + 63) // 64, np.uint64)
+    z_lo, z_hi = (0, nz) if slab is None else slab
+    rin = None if rays_in is None else np.ascontiguousarray(rays_in, dtype=np.uint32)
+    samples = lib().orc_render_gmm(
+        ctypes.byref(g), ctypes.byref(params), int(z_lo), int(z_hi),
+        None if rin is None else rin.ctypes.data, n_in,
+        None if rays_out is None else rays_out.ctypes.data, ctypes.byref(n_out),
+        out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _fp(out_f),
+        out_n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+        None if mark is None else mark.ctypes.data)
+    res = dict(out=out, out_f=out_f, out_n=out_n, samples=int(samples),
+               rays_out=None if rays_out is None else rays_out[:n_out.value].copy())
+    if mark is not None:
+        res["U"] = int(np.unpackbits(mark.view(np.uint8)).sum())
+    return res

@@ -895,3 +895,235 @@ int64_t orc_render_flex(const float *blocks, int nblk, const orc_render_params *
     run_rows(&v, p, out, out_f, out_n, row_start, row_stride, nthreads, &total);
     return total;
 }
+
+/* ------------------------------------------------------------------------ */
+/* GMM distribution volumes (config 5)                 */
+/* ------------------------------------------------------------------------ */
+
+/* T(p) over the L = K/4 lane partials, in the order k_march_gmm's DPP steps
+ * (quad_perm xor 1, xor 2, row_half_mirror) complete them:
+ * L = 2: p0 + p1;  L = 4: (p0 + p1) + (p2 + p3);
+ * L = 8: ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) */
+static inline float gmm_tree(const float *p, int L) {
+    if (L == 2) return p[0] + p[1];
+    const float a = (p[0] + p[1]) + (p[2] + p[3]);
+    if (L == 4) return a;
+    return a + ((p[4] + p[5]) + (p[6] + p[7]));
+}
+
+/* lane s of a ray's group holds components 4s .. 4s + 3 */
+float orc_gmm_stat(const float *wm, const float *sg, int K, int method) {
+    const int L = K / 4;
+    float pm[8] = {0}, pq[8] = {0};
+    for (int l = 0; l < L; l++) {
+        const int k0 = 4 * l;
+        pm[l] = wm[2 * k0] * wm[2 * k0 + 1];
+        for (int j = 1; j < 4; j++) pm[l] = fmaf(wm[2 * (k0 + j)], wm[2 * (k0 + j) + 1], pm[l]);
+    }
+    const float m = gmm_tree(pm, L);
+    if (method == 1) return m;
+    for (int l = 0; l < L; l++) {
+        const int k0 = 4 * l;
+        pq[l] = wm[2 * k0] * fmaf(sg[k0], sg[k0], wm[2 * k0 + 1] * wm[2 * k0 + 1]);
+        for (int j = 1; j < 4; j++) {
+            const int k = k0 + j;
+            pq[l] = fmaf(wm[2 * k], fmaf(sg[k], sg[k], wm[2 * k + 1] * wm[2 * k + 1]), pq[l]);
+        }
+    }
+    const float q = gmm_tree(pq, L);
+    const float mm = m * m;
+    return (q - mm) * 16.0f;
+}
+
+void orc_synth_gmm(int nx, int ny, int nz, int K, uint64_t seed, int z_base, int nzs, float *wm,
+                   float *sg, int nthreads) {
+    float amp[SYN_K];
+    float *gx = (float *)malloc(sizeof(float) * SYN_K * (size_t)nx);
+    float *gy = (float *)malloc(sizeof(float) * SYN_K * (size_t)ny);
+    float *gz = (float *)malloc(sizeof(float) * SYN_K * (size_t)nz);
+    for (int k = 0; k < SYN_K; k++) {
+        double r[5];
+        for (int j = 0; j < 5; j++) r[j] = u01(orc_splitmix64(seed + 0x100u + 8u * (uint64_t)k + (uint64_t)j));
+        amp[k] = (float)(0.3 + 0.7 * r[0]);
+        double s = 0.05 + 0.15 * r[4];
+        axis_table(nx, 0.2 + 0.6 * r[1], s, gx + (size_t)k * nx);
+        axis_table(ny, 0.2 + 0.6 * r[2], s, gy + (size_t)k * ny);
+        axis_table(nz, 0.2 + 0.6 * r[3], s, gz + (size_t)k * nz);
+    }
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int zl = 0; zl < nzs; zl++) {
+        const int z = zl + z_base;
+        for (int y = 0; y < ny; y++) {
+            for (int x = 0; x < nx; x++) {
+                float f = 0.0f;
+                for (int k = 0; k < SYN_K; k++)
+                    f = f + ((amp[k] * gx[(size_t)k * nx + x]) * gy[(size_t)k * ny + y]) *
+                                gz[(size_t)k * nz + z];
+                if (f > 1.0f) f = 1.0f;
+                const uint64_t v = ((uint64_t)z * (uint64_t)ny + (uint64_t)y) * (uint64_t)nx + (uint64_t)x;
+                const uint64_t lv = ((uint64_t)zl * (uint64_t)ny + (uint64_t)y) * (uint64_t)nx + (uint64_t)x;
+                float sum = 0.0f;
+                for (int k = 0; k < K; k++) {
+                    uint64_t h = orc_splitmix64(seed ^ 0x6A09E667F3BCC909ull ^ (v * (uint64_t)K + (uint64_t)k));
+                    sum = sum + (0.05f + (float)((h >> 16) & 0xFFFFFFull) * 0x1p-24f);
+                }
+                for (int k = 0; k < K; k++) {
+                    uint64_t h = orc_splitmix64(seed ^ 0x6A09E667F3BCC909ull ^ (v * (uint64_t)K + (uint64_t)k));
+                    const float u = (float)(h >> 40) * 0x1p-24f;
+                    const float r = 0.05f + (float)((h >> 16) & 0xFFFFFFull) * 0x1p-24f;
+                    float mu = (f * 0.8f + 0.1f) + (u - 0.5f) * 0.2f;
+                    mu = fminf(fmaxf(mu, 0.0f), 1.0f);
+                    wm[(lv * (uint64_t)K + (uint64_t)k) * 2] = r / sum;
+                    wm[(lv * (uint64_t)K + (uint64_t)k) * 2 + 1] = mu;
+                    sg[lv * (uint64_t)K + (uint64_t)k] = ((float)(h & 0xFFFFull) * 0x1p-16f) * 0.05f + 0.005f;
+                }
+            }
+        }
+    }
+    (void)nthreads;
+    free(gx);
+    free(gy);
+    free(gz);
+}
+
+/* eye ray + intersectBox (K:288-306), as render_pixel */
+static int gmm_ray(const orc_render_params *p, int x, int y, f3 *o, f3 *d, float *tnear,
+                   float *tfar) {
+    const float *M = p->inv_view;
+    float u = ((float)x / (float)p->width) * 2.0f - 1.0f;
+    float vv = ((float)y / (float)p->height) * 2.0f - 1.0f;
+    o->x = 0.0f * M[0] + 0.0f * M[1] + 0.0f * M[2] + 1.0f * M[3];
+    o->y = 0.0f * M[4] + 0.0f * M[5] + 0.0f * M[6] + 1.0f * M[7];
+    o->z = 0.0f * M[8] + 0.0f * M[9] + 0.0f * M[10] + 1.0f * M[11];
+    f3 d0 = {u, vv, -2.0f};
+    float inv = 1.0f / sqrtf(dot3(d0, d0));
+    d0.x = d0.x * inv; d0.y = d0.y * inv; d0.z = d0.z * inv;
+    d->x = d0.x * M[0] + d0.y * M[1] + d0.z * M[2];
+    d->y = d0.x * M[4] + d0.y * M[5] + d0.z * M[6];
+    d->z = d0.x * M[8] + d0.y * M[9] + d0.z * M[10];
+    f3 invR = {1.0f / d->x, 1.0f / d->y, 1.0f / d->z};
+    f3 tbot = {invR.x * (-1.0f - o->x), invR.y * (-1.0f - o->y), invR.z * (-1.0f - o->z)};
+    f3 ttop = {invR.x * (1.0f - o->x), invR.y * (1.0f - o->y), invR.z * (1.0f - o->z)};
+    f3 tmin = {fminf(ttop.x, tbot.x), fminf(ttop.y, tbot.y), fminf(ttop.z, tbot.z)};
+    f3 tmax = {fmaxf(ttop.x, tbot.x), fmaxf(ttop.y, tbot.y), fmaxf(ttop.z, tbot.z)};
+    *tnear = fmaxf(fmaxf(tmin.x, tmin.y), fmaxf(tmin.x, tmin.z));
+    *tfar = fminf(fminf(tmax.x, tmax.y), fminf(tmax.x, tmax.z));
+    if (!(*tfar > *tnear)) return 0;
+    if (*tnear < 0.0f) *tnear = 0.0f;
+    return 1;
+}
+
+static inline const float *gmm_wm(const orc_gmm *v, int x, int y, int z) {
+    size_t i = ((size_t)(z - v->z_base) * (size_t)v->ny + (size_t)y) * (size_t)v->nx + (size_t)x;
+    return v->wm + i * 2 * (size_t)v->K;
+}
+static inline const float *gmm_sg(const orc_gmm *v, int x, int y, int z) {
+    size_t i = ((size_t)(z - v->z_base) * (size_t)v->ny + (size_t)y) * (size_t)v->nx + (size_t)x;
+    return v->sg + i * (size_t)v->K;
+}
+static inline void gmm_mark(const orc_gmm *v, uint64_t *mark, int x, int y, int z) {
+    size_t idx = ((size_t)z * (size_t)v->ny + (size_t)y) * (size_t)v->nx + (size_t)x;
+    __atomic_fetch_or(&mark[idx >> 6], (uint64_t)1 << (idx & 63), __ATOMIC_RELAXED);
+}
+
+/* march one ray (state in/out) through the slab; returns 1 if it leaves the
+ * slab alive, 0 if it ended (early exit, tfar, 500 samples) */
+static int gmm_march(const orc_gmm *v, const orc_render_params *p, int z_lo, int z_hi, int slab,
+                     f3 d, float tfar, orc_gmm_ray *s, uint64_t *mark) {
+    const f3 step = {d.x * 0.01f, d.y * 0.01f, d.z * 0.01f};
+    for (;;) {
+        int x0, x1, y0, y1, z0, z1;
+        float ax, ay, az;
+        lin_axis(s->pos[0] * 0.5f + 0.5f, v->nx, &x0, &x1, &ax);
+        lin_axis(s->pos[1] * 0.5f + 0.5f, v->ny, &y0, &y1, &ay);
+        lin_axis(s->pos[2] * 0.5f + 0.5f, v->nz, &z0, &z1, &az);
+        if (slab && (z0 < z_lo || z0 >= z_hi)) return 1;
+        const int xs[2] = {x0, x1}, ys[2] = {y0, y1}, zs[2] = {z0, z1};
+        float sv[8];
+        for (int j = 0; j < 8; j++) {
+            const int X = xs[j & 1], Y = ys[(j >> 1) & 1], Z = zs[j >> 2];
+            if (mark) gmm_mark(v, mark, X, Y, Z);
+            sv[j] = orc_gmm_stat(gmm_wm(v, X, Y, Z), gmm_sg(v, X, Y, Z), v->K, p->query_method);
+        }
+        float c00 = lerpq(sv[0], sv[1], ax), c10 = lerpq(sv[2], sv[3], ax);
+        float c01 = lerpq(sv[4], sv[5], ax), c11 = lerpq(sv[6], sv[7], ax);
+        float c0 = lerpq(c00, c10, ay), c1 = lerpq(c01, c11, ay);
+        const float sample = lerpq(c0, c1, az);
+        s->n = s->n + 1;
+        float col[4];
+        orc_transfer((sample - p->transfer_offset) * p->transfer_scale, col); /* K:683 */
+        col[3] = col[3] * p->density;
+        col[0] = col[0] * col[3];
+        col[1] = col[1] * col[3];
+        col[2] = col[2] * col[3];
+        const float om = 1.0f - s->sum[3];
+        s->sum[0] = s->sum[0] + col[0] * om;
+        s->sum[1] = s->sum[1] + col[1] * om;
+        s->sum[2] = s->sum[2] + col[2] * om;
+        s->sum[3] = s->sum[3] + col[3] * om;
+        if (s->sum[3] > 0.95f) return 0;    /* K:698 */
+        s->t = s->t + 0.01f;                /* K:701 */
+        const int end = s->t > tfar || s->n >= 500; /* K:703, K:381 */
+        s->pos[0] = s->pos[0] + step.x;     /* K:706 */
+        s->pos[1] = s->pos[1] + step.y;
+        s->pos[2] = s->pos[2] + step.z;
+        if (end) return 0;
+    }
+}
+
+int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, int z_hi,
+                       const orc_gmm_ray *rays_in, uint32_t n_in, orc_gmm_ray *rays_out,
+                       uint32_t *n_out, uint32_t *out, float *out_f, int32_t *out_n,
+                       uint64_t *mark) {
+    const int slab = rays_out != NULL;
+    const uint64_t n = rays_in ? (uint64_t)n_in : (uint64_t)p->width * (uint64_t)p->height;
+    int64_t samples = 0;
+    uint32_t k_out = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        orc_gmm_ray s;
+        memset(&s, 0, sizeof s);
+        f3 o, d;
+        float tnear, tfar;
+        int x, y;
+        if (rays_in) {
+            s = rays_in[i];
+            x = (int)(s.pix % (uint32_t)p->width);
+            y = (int)(s.pix / (uint32_t)p->width);
+            if (!gmm_ray(p, x, y, &o, &d, &tnear, &tfar)) continue; /* not produced by a slab */
+        } else {
+            x = (int)(i % (uint64_t)p->width);
+            y = (int)(i / (uint64_t)p->width);
+            s.pix = (uint32_t)i;
+            if (!gmm_ray(p, x, y, &o, &d, &tnear, &tfar)) {
+                if (out_n) out_n[i] = -1;  /* K:302-303: no write */
+                continue;
+            }
+            s.t = tnear;
+            s.pos[0] = o.x + d.x * tnear;
+            s.pos[1] = o.y + d.y * tnear;
+            s.pos[2] = o.z + d.z * tnear;
+        }
+        const uint32_t n0 = s.n;
+        const int alive = gmm_march(v, p, z_lo, z_hi, slab, d, tfar, &s, mark);
+        samples += (int64_t)(s.n - n0);
+        if (alive) {
+            rays_out[k_out++] = s;
+            continue;
+        }
+        const float rgba[4] = {s.sum[0] * p->brightness, s.sum[1] * p->brightness,
+                               s.sum[2] * p->brightness, s.sum[3] * p->brightness};
+        if (out_n) out_n[s.pix] = (int32_t)s.n;
+        if (out) out[s.pix] = orc_pack(rgba);
+        if (out_f) {
+            out_f[(size_t)s.pix * 4 + 0] = sat(rgba[0]);
+            out_f[(size_t)s.pix * 4 + 1] = sat(rgba[1]);
+            out_f[(size_t)s.pix * 4 + 2] = sat(rgba[2]);
+            out_f[(size_t)s.pix * 4 + 3] = sat(rgba[3]);
+        }
+    }
+    if (n_out) *n_out = k_out;
+    return samples;
+}

@@ -134,6 +134,41 @@ uint64_t orc_splitmix64(uint64_t x);
 void orc_synth_fill(int nx, int ny, int nz, int nbins, uint64_t seed, float *vol,
                     int nthreads);
 
+/* ---- GMM distribution volumes (config 5) ----
+ * Restates vr_gmm.hip (this build's extension; the reference has no GMM).
+ * wm: (w, mu) pairs [voxel][K][2]; sg: sigma [voxel][K]; voxel order
+ * x + nx*(y + ny*(z - z_base)) over the resident slices [z_base, z_base + nzs). */
+typedef struct {                  /* alive-list entry, 48 bytes (GmmRay)        */
+    float sum[4];
+    float t, pos[3];
+    uint32_t pix, n, pad0, pad1;
+} orc_gmm_ray;
+
+typedef struct {
+    const float *wm, *sg;
+    int nx, ny, nz, K, z_base, nzs;
+} orc_gmm;
+
+/* statistic of one mixture record in the canonical order (vr_gmm.hip header):
+ * method 1 mean, 2 variance x 16 */
+float orc_gmm_stat(const float *wm_rec, const float *sg_rec, int K, int method);
+
+/* slices [z_base, z_base + nzs) of the synthetic GMM volume */
+void orc_synth_gmm(int nx, int ny, int nz, int K, uint64_t seed, int z_base, int nzs, float *wm,
+                   float *sg, int nthreads);
+
+/* Render with a GMM volume.  z_lo/z_hi: the slab (samples whose footprint z0
+ * lies in [z_lo, z_hi)); whole volume: 0, nz with rays_out == NULL.  rays_in ==
+ * NULL: camera rays of the whole frame; else n_in alive-list entries.  Rays
+ * leaving the slab alive are appended to rays_out (in input / raster order),
+ * their count stored in *n_out.  out / out_f / out_n as orc_render (pixel
+ * y*width + x).  mark: optional footprint bitset over nx*ny*nz voxels.
+ * Returns the samples taken. */
+int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, int z_hi,
+                       const orc_gmm_ray *rays_in, uint32_t n_in, orc_gmm_ray *rays_out,
+                       uint32_t *n_out, uint32_t *out, float *out_f, int32_t *out_n,
+                       uint64_t *mark);
+
 #ifdef __cplusplus
 }
 #endif

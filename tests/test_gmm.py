@@ -1,0 +1,237 @@
+"""GMM volumes (BASELINE config 5) -- CPU side.
+
+The oracle's GMM restatement is pinned by known answers (single-component
+mixtures, exact bin-free moments), an independent numpy restatement of the
+canonical decode order, the synthetic generator's stated properties, and the
+slab-chain identity (a chain of slab renders equals the whole-volume render
+bit for bit).  The reference has no GMM record, so there is nothing of the
+reference to pin against beyond the march semantics it shares with methods 1/2
+(ray, footprint, transfer, composite): "parity unpinned" for the record decode
+itself, which is this build's definition.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def np_fma32(a, b, c):
+    # float32 fma emulated in double: a*b is exact in double; the double sum
+    # rounds once more than a true fma, which can differ only at rare exact
+    # float midpoints (probability ~2^-29 per operation)
+    return np.float32(np.float64(a) * np.float64(b) + np.float64(c))
+
+
+def np_gmm_stat(wm, sg, method):
+    """independent restatement of the canonical lane order (vr_gmm.hip header):
+    L = K/4 lanes, lane s partial over components 4s .. 4s+3, pairwise tree"""
+    K = sg.shape[-1]
+    L = K // 4
+    w = wm.reshape(K, 2)[:, 0].astype(np.float32)
+    mu = wm.reshape(K, 2)[:, 1].astype(np.float32)
+    s = sg.astype(np.float32)
+    pm, pq = [], []
+    for lane in range(L):
+        k0 = 4 * lane
+        a = np.float32(w[k0] * mu[k0])
+        for j in range(1, 4):
+            a = np_fma32(w[k0 + j], mu[k0 + j], a)
+        pm.append(a)
+        q = np.float32(w[k0] * np_fma32(s[k0], s[k0], np.float32(mu[k0] * mu[k0])))
+        for j in range(1, 4):
+            k = k0 + j
+            q = np_fma32(w[k], np_fma32(s[k], s[k], np.float32(mu[k] * mu[k])), q)
+        pq.append(q)
+
+    def tree(p):
+        f = np.float32
+        while len(p) > 1:  # pairwise: (p0 + p1), (p2 + p3), ... then again
+            p = [f(p[i] + p[i + 1]) for i in range(0, len(p), 2)]
+        return p[0]
+    m = tree(pm)
+    if method == 1:
+        return float(m)
+    return float(np.float32(np.float32(tree(pq) - np.float32(m * m)) * np.float32(16.0)))
+
+
+@pytest.mark.parametrize("K", [8, 16, 32])
+def test_gmm_stat_known_answers(orc, K):
+    wm = np.zeros((K, 2), np.float32)
+    sg = np.zeros(K, np.float32)
+    # one component carries all the weight: mean = mu, variance = sigma^2
+    wm[3] = (1.0, 0.375)
+    sg[3] = 0.125
+    sg[5] = 0.5  # weightless components contribute nothing
+    wm[5, 1] = 0.9
+    assert orc.gmm_stat(wm, sg, 1) == 0.375
+    assert orc.gmm_stat(wm, sg, 2) == pytest.approx(16 * 0.125 ** 2, abs=1e-6)
+    # two equal halves at 0.25 / 0.75, sigma 0: mean 0.5, variance 0.0625
+    wm[:] = 0
+    sg[:] = 0
+    wm[0] = (0.5, 0.25)
+    wm[K - 1] = (0.5, 0.75)
+    assert orc.gmm_stat(wm, sg, 1) == 0.5
+    assert orc.gmm_stat(wm, sg, 2) == pytest.approx(16 * 0.0625, abs=1e-6)
+
+
+@pytest.mark.parametrize("K", [8, 16, 32])
+def test_gmm_stat_matches_numpy_restatement(orc, K):
+    rng = np.random.default_rng(K)
+    for _ in range(200):
+        r = rng.random(K).astype(np.float32) + np.float32(0.05)
+        wm = np.stack([r / np.float32(r.sum()), rng.random(K).astype(np.float32)], -1)
+        sg = (rng.random(K) * 0.05 + 0.005).astype(np.float32)
+        for m in (1, 2):
+            assert orc.gmm_stat(wm, sg, m) == np_gmm_stat(wm, sg, m)
+
+
+def test_synth_gmm_properties(orc):
+    wm, sg = orc.synth_gmm(20, 18, 16, 16)
+    w, mu = wm[..., 0], wm[..., 1]
+    assert np.all(np.abs(w.sum(-1, dtype=np.float64) - 1) < 1e-5)
+    assert w.min() > 0 and mu.min() >= 0 and mu.max() <= 1
+    assert sg.min() >= 0.005 and sg.max() <= 0.055
+    # the mixture follows the section-5 blob field: means are not flat
+    mean = (w * mu).sum(-1)
+    assert mean.max() - mean.min() > 0.3
+    # slices generated on their own equal the same slices of the whole volume
+    part = orc.synth_gmm(20, 18, 16, 16, z_base=5, nslices=7)
+    assert np.array_equal(part[0], wm[5:12]) and np.array_equal(part[1], sg[5:12])
+
+
+def test_gmm_render_known_answers(orc, pkg):
+    """constant mixtures: every sample has the same statistic, so the composite is
+    the closed form of a constant-alpha ray (the methods-1/2 march semantics)"""
+    nx = ny = nz = 8
+    K = 8
+    wm = np.zeros((nz, ny, nx, K, 2), np.float32)
+    sg = np.zeros((nz, ny, nx, K), np.float32)
+    wm[..., 0, :] = (1.0, 0.5)   # mean 0.5 -> TF entry 4 (green, alpha 1)
+    W, H = 32, 32
+    m = pkg.camera.single_test_inv_view()
+    p = orc.make_params(W, H, m, query_method=1)
+    r = orc.render_gmm(wm, sg, (nx, ny, nz), p)
+    steps = r["out_n"]
+    # centre ray: tnear = 3, tfar = 5 -> 200 samples without early exit; with
+    # alpha = 0.05 per sample the ray stops at sample 59 (sum.w = 0.9515)
+    assert steps[16, 16] == 59
+    assert r["out_f"][16, 16, 3] == pytest.approx(1 - 0.95 ** 59, abs=1e-5)
+    assert r["out_n"][0, 0] == -1  # corner pixel misses the box
+
+
+def _chain(orc, wm, sg, dims, p, bounds):
+    """render slab by slab (each slab from only its resident slices)"""
+    nx, ny, nz = dims
+    out = np.zeros((p.height, p.width), np.uint32)
+    out_f = np.zeros((p.height, p.width, 4), np.float32)
+    out_n = np.full((p.height, p.width), -2, np.int32)
+    rays = None
+    for (z_lo, z_hi) in bounds:
+        zb = z_lo
+        ns = min(z_hi + 1, nz) - z_lo
+        r = orc.render_gmm(wm[zb:zb + ns], sg[zb:zb + ns], dims, p, z_base=zb,
+                           slab=(z_lo, z_hi), rays_in=rays)
+        w = r["out_n"] != -2
+        out[w], out_f[w], out_n[w] = r["out"][w], r["out_f"][w], r["out_n"][w]
+        rays = r["rays_out"]
+    assert rays is not None and rays.shape[0] == 0  # the last slab ends every ray
+    return out, out_f, out_n
+
+
+@pytest.mark.parametrize("view", ["C0", (30.0, 45.0), (180.0, 0.0), (200.0, 20.0)])
+@pytest.mark.parametrize("method", [1, 2])
+def test_slab_chain_equals_whole_volume(orc, pkg, view, method):
+    dims = (22, 18, 20)
+    wm, sg = orc.synth_gmm(*dims, 16)
+    m = pkg.camera.single_test_inv_view() if view == "C0" else pkg.camera.display_inv_view(view)
+    W, H = 64, 48
+    p = orc.make_params(W, H, m, query_method=method, density=0.3)
+    full = orc.render_gmm(wm, sg, dims, p)
+    direction = pkg.slabs.march_direction(m, W, H)
+    assert direction != 0
+    for n in (1, 2, 3, 7):
+        bounds = pkg.slabs.slab_bounds(dims[2], n, direction)
+        out, out_f, out_n = _chain(orc, wm, sg, dims, p, bounds)
+        assert np.array_equal(out, full["out"]), f"{n} slabs: RGBA8 differs"
+        assert np.array_equal(out_f, full["out_f"]), f"{n} slabs: float RGBA differs"
+        assert np.array_equal(out_n, full["out_n"]), f"{n} slabs: samples differ"
+
+
+def test_slab_partition_helpers(pkg):
+    s = pkg.slabs
+    assert s.slab_bounds(2048, 8, -1)[0] == (1792, 2048)
+    b = s.slab_bounds(100, 7, 1)
+    assert b[0][0] == 0 and b[-1][1] == 100
+    assert all(b[i][1] == b[i + 1][0] for i in range(6))
+    assert s.resident_slices(1792, 2048, 2048) == (1792, 256)
+    assert s.resident_slices(0, 256, 2048) == (0, 257)
+    with pytest.raises(ValueError):
+        s.slab_bounds(10, 2, 0)
+    # the config-5 slab with its halo: 2048 x 2048 x 257 voxels x 192 B per voxel
+    assert 2048 * 2048 * 257 * 192 < 288e9 * 0.75
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _chain_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as g
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        orc = g.load_oracle()
+        pkg = g.load_package()
+        dims = (18, 16, 21)
+        m = pkg.camera.display_inv_view((30.0, 45.0))
+        W, H = 48, 40
+        p = orc.make_params(W, H, m, query_method=1, density=0.3)
+        bounds = pkg.slabs.slab_bounds(dims[2], world, pkg.slabs.march_direction(m, W, H))
+        z_lo, z_hi = bounds[rank]
+        zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, dims[2])
+        wm, sg = orc.synth_gmm(*dims, 8, z_base=zb, nslices=ns)  # this rank's slab only
+        frame = np.zeros((H, W), np.uint32)
+        rays_in = torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32)
+
+        def render_slab(rin, n_in):
+            r = orc.render_gmm(wm, sg, dims, p, z_base=zb, slab=(z_lo, z_hi),
+                               rays_in=None if rin is None else rin[:n_in].numpy().view(np.uint32))
+            frame[:] = r["out"]
+            ro = r["rays_out"]
+            return torch.from_numpy(ro.view(np.int32).copy()), ro.shape[0]
+
+        pkg.slabs.chain_frame(rank, world, render_slab, rays_in, 0, dist)
+        t = torch.from_numpy(frame.view(np.int32).copy())
+        dist.reduce(t, 0, op=dist.ReduceOp.SUM)  # every pixel is written by one rank
+        if rank == 0:
+            q.put(t.numpy().view(np.uint32).copy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_slab_chain_matches_whole_volume(orc, pkg):
+    """two ranks (gloo): rank 0 marches its slab, sends the alive list, rank 1 marches
+    the rest; the summed frames equal the single-process whole-volume render"""
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chain_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(120)
+        assert pr.exitcode == 0
+    got = q.get()
+    dims = (18, 16, 21)
+    wm, sg = orc.synth_gmm(*dims, 8)
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    full = orc.render_gmm(wm, sg, dims, orc.make_params(48, 40, m, query_method=1, density=0.3))
+    assert np.array_equal(got, full["out"])

@@ -1,0 +1,171 @@
+"""GPU parity of the GMM march (config 5) against the CPU
+oracle, through the C-ABI: whole-volume renders, slab chains with only each
+slab's slices resident, the on-device generator, the footprint count and the
+error paths.  Bar: packed RGBA8 and samples per pixel identical, float RGBA
+within 1e-4 (the north star's tolerance; the decode order is fixed, so the
+results are in fact bit-identical)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def gmm_render(pkg, W, H, m, method, torch, slab=None, density=0.05):
+    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    out_f = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+    steps = torch.full((H * W,), -2, dtype=torch.int32, device="cuda")
+    d = pkg.make_desc(out, W, H, m, query_method=method, density=density, volume_size=(1, 1, 1),
+                      d_output_f=out_f, d_steps=steps)
+    pkg.render_gmm(d, slab)
+    torch.cuda.synchronize()
+    return (out.cpu().numpy().view(np.uint32).reshape(H, W),
+            out_f.cpu().numpy().reshape(H, W, 4), steps.cpu().numpy().reshape(H, W))
+
+
+def check(got, ref, what):
+    g8, gf, gn = got
+    assert np.array_equal(gn, ref["out_n"]), f"{what}: samples per pixel differ"
+    assert np.array_equal(g8, ref["out"]), f"{what}: {int(np.sum(g8 != ref['out']))} RGBA8 differ"
+    err = float(np.max(np.abs(gf - ref["out_f"])))
+    assert err <= TOL, f"{what}: max |RGBA - oracle| = {err}"
+
+
+CAMS = {"C0": None, "C1": (30.0, 45.0), "below": (180.0, 0.0), "side": (90.0, 0.0)}
+
+
+def cam(pkg, name):
+    return pkg.camera.single_test_inv_view() if CAMS[name] is None else \
+        pkg.camera.display_inv_view(CAMS[name])
+
+
+@pytest.mark.parametrize("K", [8, 16, 32])
+@pytest.mark.parametrize("method", [1, 2])
+def test_gmm_whole_volume(pkg, orc, gpu, K, method):
+    import torch
+    dims = (26, 22, 18)
+    wm, sg = orc.synth_gmm(*dims, K, seed=K)
+    pkg.init_gmm(wm, sg)
+    for c in CAMS:
+        for density in (0.05, 0.6):
+            m = cam(pkg, c)
+            got = gmm_render(pkg, 80, 64, m, method, torch, density=density)
+            ref = orc.render_gmm(wm, sg, dims, orc.make_params(80, 64, m, query_method=method,
+                                                               density=density))
+            check(got, ref, f"K={K} m{method} {c} d={density}")
+    assert pkg.last_kernel().startswith("k_march_gmm") and f"<B={K},M={method}>" in pkg.last_kernel()
+    pkg.free_gmm()
+
+
+def test_synth_gmm_matches_oracle(pkg, orc, gpu):
+    import torch
+    dims = (20, 14, 12)
+    for zb, ns in ((0, 12), (5, 4)):
+        pkg.synthesize_gmm(dims, 16, seed=99, z_base=zb, nslices=ns)
+        (X, Y, Z), K, z0, n, pwm, psg = pkg.gmm_info()
+        assert (X, Y, Z, K, z0, n) == (20, 14, 12, 16, zb, ns)
+        nvox = 20 * 14 * ns
+        wm = torch.empty(nvox * K * 2, dtype=torch.float32, device="cuda")
+        sg = torch.empty(nvox * K, dtype=torch.float32, device="cuda")
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(wm.data_ptr(), pwm, wm.numel() * 4, 3) == 0
+        assert hip.hipMemcpy(sg.data_ptr(), psg, sg.numel() * 4, 3) == 0
+        rwm, rsg = orc.synth_gmm(*dims, 16, seed=99, z_base=zb, nslices=ns)
+        assert np.array_equal(wm.cpu().numpy(), rwm.reshape(-1))
+        assert np.array_equal(sg.cpu().numpy(), rsg.reshape(-1))
+    pkg.free_gmm()
+
+
+@pytest.mark.parametrize("c", ["C0", "C1", "below"])
+@pytest.mark.parametrize("nslabs", [2, 3, 5])
+def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs):
+    """each slab generated on its own (only its slices + halo resident), the alive
+    list handed from slab to slab on the device: the frame, the samples and every
+    alive ray's exact state equal the oracle's chain and the whole-volume render"""
+    import torch
+    dims = (24, 20, 23)
+    K, method, W, H = 16, 1 if nslabs != 3 else 2, 72, 56
+    m = cam(pkg, c)
+    direction = pkg.slabs.march_direction(m, W, H)
+    bounds = pkg.slabs.slab_bounds(dims[2], nslabs, direction)
+    wm, sg = orc.synth_gmm(*dims, K)
+    p = orc.make_params(W, H, m, query_method=method, density=0.2)
+    full = orc.render_gmm(wm, sg, dims, p)
+    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    out_f = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+    steps = torch.full((H * W,), -2, dtype=torch.int32, device="cuda")
+    d = pkg.make_desc(out, W, H, m, query_method=method, density=0.2, volume_size=(1, 1, 1),
+                      d_output_f=out_f, d_steps=steps)
+    bufs = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
+    cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
+    n_in = 0
+    ref_rays = None
+    for i, (z_lo, z_hi) in enumerate(bounds):
+        zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, dims[2])
+        pkg.synthesize_gmm(dims, K, z_base=zb, nslices=ns)
+        cnt.zero_()
+        rin = bufs[(i + 1) % 2] if i else None
+        s = pkg.gmm_slab(z_lo, z_hi, bufs[i % 2], cnt[0:1], d_rays_in=rin, n_rays_in=n_in)
+        pkg.render_gmm(d, s)
+        torch.cuda.synchronize()
+        n_in = int(cnt[0].item())
+        r = orc.render_gmm(wm[zb:zb + ns], sg[zb:zb + ns], dims, p, z_base=zb, slab=(z_lo, z_hi),
+                           rays_in=ref_rays)
+        ref_rays = r["rays_out"]
+        assert n_in == ref_rays.shape[0], f"slab {i}: {n_in} alive rays vs {ref_rays.shape[0]}"
+        got_rays = bufs[i % 2][:n_in].cpu().numpy().view(np.uint32)
+        order = np.argsort(got_rays[:, 8], kind="stable")
+        assert np.array_equal(got_rays[order], ref_rays[np.argsort(ref_rays[:, 8], kind="stable")])
+    assert n_in == 0
+    torch.cuda.synchronize()
+    got = (out.cpu().numpy().view(np.uint32).reshape(H, W), out_f.cpu().numpy().reshape(H, W, 4),
+           steps.cpu().numpy().reshape(H, W))
+    check(got, full, f"{nslabs} slabs {c}")
+    pkg.free_gmm()
+
+
+def test_gmm_footprint_count(pkg, orc, gpu):
+    import torch
+    dims = (30, 26, 22)
+    wm, sg = orc.synth_gmm(*dims, 16)
+    pkg.init_gmm(wm, sg)
+    for c in ("C0", "C1"):
+        m = cam(pkg, c)
+        out = torch.zeros(96 * 80, dtype=torch.int32, device="cuda")
+        d = pkg.make_desc(out, 96, 80, m, query_method=1, volume_size=(1, 1, 1))
+        u = pkg.gmm_count_footprint(d)
+        ref = orc.render_gmm(wm, sg, dims, orc.make_params(96, 80, m, query_method=1),
+                             want_mark=True)
+        assert u == ref["U"] > 0
+    pkg.free_gmm()
+
+
+def test_gmm_errors(pkg, orc, gpu):
+    import torch
+    dims = (16, 16, 16)
+    pkg.synthesize_gmm(dims, 8, z_base=4, nslices=6)
+    out = torch.zeros(32 * 32, dtype=torch.int32, device="cuda")
+    rays = torch.zeros((32 * 32, 12), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    m = pkg.camera.single_test_inv_view()
+    d = pkg.make_desc(out, 32, 32, m, query_method=1, volume_size=(1, 1, 1))
+    with pytest.raises(pkg.VRError, match="resident"):
+        pkg.render_gmm(d)  # not all slices resident
+    with pytest.raises(pkg.VRError, match="needs slices"):
+        pkg.render_gmm(d, pkg.gmm_slab(4, 10, rays, cnt))  # halo slice 10 missing
+    pkg.render_gmm(d, pkg.gmm_slab(4, 9, rays, cnt))      # [4, 9) + halo 9: resident
+    d3 = pkg.make_desc(out, 32, 32, m, query_method=3, volume_size=(1, 1, 1))
+    with pytest.raises(pkg.VRError) as e:
+        pkg.render_gmm(d3, pkg.gmm_slab(4, 9, rays, cnt))
+    assert e.value.status == pkg._lib.VR_ERR_UNSUPPORTED
+    side = pkg.make_desc(out, 32, 32, pkg.camera.display_inv_view((90.0, 0.0)), query_method=1,
+                         volume_size=(1, 1, 1))
+    with pytest.raises(pkg.VRError, match="both directions"):
+        pkg.render_gmm(side, pkg.gmm_slab(4, 9, rays, cnt))
+    with pytest.raises(pkg.VRError):
+        pkg.synthesize_gmm(dims, 12)  # K must be 8, 16 or 32
+    torch.cuda.synchronize()
+    pkg.free_gmm()

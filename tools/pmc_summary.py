@@ -8,7 +8,7 @@ import sys
 root = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else "k_march<8, 1, false>"
 vals = collections.defaultdict(list)
-for f in sorted(glob.glob(f"{root}/p*/*counter_collection.csv")):
+for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
     per = collections.defaultdict(dict)
     for r in csv.DictReader(open(f)):
         if pat in r["Kernel_Name"]:

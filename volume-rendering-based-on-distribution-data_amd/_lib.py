@@ -57,6 +57,21 @@ class RenderDesc(ctypes.Structure):
     ]
 
 
+class GmmSlab(ctypes.Structure):
+    """vr_gmm_slab (include/vr.h): one slab of a slab-chained GMM render"""
+    _fields_ = [
+        ("z_lo", ctypes.c_int),
+        ("z_hi", ctypes.c_int),
+        ("d_rays_in", ctypes.c_void_p),
+        ("n_rays_in", ctypes.c_uint32),
+        ("d_rays_out", ctypes.c_void_p),
+        ("d_n_rays_out", ctypes.c_void_p),
+    ]
+
+
+GMM_RAY_BYTES = 48  # alive-list entry: float sum[4], t, pos[3]; uint32 pixel, samples, 0, 0
+
+
 class FlexTables(ctypes.Structure):
     """vr_flex_tables (include/vr.h)"""
     _fields_ = [
@@ -81,6 +96,8 @@ EXPORTS = [
     "vr_load_reference_files", "vr_init_flex", "vr_flex_process", "vr_flex_info",
     "vr_parse_span_list", "vr_parse_fractal_histogram", "vr_parse_simple_histogram",
     "vr_load_flex_files", "vr_debug_wave_clock",
+    "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_render_gmm",
+    "vr_gmm_count_footprint",
 ]
 
 _lib = None
@@ -177,6 +194,18 @@ def load() -> ctypes.CDLL:
     L.vr_debug_wave_clock.restype = ctypes.c_int
     L.vr_last_kernel.argtypes = []
     L.vr_last_kernel.restype = ctypes.c_char_p
+    L.vr_init_gmm.argtypes = [vp, vp, Extent, i32, i32, i32, i32]
+    L.vr_init_gmm.restype = i32
+    L.vr_synthesize_gmm.argtypes = [Extent, i32, ctypes.c_uint64, i32, i32]
+    L.vr_synthesize_gmm.restype = i32
+    L.vr_gmm_info.argtypes = [vp] * 6
+    L.vr_gmm_info.restype = i32
+    L.vr_free_gmm.argtypes = []
+    L.vr_free_gmm.restype = i32
+    L.vr_render_gmm.argtypes = [ctypes.POINTER(RenderDesc), ctypes.POINTER(GmmSlab)]
+    L.vr_render_gmm.restype = i32
+    L.vr_gmm_count_footprint.argtypes = [ctypes.POINTER(RenderDesc)]
+    L.vr_gmm_count_footprint.restype = ctypes.c_int64
     _lib = L
     return L
 

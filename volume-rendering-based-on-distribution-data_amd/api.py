@@ -369,6 +369,75 @@ def debug_wave_clock(d_buf) -> None:
     check(_lib.load().vr_debug_wave_clock(None if d_buf is None else _ptr(d_buf)))
 
 
+# ------------------------------------------- GMM volumes (config 5)
+
+def init_gmm(wm, sigma, dims=None, z_base: int = 0, adopt: bool = False) -> None:
+    """Make a K-component GMM volume resident.
+
+    wm: (nzs, ny, nx, K, 2) float32 (w, mu) pairs; sigma: (nzs, ny, nx, K).  numpy
+    arrays are copied from the host, torch CUDA tensors device-to-device (or used
+    in place with adopt=True).  dims: the whole volume's (X, Y, Z) when only the
+    slices [z_base, z_base + nzs) are given (default: wm's own shape)."""
+    L = _lib.load()
+    nzs, ny, nx, K = (int(v) for v in wm.shape[:4])
+    if dims is None:
+        dims = (nx, ny, nzs)
+    if hasattr(wm, "data_ptr") and getattr(wm, "is_cuda", False):
+        check(L.vr_init_gmm(_ptr(wm), _ptr(sigma), _extent(dims), K, int(z_base), nzs,
+                            2 if adopt else 1))
+        return
+    a = np.ascontiguousarray(np.asarray(wm, dtype=np.float32))
+    b = np.ascontiguousarray(np.asarray(sigma, dtype=np.float32))
+    if b.shape != a.shape[:4]:
+        raise ValueError("sigma must have shape wm.shape[:4]")
+    check(L.vr_init_gmm(a.ctypes.data, b.ctypes.data, _extent(dims), K, int(z_base), nzs, 0))
+
+
+def synthesize_gmm(dims, ncomp: int = 16, seed: int = 20261015, z_base: int = 0,
+                   nslices: Optional[int] = None) -> None:
+    """Generate slices [z_base, z_base + nslices) of the seeded synthetic GMM volume in HBM."""
+    if nslices is None:
+        nslices = int(tuple(dims)[2]) - int(z_base)
+    check(_lib.load().vr_synthesize_gmm(_extent(dims), int(ncomp), int(seed), int(z_base),
+                                        int(nslices)))
+
+
+def gmm_info():
+    """((X, Y, Z), K, z_base, nslices, wm_ptr, sigma_ptr) of the resident GMM volume"""
+    e = Extent()
+    k, zb, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    check(_lib.load().vr_gmm_info(ctypes.byref(e), ctypes.byref(k), ctypes.byref(zb),
+                                  ctypes.byref(ns), ctypes.byref(a), ctypes.byref(b)))
+    return (e.width, e.height, e.depth), k.value, zb.value, ns.value, a.value, b.value
+
+
+def free_gmm() -> None:
+    check(_lib.load().vr_free_gmm())
+
+
+def gmm_slab(z_lo: int, z_hi: int, d_rays_out, d_n_rays_out, d_rays_in=None,
+             n_rays_in: int = 0) -> _lib.GmmSlab:
+    s = _lib.GmmSlab()
+    s.z_lo, s.z_hi = int(z_lo), int(z_hi)
+    s.d_rays_in = _ptr(d_rays_in) or None
+    s.n_rays_in = int(n_rays_in)
+    s.d_rays_out = _ptr(d_rays_out) or None
+    s.d_n_rays_out = _ptr(d_n_rays_out) or None
+    return s
+
+
+def render_gmm(desc: RenderDesc, slab: Optional[_lib.GmmSlab] = None) -> None:
+    """Launch the GMM march: the whole frame (slab None) or one slab of a chain."""
+    L = _lib.load()
+    check(L.vr_render_gmm(ctypes.byref(desc), None if slab is None else ctypes.byref(slab)))
+
+
+def gmm_count_footprint(desc: RenderDesc) -> int:
+    """U of a whole-volume GMM render (synchronous)"""
+    return int(check(_lib.load().vr_gmm_count_footprint(ctypes.byref(desc))))
+
+
 def version() -> str:
     return _lib.load().vr_version().decode()
 
@@ -380,5 +449,7 @@ __all__ = [
     "volume_info",
     "volume_layout",
     "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "version",
+    "init_gmm", "synthesize_gmm", "gmm_info", "free_gmm", "gmm_slab", "render_gmm",
+    "gmm_count_footprint",
     "VRError", "PAD",
 ]

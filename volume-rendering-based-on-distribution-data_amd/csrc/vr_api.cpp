@@ -55,6 +55,14 @@ struct State {
     uint32_t *tile_cost = nullptr;
     size_t tile_cost_cap = 0;
     unsigned long long *wave_clock = nullptr;  // vr_debug_wave_clock (tooling)
+    // GMM volume (config 5, vr_gmm.hip): planes (w, mu)[voxel][K][2] and
+    // sigma[voxel][K] of the resident slices [z_base, z_base + nzs) of an
+    // nx x ny x nz volume
+    struct Gmm {
+        float *wm = nullptr, *sg = nullptr;
+        bool owned = false;
+        int nx = 0, ny = 0, nz = 0, K = 0, z_base = 0, nzs = 0;
+    } gmm;
     // bumped whenever a resident volume / codec / flexible-block set is
     // released, so an order learned on old data is not reused (the order is a
     // scheduling hint only: any order renders the same image)
@@ -1101,6 +1109,255 @@ int vr_unscatter_tiles(const uint32_t *d_packed, const uint32_t *d_tile_lists, u
     return VR_OK;
 }
 
+// ---------------- GMM volumes (config 5) ----------
+
+}  // extern "C"
+
+namespace {
+
+void release_gmm() {
+    g.volume_epoch++;
+    if (g.gmm.owned) {
+        if (g.gmm.wm) (void)hipFree(g.gmm.wm);
+        if (g.gmm.sg) (void)hipFree(g.gmm.sg);
+    }
+    g.gmm = State::Gmm{};
+}
+
+int check_gmm_shape(vr_extent dims, int K, int z_base, int nzs) {
+    if (K != 8 && K != 16 && K != 32)
+        return fail(VR_ERR_UNSUPPORTED, "GMM volumes with %d components (compiled: 8, 16, 32)", K);
+    if (dims.width == 0 || dims.height == 0 || dims.depth == 0 || dims.width > 65536 ||
+        dims.height > 65536 || dims.depth > 65536)
+        return fail(VR_ERR_ARG, "GMM volume: bad dims");
+    if (z_base < 0 || nzs < 1 || (size_t)z_base + (size_t)nzs > dims.depth)
+        return fail(VR_ERR_ARG, "GMM volume: resident slices [%d, %d) outside [0, %zu)", z_base,
+                    z_base + nzs, dims.depth);
+    return VR_OK;
+}
+
+// Parameters of a GMM launch: the reference's ray / transfer / composite
+// inputs from the descriptor, the resident slices, and the slab.
+int fill_gmm_params(const vr_render_desc *d, const vr_gmm_slab *slab, vr::Params &P,
+                    uint32_t &nblocks) {
+    if (!d) return fail(VR_ERR_ARG, "null render descriptor");
+    if (!g.gmm.wm) return fail(VR_ERR_STATE, "no GMM volume resident (vr_init_gmm / vr_synthesize_gmm)");
+    if (d->query_method != 1 && d->query_method != 2)
+        return fail(VR_ERR_UNSUPPORTED, "GMM volumes support queryMethod 1 (mean) and 2 (variance)");
+    if (!d->d_output) return fail(VR_ERR_ARG, "d_output is null");
+    if (d->width == 0 || d->height == 0) return fail(VR_ERR_ARG, "empty image");
+    if ((uint64_t)d->width * d->height > 0xFFFFFFFFull) return fail(VR_ERR_ARG, "image too large");
+    if (d->d_tile_list) return fail(VR_ERR_UNSUPPORTED, "GMM renders take whole frames or alive lists");
+    std::memset(&P, 0, sizeof P);
+    std::memcpy(P.m, d->inv_view, sizeof P.m);
+    P.W = d->width;
+    P.H = d->height;
+    P.density = d->density;
+    P.brightness = d->brightness;
+    P.toff = d->transfer_offset;
+    P.tscale = d->transfer_scale;
+    P.nx = g.gmm.nx; P.ny = g.gmm.ny; P.nz = g.gmm.nz;
+    P.gwm = g.gmm.wm;
+    P.gsg = g.gmm.sg;
+    P.gk = g.gmm.K;
+    P.z_base = g.gmm.z_base;
+    P.nzs = g.gmm.nzs;
+    P.tiles_x = tiles_x(d->width);
+    P.out = d->d_output;
+    P.out_f = d->d_output_f;
+    P.out_n = d->d_steps;
+    device_lds(P.lds_cu, P.lds_wg);
+    if (const char *e = std::getenv("VR_WG_PER_CU")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= 32) P.wg_per_cu = v;
+    }
+    if (const char *e = std::getenv("VR_GMM_LOCKSTEP")) P.path = std::atoi(e) ? 1 : 0;
+    const int zr_hi = g.gmm.z_base + g.gmm.nzs;  // resident slices end (exclusive)
+    if (!slab) {
+        if (g.gmm.z_base != 0 || g.gmm.nzs != g.gmm.nz)
+            return fail(VR_ERR_STATE, "only slices [%d, %d) of the GMM volume are resident: "
+                        "render it slab by slab (vr_render_gmm with a vr_gmm_slab)",
+                        g.gmm.z_base, zr_hi);
+        P.z_lo = 0;
+        P.z_hi = g.gmm.nz;
+    } else {
+        if (slab->z_lo < 0 || slab->z_hi > g.gmm.nz || slab->z_lo >= slab->z_hi)
+            return fail(VR_ERR_ARG, "slab [%d, %d) outside the volume's [0, %d)", slab->z_lo,
+                        slab->z_hi, g.gmm.nz);
+        // a footprint with z0 in [z_lo, z_hi) reads slices z0 and min(z0 + 1, nz - 1)
+        const int need_hi = std::min(slab->z_hi + 1, g.gmm.nz);
+        if (slab->z_lo < g.gmm.z_base || need_hi > zr_hi)
+            return fail(VR_ERR_ARG, "slab [%d, %d) needs slices [%d, %d); resident: [%d, %d)",
+                        slab->z_lo, slab->z_hi, slab->z_lo, need_hi, g.gmm.z_base, zr_hi);
+        if (!slab->d_rays_out || !slab->d_n_rays_out)
+            return fail(VR_ERR_ARG, "a slab launch needs d_rays_out and d_n_rays_out");
+        if (slab->n_rays_in && !slab->d_rays_in) return fail(VR_ERR_ARG, "d_rays_in is null");
+        // slabs must be taken in the order every ray crosses them: the sign of
+        // a ray's z step is that of the linear form u M8 + v M9 - 2 M10, so the
+        // four frame corners decide whether it is the same for the whole frame
+        const float *M = d->inv_view;
+        int pos = 0, neg = 0;
+        for (int c = 0; c < 4; c++) {
+            const float u = (c & 1) ? ((float)(d->width - 1) / (float)d->width) * 2.0f - 1.0f : -1.0f;
+            const float v = (c & 2) ? ((float)(d->height - 1) / (float)d->height) * 2.0f - 1.0f : -1.0f;
+            const float dz = u * M[8] + v * M[9] - 2.0f * M[10];
+            pos += dz > 0.0f;
+            neg += dz < 0.0f;
+        }
+        if (pos && neg)
+            return fail(VR_ERR_UNSUPPORTED, "rays of this view cross z-slabs in both directions: "
+                        "slab-chained rendering needs one crossing order");
+        P.z_lo = slab->z_lo;
+        P.z_hi = slab->z_hi;
+        P.rays_in = reinterpret_cast<const uint4 *>(slab->d_rays_in);
+        P.n_rays_in = slab->d_rays_in ? slab->n_rays_in : 0;
+        P.rays_out = reinterpret_cast<uint4 *>(slab->d_rays_out);
+        P.n_rays_out = slab->d_n_rays_out;
+    }
+    if (P.rays_in || (slab && slab->d_rays_in)) {
+        nblocks = (uint32_t)(((uint64_t)P.n_rays_in + 255) / 256);
+        P.n_tiles = nblocks;
+    } else {
+        nblocks = tiles_x(d->width) * tiles_y(d->height);
+        P.n_tiles = nblocks;
+        int rc = frame_order(d, tiles_x(d->width), tiles_y(d->height), P.perm, nullptr);
+        if (rc != VR_OK) return rc;
+    }
+    return VR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vr_init_gmm(const float *wm, const float *sigma, vr_extent dims, int ncomp, int z_base,
+                int nslices, int where) {
+    int rc = check_gmm_shape(dims, ncomp, z_base, nslices);
+    if (rc != VR_OK) return rc;
+    if (!wm || !sigma) return fail(VR_ERR_ARG, "vr_init_gmm: null plane");
+    if (where < 0 || where > 2) return fail(VR_ERR_ARG, "vr_init_gmm: where must be 0, 1 or 2");
+    const uint64_t nvox = (uint64_t)dims.width * dims.height * (uint64_t)nslices;
+    const size_t bwm = nvox * (size_t)ncomp * 8, bsg = nvox * (size_t)ncomp * 4;
+    release_gmm();
+    State::Gmm m;
+    m.nx = (int)dims.width; m.ny = (int)dims.height; m.nz = (int)dims.depth;
+    m.K = ncomp; m.z_base = z_base; m.nzs = nslices;
+    if (where == 2) {
+        m.wm = const_cast<float *>(wm);
+        m.sg = const_cast<float *>(sigma);
+        m.owned = false;
+    } else {
+        hipError_t e = hipMalloc(&m.wm, bwm);
+        if (e == hipSuccess) e = hipMalloc(&m.sg, bsg);
+        const hipMemcpyKind k = where == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+        if (e == hipSuccess) e = hipMemcpy(m.wm, wm, bwm, k);
+        if (e == hipSuccess) e = hipMemcpy(m.sg, sigma, bsg, k);
+        if (e != hipSuccess) {
+            if (m.wm) (void)hipFree(m.wm);
+            if (m.sg) (void)hipFree(m.sg);
+            return hip_fail(e, "vr_init_gmm");
+        }
+        m.owned = true;
+    }
+    g.gmm = m;
+    return VR_OK;
+}
+
+int vr_synthesize_gmm(vr_extent dims, int ncomp, uint64_t seed, int z_base, int nslices) {
+    int rc = check_gmm_shape(dims, ncomp, z_base, nslices);
+    if (rc != VR_OK) return rc;
+    const int nx = (int)dims.width, ny = (int)dims.height, nz = (int)dims.depth;
+    const uint64_t nvox = (uint64_t)nx * ny * (uint64_t)nslices;
+    vr::SynthArgs a{};
+    std::vector<float> gx, gy, gz;
+    blob_tables(nx, ny, nz, seed, a, gx, gy, gz);
+    release_gmm();
+    State::Gmm m;
+    float *dgx = nullptr, *dgy = nullptr, *dgz = nullptr;
+    hipError_t e = hipMalloc(&m.wm, nvox * (size_t)ncomp * 8);
+    if (e == hipSuccess) e = hipMalloc(&m.sg, nvox * (size_t)ncomp * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgx, gx.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgy, gy.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&dgz, gz.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(dgx, gx.data(), gx.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgy, gy.data(), gy.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgz, gz.data(), gz.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        a.gx = dgx; a.gy = dgy; a.gz = dgz;
+        a.nx = nx; a.ny = ny; a.nz = nz; a.nb = ncomp; a.seed = seed;
+        e = vr::launch_synth_gmm(m.wm, m.sg, a, ncomp, z_base, nslices, g.stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    if (dgx) (void)hipFree(dgx);
+    if (dgy) (void)hipFree(dgy);
+    if (dgz) (void)hipFree(dgz);
+    if (e != hipSuccess) {
+        if (m.wm) (void)hipFree(m.wm);
+        if (m.sg) (void)hipFree(m.sg);
+        return hip_fail(e, "vr_synthesize_gmm");
+    }
+    m.nx = nx; m.ny = ny; m.nz = nz; m.K = ncomp; m.z_base = z_base; m.nzs = nslices;
+    m.owned = true;
+    g.gmm = m;
+    return VR_OK;
+}
+
+int vr_gmm_info(vr_extent *dims, int *ncomp, int *z_base, int *nslices, const float **d_wm,
+                const float **d_sigma) {
+    if (!g.gmm.wm) return fail(VR_ERR_STATE, "no GMM volume resident");
+    if (dims) {
+        dims->width = (size_t)g.gmm.nx;
+        dims->height = (size_t)g.gmm.ny;
+        dims->depth = (size_t)g.gmm.nz;
+    }
+    if (ncomp) *ncomp = g.gmm.K;
+    if (z_base) *z_base = g.gmm.z_base;
+    if (nslices) *nslices = g.gmm.nzs;
+    if (d_wm) *d_wm = g.gmm.wm;
+    if (d_sigma) *d_sigma = g.gmm.sg;
+    return VR_OK;
+}
+
+int vr_free_gmm(void) {
+    release_gmm();
+    return VR_OK;
+}
+
+int vr_render_gmm(const vr_render_desc *desc, const vr_gmm_slab *slab) {
+    vr::Params P;
+    uint32_t nblocks = 0;
+    int rc = fill_gmm_params(desc, slab, P, nblocks);
+    if (rc != VR_OK) return rc;
+    hipError_t e = vr::launch_march_gmm(g.gmm.K, desc->query_method, P, nblocks, false, g.stream);
+    if (e != hipSuccess) return hip_fail(e, "launch(k_march_gmm)");
+    return VR_OK;
+}
+
+int64_t vr_gmm_count_footprint(const vr_render_desc *desc) {
+    vr::Params P;
+    uint32_t nblocks = 0;
+    int rc = fill_gmm_params(desc, nullptr, P, nblocks);
+    if (rc != VR_OK) return rc;
+    const uint64_t nvox = (uint64_t)g.gmm.nx * g.gmm.ny * g.gmm.nz;
+    const uint64_t nwords = (nvox + 63) / 64;
+    unsigned long long *bits = nullptr;
+    VR_HIP(hipMalloc(&bits, nwords * 8 + 8));
+    unsigned long long *total = bits + nwords;
+    hipError_t e = hipMemsetAsync(bits, 0, nwords * 8 + 8, g.stream);
+    P.mark = bits;
+    P.out = nullptr;  // count launch writes no pixels
+    P.out_f = nullptr;
+    P.out_n = nullptr;
+    if (e == hipSuccess) e = vr::launch_march_gmm(g.gmm.K, desc->query_method, P, nblocks, true, g.stream);
+    if (e == hipSuccess) e = vr::launch_popcount(bits, nwords, total, g.stream);
+    unsigned long long u = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&u, total, 8, hipMemcpyDeviceToHost, g.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+    (void)hipFree(bits);
+    if (e != hipSuccess) return hip_fail(e, "vr_gmm_count_footprint");
+    return (int64_t)u;
+}
+
 // ---------------- reference entry points (K:1889-2406) ------------------
 
 void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output, uint32_t imageW,
@@ -1197,6 +1454,7 @@ void freeCudaBuffers(void) {
     release_volume();
     release_codec();
     release_flex();
+    release_gmm();
 }
 
 void setTextureFilterMode(bool bLinearFilter) { g.linear_filter = bLinearFilter; }

@@ -62,6 +62,18 @@ struct Params {
     // adaptive tile order: per-tile cost record of the pipelined march
     // (record_tile_cost), indexed by tile id, nullptr = off
     uint32_t *tile_cost;
+    // GMM volumes (vr_gmm.hip): K components per voxel in
+    // two planes, (w, mu) pairs [voxel][K][2] and sigma [voxel][K], voxel
+    // order x + nx*(y + ny*(z - z_base)) for the resident slices
+    // [z_base, z_base + nzs); nx/ny/nz above are the whole volume's dims.
+    const float *gwm, *gsg;
+    int gk;
+    int z_base, nzs;
+    int z_lo, z_hi;              // slab: samples whose footprint z0 lies in [z_lo, z_hi)
+    const uint4 *rays_in;        // slab chain: alive rays entering (GmmRay), nullptr = camera
+    uint32_t n_rays_in;
+    uint4 *rays_out;             // alive rays leaving the slab (nullptr: slab = whole volume)
+    uint32_t *n_rays_out;
 };
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)

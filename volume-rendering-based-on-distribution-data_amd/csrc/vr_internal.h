@@ -75,6 +75,11 @@ hipError_t launch_flex_corners(const FlexTables &t, int block, int nblk, float *
 hipError_t launch_flex_blocks(int nb, int nblk, const float *corner_hist, float4 *blocks,
                               hipStream_t s);
 hipError_t launch_march_flex(int method, const Params &P, uint32_t nslots, hipStream_t s);
+// ---- GMM volumes (config 5, vr_gmm.hip) ----
+hipError_t launch_march_gmm(int K, int method, const Params &P, uint32_t nblocks, bool count,
+                            hipStream_t s);
+hipError_t launch_synth_gmm(float *wm, float *sg, const SynthArgs &a, int K, int z_base, int nzs,
+                            hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,

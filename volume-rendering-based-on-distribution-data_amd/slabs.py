@@ -1,0 +1,97 @@
+"""Slab-chained GMM rendering: host logic of BASELINE config 5.
+
+A 2048^3 x 16-component GMM volume is 1.65 TB: it cannot be replicated per
+GPU (288 GB HBM), but split into z-slabs it is resident across 8 GPUs (one
+slab of 256 slices + 1 halo slice, 207 GB, per rank).  Every ray crosses the
+slabs in one order (its z step has the sign of the view's; vr_render_gmm
+rejects views whose rays step both ways), so the march is a chain: slab 0
+marches the camera rays and hands every ray that leaves it alive -- its exact
+state: colour sums, t, position, samples taken -- to slab 1, and so on.  The
+chain reproduces the whole-volume march bit for bit (same float operations in
+the same order); a ray's pixel is written by the slab where it ends, and the
+ranks' frames (zero elsewhere) add up to the frame.
+
+This module has no device code: partitions, the march order and the
+alive-list exchange over torch.distributed (RCCL send/recv on GPUs, gloo in
+the CPU tests).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+RAY_WORDS = 12  # alive-list entry: 48 bytes (float sum[4], t, pos[3]; u32 pixel, samples, 0, 0)
+
+
+def march_direction(inv_view, width: int, height: int) -> int:
+    """+1 if every ray of the frame steps towards +z, -1 towards -z, 0 if both
+    occur.  A ray's z step has the sign of u M8 + v M9 - 2 M10 (K:288-296), a
+    linear form of (u, v), so the frame's four corner pixels decide."""
+    M = np.asarray(inv_view, dtype=np.float32).reshape(12)
+    pos = neg = 0
+    for c in range(4):
+        u = np.float32(np.float32((width - 1) / width) * 2 - 1) if c & 1 else np.float32(-1)
+        v = np.float32(np.float32((height - 1) / height) * 2 - 1) if c & 2 else np.float32(-1)
+        dz = np.float32(u * M[8] + v * M[9]) - np.float32(2) * M[10]
+        pos += dz > 0
+        neg += dz < 0
+    if pos and neg:
+        return 0
+    return -1 if neg else 1
+
+
+def slab_bounds(nz: int, n: int, direction: int) -> List[Tuple[int, int]]:
+    """n z-ranges [z_lo, z_hi) covering [0, nz), listed in march order (the
+    i-th is crossed i-th by every ray).  Equal splits (+-1 slice)."""
+    if n < 1 or n > nz:
+        raise ValueError(f"cannot split {nz} slices into {n} slabs")
+    if direction == 0:
+        raise ValueError("rays of this view cross z-slabs in both directions")
+    edges = [(i * nz) // n for i in range(n + 1)]
+    b = [(edges[i], edges[i + 1]) for i in range(n)]
+    return b if direction > 0 else b[::-1]
+
+
+def resident_slices(z_lo: int, z_hi: int, nz: int) -> Tuple[int, int]:
+    """(z_base, nslices) a slab must hold: footprints starting in [z_lo, z_hi)
+    read slices z0 and min(z0 + 1, nz - 1), i.e. one halo slice past z_hi."""
+    return z_lo, min(z_hi + 1, nz) - z_lo
+
+
+def send_alive(rays, count: int, dst: int, dist) -> None:
+    """Send an alive list (first `count` rows of an (n, 12) int32 tensor) to rank
+    dst: the count first, then the rows (RCCL point-to-point over xGMI on GPUs)."""
+    import torch
+    c = torch.tensor([count], dtype=torch.int64, device=rays.device)
+    dist.send(c, dst)
+    if count:
+        dist.send(rays[:count].contiguous(), dst)
+
+
+def recv_alive(src: int, out, dist) -> int:
+    """Receive an alive list from rank src into out ((cap, 12) int32 tensor);
+    returns its length."""
+    import torch
+    c = torch.zeros(1, dtype=torch.int64, device=out.device)
+    dist.recv(c, src)
+    n = int(c.item())
+    if n > out.shape[0]:
+        raise RuntimeError(f"alive list of {n} rays exceeds the buffer ({out.shape[0]})")
+    if n:
+        buf = out[:n]
+        dist.recv(buf, src)
+    return n
+
+
+def chain_frame(rank: int, world: int, render_slab, rays_in, n_in: Optional[int], dist):
+    """One frame of the slab chain on this rank: receive the previous slab's
+    alive list (rank > 0), march this slab (render_slab(rays_in, n_in) ->
+    (rays_out, n_out)), pass the alive list on (rank < world - 1).  Returns the
+    number of rays this slab handed on."""
+    if rank > 0:
+        n_in = recv_alive(rank - 1, rays_in, dist)
+    rays_out, n_out = render_slab(rays_in if rank > 0 else None, n_in if rank > 0 else 0)
+    if rank < world - 1:
+        send_alive(rays_out, n_out, rank + 1, dist)
+    return n_out
