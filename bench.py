@@ -34,6 +34,13 @@ CONFIGS = {
     "512x8": (512, 8, 1920, 1080),
     "1024x8": (1024, 8, 1920, 1080),
 }
+# GMM volumes: name -> (volume edge, components, W, H)
+GMM_CONFIGS = {
+    "gmm96": (96, 16, 256, 256),       # tests
+    "gmm1024": (1024, 16, 1920, 1080),  # in-core on one GPU (206 GB)
+    "gmm2048": (2048, 16, 3840, 2160),  # BASELINE config 5: z-slabs over 8 GPUs (207 GB each)
+}
+GMM_CPU_EDGE = 512  # CPU-baseline volume edge (a 1024^3 GMM exceeds the box's host-memory cap)
 SEED = 20261015
 CODEC_TEMPLATES, CODEC_SLOTS = 64, 4  # synthetic codec volume (methods 4/5/6)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
@@ -44,7 +51,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="1024x8", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="1024x8", choices=sorted(CONFIGS) + sorted(GMM_CONFIGS))
     ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 4, 5, 6, 7])
     ap.add_argument("--camera", default="C0", choices=["C0", "C1"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -127,8 +134,197 @@ def balanced_lists(pkg, lists, world, rank, W, H, m, method, dev, stream, backen
     return pkg.tiles.tile_lists_by_cost(W, H, world, cost.cpu().numpy())
 
 
+def gmm_cpu_baseline(m, method, W, H, K):
+    """The CPU oracle's GMM march (C) on this host's cores: a band of rows of the
+    same frame, on a GMM_CPU_EDGE^3 volume held in host RAM."""
+    import __graft_entry__ as graft
+    orc = graft.load_oracle()
+    n = GMM_CPU_EDGE
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    wm, sg = orc.synth_gmm(n, n, n, K, SEED, nthreads=threads)
+    rows = (H // 2 - 24, H // 2 + 24)  # the centre band: the longest rays
+    p = orc.make_params(W, H, m, query_method=method)
+    frames, rays, dt = 0, 0, 0.0
+    while frames == 0 or dt * threads < 24.0 and frames < 8:
+        t0 = time.perf_counter()
+        orc.render_gmm_rows(wm, sg, (n, n, n), p, rows[0], rows[1], nthreads=threads)
+        dt += time.perf_counter() - t0
+        rays += (rows[1] - rows[0]) * W
+        frames += 1
+    return {
+        "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+        "sample": (f"oracle/vr_oracle.c GMM march (-O3, OpenMP) on the {rows[1] - rows[0]} centre rows of the "
+                   f"{W}x{H} frame, {frames} pass(es) ({rays} rays, {dt:.2f} s on {threads} "
+                   f"threads), {n}^3 x {K} GMM volume in host RAM (the GPU workload's "
+                   f"volume is larger than the box's host-memory cap)"),
+    }
+
+
+def main_gmm(args):
+    """GMM volumes.  N = 1: the whole volume resident, one
+    launch per frame.  N > 1: rank r holds z-slab r (in the view's march order)
+    and the frame is a chain: receive the previous slab's alive rays, march,
+    send the survivors on (RCCL point-to-point over xGMI), then the ranks'
+    frames are summed on rank 0.  Ranks run ahead frame by frame (a pipeline,
+    one frame in flight per rank)."""
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as graft
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks need {world} GPUs, {ndev} visible")
+    dev = torch.device("cuda", local_rank % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    pkg = graft.load_package()
+    n, K, W, H = GMM_CONFIGS[args.config]
+    if args.method not in (1, 2):
+        raise SystemExit("GMM volumes support --method 1 (mean) and 2 (variance)")
+    m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
+         else pkg.camera.display_inv_view((30.0, 45.0)))
+    rec_bytes = 8 * K if args.method == 1 else 12 * K
+    free, _ = torch.cuda.mem_get_info(dev)
+    stream = torch.cuda.Stream(device=dev)
+    pkg.set_stream(stream)
+    if world == 1:
+        need = n ** 3 * 12 * K
+        if need > free * 0.95:
+            raise SystemExit(f"{args.config}: {need / 1e9:.0f} GB of GMM records exceed this GPU's "
+                             f"{free / 1e9:.0f} GB; run it on >= {int(need / (free * 0.9)) + 1} "
+                             "GPUs (z-slabs) or simulate the ranks with tools/gmm_slab_sim.py")
+        pkg.synthesize_gmm((n, n, n), K, SEED)
+        z_lo, z_hi = 0, n
+    else:
+        direction = pkg.slabs.march_direction(m, W, H)
+        z_lo, z_hi = pkg.slabs.slab_bounds(n, world, direction)[rank]
+        zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
+        pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
+    frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    desc = pkg.make_desc(frame, W, H, m, query_method=args.method, volume_size=(1, 1, 1))
+    if world > 1:
+        rays_in = torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device=dev)
+        rays_out = torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ev, alive = [], []
+
+    def step(timed):
+        with torch.cuda.stream(stream):
+            frame.zero_()  # C:208
+            n_in = 0
+            if world > 1:
+                cnt.zero_()
+                if rank > 0:
+                    n_in = pkg.slabs.recv_alive(rank - 1, rays_in, dist)
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            if world == 1:
+                pkg.render_gmm(desc)
+            else:
+                pkg.render_gmm(desc, pkg.gmm_slab(z_lo, z_hi, rays_out, cnt,
+                                                  d_rays_in=rays_in if rank > 0 else None,
+                                                  n_rays_in=n_in))
+            if timed:
+                e1.record(stream)
+                ev.append((e0, e1))
+            if world > 1:
+                n_out = int(cnt.item())
+                if timed:
+                    alive.append(n_out)
+                if rank < world - 1:
+                    pkg.slabs.send_alive(rays_out, n_out, rank + 1, dist)
+                pkg.slabs.reduce_frame(frame, dist)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if args.dump_frame and rank == 0:
+        np.save(args.dump_frame, frame.cpu().numpy().view(np.uint32).reshape(H, W))
+    kernel = pkg.last_kernel()
+    u = pkg.gmm_count_footprint(desc) if world == 1 else None
+    alg_bytes = u * rec_bytes + W * H * 4 if u is not None else None
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
+    ms_per_step = elapsed / args.steps * 1e3
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = gmm_cpu_baseline(m, args.method, W, H, K)
+        out = {
+            "metric": f"Mrays/s + fps at {n}^3 x {K}-component GMM volume, {W}x{H}; % HBM roofline",
+            "value": round(W * H / (elapsed / args.steps) / 1e6, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "fps": round(1e3 / ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic seeded GMM volume (seed {SEED}, DESIGN.md s11.1)",
+            "config": {
+                "workload": f"{n}^3 x {K}-component GMM volume, {W}x{H}, camera {args.camera}, "
+                            f"queryMethod {args.method}",
+                "volume": [n, n, n], "components": K, "image": [W, H], "camera": args.camera,
+                "query_method": args.method, "density": 0.05,
+                "parallelism": ("whole volume x1" if world == 1 else
+                                f"z-slabs x{world} + " + ("RCCL send/recv of alive rays + reduce"
+                                                          if args.dist_backend == "nccl"
+                                                          else "gloo host staging")),
+                "slab": [z_lo, z_hi],
+                "alive_rays_out_rank0": int(np.mean(alive)) if alive else None,
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": None,
+                "kernel": kernel,
+                "kernel_ms": round(kern_ms, 4),
+                "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
+                "U_records": int(u) if u is not None else None,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
 def main():
     args = parse()
+    if args.config in GMM_CONFIGS:
+        return main_gmm(args)
     import torch
     import torch.distributed as dist
     import __graft_entry__ as graft

@@ -84,6 +84,9 @@ def lib():
                                      ctypes.c_uint32, ctypes.c_void_p, u32p, u32p, fp, i32p,
                                      ctypes.c_void_p]
         L.orc_render_gmm.restype = ctypes.c_int64
+        L.orc_render_gmm_rows.argtypes = [ctypes.POINTER(Gmm), ctypes.POINTER(RenderParams),
+                                          ctypes.c_int, ctypes.c_int, u32p, ctypes.c_int]
+        L.orc_render_gmm_rows.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -470,3 +473,14 @@ def render_gmm(wm, sg, dims, params, z_base=0, slab=None, rays_in=None, want_mar
     if mark is not None:
         res["U"] = int(np.unpackbits(mark.view(np.uint8)).sum())
     return res
+
+
+def render_gmm_rows(wm, sg, dims, params, row_lo, row_hi, nthreads=0):
+    """CPU-baseline GMM render of rows [row_lo, row_hi) (OpenMP); returns
+    (out (H, W) uint32, samples)"""
+    nx, ny, nz = (int(v) for v in dims)
+    g = Gmm(_fp(wm), _fp(sg), nx, ny, nz, int(sg.shape[-1]), 0, int(sg.shape[0]))
+    out = np.zeros((params.height, params.width), np.uint32)
+    s = lib().orc_render_gmm_rows(ctypes.byref(g), ctypes.byref(params), int(row_lo), int(row_hi),
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), nthreads)
+    return out, int(s)

@@ -1127,3 +1127,35 @@ int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, i
     if (n_out) *n_out = k_out;
     return samples;
 }
+
+int64_t orc_render_gmm_rows(const orc_gmm *v, const orc_render_params *p, int row_lo, int row_hi,
+                            uint32_t *out, int nthreads) {
+    int64_t acc = 0;
+    if (row_lo < 0) row_lo = 0;
+    if (row_hi > p->height) row_hi = p->height;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(+ : acc)
+#endif
+    for (int y = row_lo; y < row_hi; y++) {
+        for (int x = 0; x < p->width; x++) {
+            f3 o, d;
+            float tnear, tfar;
+            if (!gmm_ray(p, x, y, &o, &d, &tnear, &tfar)) continue;
+            orc_gmm_ray s;
+            memset(&s, 0, sizeof s);
+            s.pix = (uint32_t)y * (uint32_t)p->width + (uint32_t)x;
+            s.t = tnear;
+            s.pos[0] = o.x + d.x * tnear;
+            s.pos[1] = o.y + d.y * tnear;
+            s.pos[2] = o.z + d.z * tnear;
+            gmm_march(v, p, 0, v->nz, 0, d, tfar, &s, NULL);
+            acc += s.n;
+            const float rgba[4] = {s.sum[0] * p->brightness, s.sum[1] * p->brightness,
+                                   s.sum[2] * p->brightness, s.sum[3] * p->brightness};
+            if (out) out[s.pix] = orc_pack(rgba);
+        }
+    }
+    (void)nthreads;
+    return acc;
+}

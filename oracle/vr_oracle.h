@@ -169,6 +169,11 @@ int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, i
                        uint32_t *n_out, uint32_t *out, float *out_f, int32_t *out_n,
                        uint64_t *mark);
 
+/* CPU baseline: camera rays of rows [row_lo, row_hi), whole resident volume,
+ * OpenMP over rows; returns the samples taken */
+int64_t orc_render_gmm_rows(const orc_gmm *v, const orc_render_params *p, int row_lo, int row_hi,
+                            uint32_t *out, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

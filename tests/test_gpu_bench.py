@@ -43,3 +43,22 @@ def test_bench_single_and_two_rank_frames_agree(gpu, tmp_path):
     a, b = np.load(f1), np.load(f2)
     assert a.shape == (512, 512) and np.count_nonzero(a) > 0
     assert np.array_equal(a, b), f"{int(np.sum(a != b))} pixels differ between N=1 and N=2"
+
+
+def test_bench_gmm_single_and_two_slab_frames_agree(gpu, tmp_path):
+    """GMM mode: the whole-volume frame (N = 1) equals the 2-rank z-slab chain's
+    (alive rays handed rank to rank, frames summed on rank 0; gloo staging)"""
+    args = ["--config", "gmm96", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    f1 = str(tmp_path / "g1.npy")
+    out1 = _run([sys.executable, "bench.py", *args, "--dump-frame", f1], tmp_path)
+    assert out1["n_gpus"] == 1 and out1["value"] > 0
+    assert out1["roofline"]["kernel"].startswith("k_march_gmm") and 0 < out1["roofline"]["frac"] < 1
+    f2 = str(tmp_path / "g2.npy")
+    out2 = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                 "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", "29534",
+                 "bench.py", "--gpus", "2", *args, "--dist-backend", "gloo",
+                 "--dump-frame", f2], tmp_path)
+    assert out2["n_gpus"] == 2 and out2["config"]["parallelism"].startswith("z-slabs x2")
+    a, b = np.load(f1), np.load(f2)
+    assert a.shape == (256, 256) and np.count_nonzero(a) > 0
+    assert np.array_equal(a, b), f"{int(np.sum(a != b))} pixels differ between N=1 and N=2"

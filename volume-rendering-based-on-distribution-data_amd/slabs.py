@@ -59,29 +59,54 @@ def resident_slices(z_lo: int, z_hi: int, nz: int) -> Tuple[int, int]:
     return z_lo, min(z_hi + 1, nz) - z_lo
 
 
+def _staged(dist) -> bool:
+    """gloo carries only host tensors: device buffers are staged through host
+    memory (multi-rank rehearsal on one GPU; never for measurement)"""
+    return dist.get_backend() == "gloo"
+
+
 def send_alive(rays, count: int, dst: int, dist) -> None:
     """Send an alive list (first `count` rows of an (n, 12) int32 tensor) to rank
     dst: the count first, then the rows (RCCL point-to-point over xGMI on GPUs)."""
     import torch
-    c = torch.tensor([count], dtype=torch.int64, device=rays.device)
+    dev = "cpu" if _staged(dist) else rays.device
+    c = torch.tensor([count], dtype=torch.int64, device=dev)
     dist.send(c, dst)
     if count:
-        dist.send(rays[:count].contiguous(), dst)
+        dist.send(rays[:count].contiguous().to(dev), dst)
 
 
 def recv_alive(src: int, out, dist) -> int:
     """Receive an alive list from rank src into out ((cap, 12) int32 tensor);
     returns its length."""
     import torch
-    c = torch.zeros(1, dtype=torch.int64, device=out.device)
+    dev = "cpu" if _staged(dist) else out.device
+    c = torch.zeros(1, dtype=torch.int64, device=dev)
     dist.recv(c, src)
     n = int(c.item())
     if n > out.shape[0]:
         raise RuntimeError(f"alive list of {n} rays exceeds the buffer ({out.shape[0]})")
     if n:
-        buf = out[:n]
-        dist.recv(buf, src)
+        if dev == "cpu" and out.is_cuda:
+            buf = torch.empty((n, out.shape[1]), dtype=out.dtype)
+            dist.recv(buf, src)
+            out[:n].copy_(buf)
+        else:
+            buf = out[:n]
+            dist.recv(buf, src)
     return n
+
+
+def reduce_frame(frame, dist) -> None:
+    """Sum the ranks' frames on rank 0: each pixel was written by the one slab
+    where its ray ended (or by none: a miss), every other rank holds 0 there."""
+    if _staged(dist) and frame.is_cuda:
+        h = frame.cpu()
+        dist.reduce(h, 0, op=dist.ReduceOp.SUM)
+        if dist.get_rank() == 0:
+            frame.copy_(h)
+    else:
+        dist.reduce(frame, 0, op=dist.ReduceOp.SUM)
 
 
 def chain_frame(rank: int, world: int, render_slab, rays_in, n_in: Optional[int], dist):
