@@ -360,8 +360,8 @@ __device__ __forceinline__ void codec_decode(const Params &P, uint64_t vidx, flo
 // bin centre is used in both mean and variance
 template <int B, int C>
 __device__ __forceinline__ float codec_stat_of(const float (&dec)[B], float enorm) {
-    if constexpr (C == 0) {
-        return (float)div_const((double)raw_mean<B>(dec), kMeanD, kMeanR);
+    if constexpr (C == 0) {  // K:857, the same (float)((double)mean / 0.0217) as K:758
+        return div_to_float(raw_mean<B>(dec), kMeanR);
     } else if constexpr (C == 1) {
         const float mean = raw_mean<B>(dec);
         const float bw = bin_width(B);
@@ -432,7 +432,13 @@ __device__ __forceinline__ void load_rec(const float *__restrict__ vol, uint64_t
     if constexpr (B % 4 == 0) {
 #pragma unroll
         for (int i = 0; i < B / 4; i++) {
+#ifdef VR_NT_LOADS  // A/B builds only: non-temporal record loads
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v qv = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(src + 4 * i));
+            const float4 q = make_float4(qv.x, qv.y, qv.z, qv.w);
+#else
             const float4 q = *reinterpret_cast<const float4 *>(src + 4 * i);
+#endif
             r[4 * i + 0] = q.x; r[4 * i + 1] = q.y; r[4 * i + 2] = q.z; r[4 * i + 3] = q.w;
         }
     } else if constexpr (B == 2) {

@@ -1179,20 +1179,71 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
 // for methods 1/2/3, each of the 8 corners is decoded from its codebook entry,
 // template and sparse errors at every step and blended with the quantised
 // weights.  One lane per ray.
-template <int B, int C, bool COUNT>
+//
+// Decode of one corner (codec_decode_pre's arithmetic, vr_device.h): the
+// template row -- from LDS when the table is staged there (TL), read with LDS
+// instructions rather than generic loads -- flipped and circularly shifted
+// (fractalDecoding, K:195-222); the NE sparse errors (K:805-823) are applied
+// through the thread's own LDS scratch column (bin i at scr[i * 256]: a lane's
+// dynamic bin index never conflicts with another lane's bank), one
+// read-add-clamp-write per error instead of a compare-and-select over every
+// bin; then renormalised (K:826-835).
+template <int B, bool TL>
+__device__ __forceinline__ void codec_decode_scr(const Params &P, const float *s_tpl, float *scr,
+                                                 const int4 c, const float4 (&pre)[2],
+                                                 const float2 *e, float (&dec)[B]) {
+    const uint32_t row = (uint32_t)c.x * B;
+#pragma unroll
+    for (int m = 0; m < B; m++) {
+        int i = m - c.y;                    // dec[(i + shift) mod B] = src[i]
+        if (i < 0) i += B;
+        const uint32_t k = row + (uint32_t)(c.z ? B - 1 - i : i);
+        dec[m] = TL ? s_tpl[k] : P.tpl[k];
+    }
+    if (c.w > 0) {
+#pragma unroll
+        for (int m = 0; m < B; m++) scr[m * 256] = dec[m];
+        for (int j = 0; j < c.w; j++) {
+            float2 ev;
+            if (j < kCodecPre) {
+                const float4 h = pre[j >> 1];
+                ev = (j & 1) ? make_float2(h.z, h.w) : make_float2(h.x, h.y);
+            } else {
+                ev = e[j];
+            }
+            const int idx = (int)ev.x;
+            if (idx >= 0 && idx < B) {      // bin ids outside [0, B) skipped
+                float v = scr[idx * 256] + ev.y;
+                if (v < 0) v = 0;
+                scr[idx * 256] = v;
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < B; m++) dec[m] = scr[m * 256];
+    }
+    float total = 0.0f;
+#pragma unroll
+    for (int i = 0; i < B; i++) total = total + dec[i];
+    if (total > 0) {
+#pragma unroll
+        for (int i = 0; i < B; i++) dec[i] = dec[i] / total;
+    }
+}
+
+template <int B, int C, bool COUNT, bool TL>
 __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ unused, Params P) {
     (void)unused;
-    extern __shared__ __attribute__((aligned(16))) float s_tpl[];
+    extern __shared__ __attribute__((aligned(16))) float s_lds[];
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // whole workgroup
-    const float *tpl = P.tpl;
-    if (P.tpl_lds) {  // small template tables live in LDS: no gathers for them
+    if constexpr (TL) {  // small template tables live in LDS: no gathers for them
         const uint32_t n = (uint32_t)P.tpl_lds / 4;
-        for (uint32_t i = threadIdx.x; i < n; i += 256) s_tpl[i] = P.tpl[i];
+        for (uint32_t i = threadIdx.x; i < n; i += 256) s_lds[i] = P.tpl[i];
         __syncthreads();
-        tpl = s_tpl;
     }
+    // this thread's error scratch column, after the (16-byte aligned) template table
+    float *scr = s_lds + (TL ? ((uint32_t)P.tpl_lds / 4 + 3u) & ~3u : 0u) + threadIdx.x;
     uint32_t lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
@@ -1209,6 +1260,9 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
     float t = r.tnear;
     float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
     const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    // the first kCodecPre error pairs of a voxel are gathered with its codebook
+    // entry as two 16-byte loads when the per-voxel block allows (even slot count)
+    const bool pre16 = P.err_slots >= kCodecPre && (P.err_slots & 1) == 0;
     const int npre = P.err_slots < kCodecPre ? P.err_slots : kCodecPre;
     int n = 0;
     for (int i = 0; i < kMaxSteps; i++) {
@@ -1222,21 +1276,29 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
                                r01 + f.x0, r01 + f.x1, r11 + f.x0, r11 + f.x1};
         // all 8 codebook entries and their first error pairs in one batch
         int4 c[8];
-        float2 pre[8][kCodecPre];
+        float4 pre[8][2];
 #pragma unroll
         for (int j = 0; j < 8; j++) c[j] = P.cb[v[j]];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const float2 *e = P.err + v[j] * (uint64_t)P.err_slots;
+            if (pre16) {
+                pre[j][0] = reinterpret_cast<const float4 *>(e)[0];
+                pre[j][1] = reinterpret_cast<const float4 *>(e)[1];
+            } else {
+                float2 q[kCodecPre];
 #pragma unroll
-            for (int k = 0; k < kCodecPre; k++)
-                pre[j][k] = k < npre ? e[k] : make_float2(0.f, 0.f);
+                for (int k = 0; k < kCodecPre; k++) q[k] = k < npre ? e[k] : make_float2(0.f, 0.f);
+                pre[j][0] = make_float4(q[0].x, q[0].y, q[1].x, q[1].y);
+                pre[j][1] = make_float4(q[2].x, q[2].y, q[3].x, q[3].y);
+            }
         }
         float sv[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             float dec[B];
-            codec_decode_pre<B>(tpl, c[j], pre[j], P.err + v[j] * (uint64_t)P.err_slots, dec);
+            codec_decode_scr<B, TL>(P, s_lds, scr, c[j], pre[j],
+                                    P.err + v[j] * (uint64_t)P.err_slots, dec);
             sv[j] = codec_stat_of<B, C>(dec, P.enorm);
         }
         n = i + 1;
@@ -1255,12 +1317,18 @@ template <int B, bool COUNT>
 static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream_t s) {
     const dim3 grid(nslots), block(256);
     if (!COUNT) note_kernel("k_march_codec", B, method);
-    // template table (if staged) at the front of the request; VR_WG_PER_CU caps
-    const size_t lds = cap_lds(P, P.wg_per_cu, (size_t)P.tpl_lds);
-    switch (method) {
-    case 4: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT>), grid, block, lds, s, nullptr, P); break;
-    case 5: hipLaunchKernelGGL((k_march_codec<B, 1, COUNT>), grid, block, lds, s, nullptr, P); break;
-    case 6: hipLaunchKernelGGL((k_march_codec<B, 2, COUNT>), grid, block, lds, s, nullptr, P); break;
+    // template table (if staged) at the front of the request, then the error
+    // scratch (B floats per thread); VR_WG_PER_CU caps
+    const size_t need = (((size_t)P.tpl_lds + 15) & ~(size_t)15) + (size_t)B * 256u * 4u;
+    const size_t lds = cap_lds(P, P.wg_per_cu, need);
+    const bool tl = P.tpl_lds != 0;
+    switch (method * 2 + (tl ? 1 : 0)) {
+    case 8: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT, false>), grid, block, lds, s, nullptr, P); break;
+    case 9: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT, true>), grid, block, lds, s, nullptr, P); break;
+    case 10: hipLaunchKernelGGL((k_march_codec<B, 1, COUNT, false>), grid, block, lds, s, nullptr, P); break;
+    case 11: hipLaunchKernelGGL((k_march_codec<B, 1, COUNT, true>), grid, block, lds, s, nullptr, P); break;
+    case 12: hipLaunchKernelGGL((k_march_codec<B, 2, COUNT, false>), grid, block, lds, s, nullptr, P); break;
+    case 13: hipLaunchKernelGGL((k_march_codec<B, 2, COUNT, true>), grid, block, lds, s, nullptr, P); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
