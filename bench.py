@@ -215,6 +215,7 @@ def main_gmm(args):
         cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     ev, alive = [], []
+    balanced = False
 
     def step(timed):
         with torch.cuda.stream(stream):
@@ -244,6 +245,35 @@ def main_gmm(args):
                     pkg.slabs.send_alive(rays_out, n_out, rank + 1, dist)
                 pkg.slabs.reduce_frame(frame, dist)
 
+    if world > 1 and not args.no_balance:
+        # Cost-balanced slabs (untimed, once per view): early ray termination
+        # front-loads the work, so one frame on equal slabs measures every rank's
+        # march, and all ranks re-cut the slabs by those costs (largest slab cost
+        # minimised, each slab within the smallest rank's free HBM), then
+        # generate their new slab (slabs.bounds_by_cost).
+        step(True)
+        torch.cuda.synchronize()
+        ms = ev[-1][0].elapsed_time(ev[-1][1])
+        ev.clear()
+        alive.clear()
+        pkg.free_gmm()
+        free_now, _ = torch.cuda.mem_get_info(dev)
+        cdev = dev if args.dist_backend == "nccl" else "cpu"
+        costs = torch.zeros(world, dtype=torch.float64, device=cdev)
+        costs[rank] = ms
+        dist.all_reduce(costs)
+        cap = torch.tensor([pkg.slabs.max_slices_for(n, n, K, free_now)], dtype=torch.int64,
+                           device=cdev)
+        dist.all_reduce(cap, op=dist.ReduceOp.MIN)
+        direction = pkg.slabs.march_direction(m, W, H)
+        bounds = pkg.slabs.bounds_by_cost(n, world, direction,
+                                          pkg.slabs.slab_bounds(n, world, direction),
+                                          costs.cpu().tolist(), int(cap.item()))
+        z_lo, z_hi = bounds[rank]
+        zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
+        pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
+        torch.cuda.synchronize()
+        balanced = True
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
@@ -300,6 +330,8 @@ def main_gmm(args):
                                                           if args.dist_backend == "nccl"
                                                           else "gloo host staging")),
                 "slab": [z_lo, z_hi],
+                "slab_cut": (None if world == 1 else "measured cost (one untimed frame)"
+                             if balanced else "equal"),
                 "alive_rays_out_rank0": int(np.mean(alive)) if alive else None,
             },
             "roofline": {

@@ -235,3 +235,25 @@ def test_gloo_slab_chain_matches_whole_volume(orc, pkg):
     m = pkg.camera.display_inv_view((30.0, 45.0))
     full = orc.render_gmm(wm, sg, dims, orc.make_params(48, 40, m, query_method=1, density=0.3))
     assert np.array_equal(got, full["out"])
+
+
+def test_bounds_by_cost(pkg):
+    S = pkg.slabs
+    # front-loaded costs (the measured config-5 chain): the largest slab cost drops
+    b = S.slab_bounds(2048, 8, -1)
+    c = [6.12, 6.56, 3.90, 1.25, 0.48, 0.08, 0.006, 0.004]
+    cap = S.max_slices_for(2048, 2048, 16, 288e9)
+    nb = S.bounds_by_cost(2048, 8, -1, b, c, cap)
+    assert len(nb) == 8 and nb[0][1] == 2048 and nb[-1][0] == 0
+    assert all(nb[i][0] == nb[i + 1][1] for i in range(7))       # contiguous, march order
+    assert all(0 < hi - lo <= cap for lo, hi in nb)
+
+    def cost(lo, hi):  # the uniform-density model the cut assumes
+        return sum(cc * (min(hi, h) - max(lo, l)) / (h - l)
+                   for (l, h), cc in zip(b, c) if min(hi, h) > max(lo, l))
+    assert max(cost(lo, hi) for lo, hi in nb) < 0.65 * max(c)
+    # uniform costs keep (nearly) equal slabs; ascending march order too
+    nb = S.bounds_by_cost(100, 4, 1, S.slab_bounds(100, 4, 1), [1, 1, 1, 1])
+    assert [hi - lo for lo, hi in nb] == [25, 25, 25, 25]
+    with pytest.raises(ValueError):
+        S.bounds_by_cost(100, 2, 1, [(0, 50), (50, 100)], [1, 1], max_slices=40)

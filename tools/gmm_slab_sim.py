@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--balance", action="store_true",
+                    help="after the equal slabs, re-cut them by the measured per-slab cost "
+                         "(slabs.bounds_by_cost, capped at this GPU's HBM) and run again")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -38,11 +41,36 @@ def main():
     pkg.set_stream(s)
     n, K, W, H = a.dim, a.K, a.W, a.H
     m = pkg.camera.single_test_inv_view() if a.camera == "C0" else pkg.camera.display_inv_view()
-    bounds = pkg.slabs.slab_bounds(n, a.slabs, pkg.slabs.march_direction(m, W, H))
+    direction = pkg.slabs.march_direction(m, W, H)
+    bounds = pkg.slabs.slab_bounds(n, a.slabs, direction)
     frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     desc = pkg.make_desc(frame, W, H, m, query_method=a.method, volume_size=(1, 1, 1))
     rays = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rows = run_chain(a, pkg, torch, np, s, bounds, n, K, W, H, desc, rays, cnt, frame, "equal")
+    if a.balance:
+        pkg.free_gmm()
+        free, _ = torch.cuda.mem_get_info()
+        cap = pkg.slabs.max_slices_for(n, n, K, free)
+        nb = pkg.slabs.bounds_by_cost(n, a.slabs, direction, bounds,
+                                      [r["kernel_ms"] for r in rows], cap)
+        print(json.dumps({"balanced_bounds": nb, "max_slices": cap}), flush=True)
+        frame.zero_()
+        run_chain(a, pkg, torch, np, s, nb, n, K, W, H, desc, rays, cnt, frame, "cost-balanced")
+    if a.check:
+        got = frame.clone()
+        pkg.synthesize_gmm((n, n, n), K, 20261015)
+        frame.zero_()
+        with torch.cuda.stream(s):
+            pkg.render_gmm(desc)
+        torch.cuda.synchronize()
+        same = torch.equal(got, frame)
+        print(json.dumps({"check_whole_volume_identical": bool(same)}), flush=True)
+        if not same:
+            sys.exit(1)
+
+
+def run_chain(a, pkg, torch, np, s, bounds, n, K, W, H, desc, rays, cnt, frame, label):
     n_in, rows = 0, []
     for i, (z_lo, z_hi) in enumerate(bounds):
         zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
@@ -62,7 +90,7 @@ def main():
                 e1.synchronize()
                 ms.append(e0.elapsed_time(e1))
         n_out = int(cnt.item())
-        r = {"slab": i, "z": [z_lo, z_hi], "resident_GB": round(n * n * ns * 12 * K / 1e9, 1),
+        r = {"slabs": label, "slab": i, "z": [z_lo, z_hi], "resident_GB": round(n * n * ns * 12 * K / 1e9, 1),
              "synth_s": round(t_syn, 2), "kernel_ms": round(float(np.median(ms)), 4),
              "kernel_ms_min": round(float(min(ms)), 4), "rays_in": n_in if i else W * H,
              "rays_out": n_out, "handoff_MB": round(n_out * 48 / 1e6, 1)}
@@ -72,22 +100,13 @@ def main():
     assert n_in == 0, "the last slab must end every ray"
     tot = sum(r["kernel_ms"] for r in rows)
     mx = max(r["kernel_ms"] for r in rows)
-    print(json.dumps({"summary": f"{n}^3 x {K} GMM, {W}x{H}, {a.camera} m{a.method}, {a.slabs} slabs",
+    print(json.dumps({"summary": f"{n}^3 x {K} GMM, {W}x{H}, {a.camera} m{a.method}, "
+                                 f"{a.slabs} {label} slabs",
                       "sum_kernel_ms": round(tot, 3), "max_kernel_ms": round(mx, 3),
                       "one_gpu_out_of_core_Mrays_s_excl_streaming": round(W * H / tot / 1e3, 1),
                       "pipelined_ranks_Mrays_s_upper": round(W * H / mx / 1e3, 1),
                       "max_handoff_MB": max(r["handoff_MB"] for r in rows)}), flush=True)
-    if a.check:
-        got = frame.clone()
-        pkg.synthesize_gmm((n, n, n), K, 20261015)
-        frame.zero_()
-        with torch.cuda.stream(s):
-            pkg.render_gmm(desc)
-        torch.cuda.synchronize()
-        same = torch.equal(got, frame)
-        print(json.dumps({"check_whole_volume_identical": bool(same)}), flush=True)
-        if not same:
-            sys.exit(1)
+    return rows
 
 
 if __name__ == "__main__":

@@ -53,6 +53,68 @@ def slab_bounds(nz: int, n: int, direction: int) -> List[Tuple[int, int]]:
     return b if direction > 0 else b[::-1]
 
 
+def bounds_by_cost(nz: int, n: int, direction: int, bounds, costs,
+                   max_slices: Optional[int] = None) -> List[Tuple[int, int]]:
+    """Re-cut n slabs so every rank gets about the same march time.
+
+    bounds/costs: a previous partition (march order) and its measured cost per
+    slab (kernel ms).  Early ray termination front-loads the work (the first
+    slabs a view's rays cross do most of the sampling), so equal slabs leave the
+    back ranks idle.  The cost density is taken as uniform inside each measured
+    slab; the cuts minimise the largest slab cost (bisection on it, greedy
+    fill) with no slab holding more than max_slices slices (the HBM cap: a
+    slab's records + halo must fit one GPU).  Returns n (z_lo, z_hi) ranges in
+    march order covering [0, nz)."""
+    if direction == 0:
+        raise ValueError("rays of this view cross z-slabs in both directions")
+    # per-slice cost in march order (slice index 0 = first crossed)
+    dens = np.zeros(nz, dtype=np.float64)
+    for (lo, hi), c in zip(bounds, costs):
+        for z in range(lo, hi):
+            k = z if direction > 0 else nz - 1 - z
+            dens[k] = max(float(c), 1e-9) / (hi - lo)
+    cap = nz if max_slices is None else int(max_slices)
+    if cap * n < nz:
+        raise ValueError(f"{n} slabs of at most {cap} slices cannot cover {nz} slices")
+    pre = np.concatenate([[0.0], np.cumsum(dens)])
+
+    def greedy(T):
+        """fewest cuts with every slab's cost <= T and <= cap slices (None: > n slabs)"""
+        cuts, start = [0], 0
+        while start < nz:
+            # furthest end with cost(start, end) <= T and end - start <= cap
+            end = int(np.searchsorted(pre, pre[start] + T * (1 + 1e-12), side="right")) - 1
+            end = min(max(end, start + 1), start + cap, nz)
+            cuts.append(end)
+            start = end
+            if len(cuts) - 1 > n:
+                return None
+        return cuts
+
+    lo, hi = float(dens.max()), float(pre[-1])
+    for _ in range(100):  # bisection on the largest slab cost
+        mid = (lo + hi) / 2
+        if greedy(mid) is None:
+            lo = mid
+        else:
+            hi = mid
+    cuts = greedy(hi)
+    while len(cuts) - 1 < n:  # fewer slabs needed: halve the thickest
+        i = max(range(len(cuts) - 1), key=lambda j: cuts[j + 1] - cuts[j])
+        cuts.insert(i + 1, (cuts[i] + cuts[i + 1]) // 2)
+    march = [(cuts[i], cuts[i + 1]) for i in range(n)]  # in march-order slice indices
+    if direction > 0:
+        return march
+    return [(nz - b, nz - a) for a, b in march]
+
+
+def max_slices_for(nx: int, ny: int, ncomp: int, hbm_bytes: float, reserve: float = 0.1) -> int:
+    """Largest slab (slices, excluding its halo slice) whose GMM records fit in
+    hbm_bytes with a `reserve` fraction left for frame and alive-list buffers."""
+    per_slice = nx * ny * 12 * ncomp
+    return int(hbm_bytes * (1 - reserve) // per_slice) - 1
+
+
 def resident_slices(z_lo: int, z_hi: int, nz: int) -> Tuple[int, int]:
     """(z_base, nslices) a slab must hold: footprints starting in [z_lo, z_hi)
     read slices z0 and min(z0 + 1, nz - 1), i.e. one halo slice past z_hi."""
