@@ -256,10 +256,11 @@ const char *vr_last_kernel(void);
  * bits).  d_buf must hold 12 * n_slots values.  nullptr turns it off. */
 int vr_debug_wave_clock(uint64_t *d_buf);
 
-/* Device self-test: compares the entropy decode's fast float logarithm with
- * (float)log((double)x) for every positive finite float (synchronous, about a
- * second).  counts[0] = mismatches (must be 0), counts[1] = inputs decided by
- * the double-log fallback. */
+/* Device self-test: compares the entropy decode's fast float logarithms (the
+ * series form and the table form, vr_device.h) with (float)log((double)x) for
+ * every positive finite float (synchronous, a few seconds).  counts[0] =
+ * mismatches of either (must be 0), counts[1] = inputs either form left to the
+ * double-log fallback (summed). */
 int vr_selftest_logf(uint64_t counts[2]);
 
 /* ---- the reference's input files ---- */

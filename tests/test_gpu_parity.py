@@ -383,13 +383,13 @@ def test_padded_layout(pkg, orc, gpu, monkeypatch):
 
 def test_fast_log_is_exact_for_every_float(pkg, gpu):
     """the entropy decode's logf_canon == (float)log((double)x) for all 2^31 - 2^23
-    positive finite floats (exhaustive, on the device)"""
+    positive finite floats, series and table forms (exhaustive, on the device)"""
     import ctypes
     L = pkg._lib.load()
     counts = (ctypes.c_uint64 * 2)()
     assert L.vr_selftest_logf(counts) == 0, L.vr_last_error()
     assert counts[0] == 0, f"{counts[0]} floats differ"
-    assert counts[1] < 1 << 16, f"{counts[1]} fallbacks"
+    assert counts[1] < 1 << 17, f"{counts[1]} fallbacks (both forms)"
 
 
 # ---- methods 4/5/6: fractal/template codec ----

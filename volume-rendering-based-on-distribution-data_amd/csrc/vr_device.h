@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "vr_logtab.h"
+
 // log(2.0), correctly rounded (K:766)
 #define VR_LN2_D 0x1.62e42fefa39efp-1
 
@@ -226,14 +228,55 @@ __device__ __forceinline__ float raw_variance(const float (&p)[B], float mean) {
 }
 
 // log of a float as the reference evaluates it, (float)log((double)x)
-// (DESIGN.md section 3), for finite x > 0, at a third of the double log's
-// cost.  A short atanh series in double gives y = log x to ~2^-50 relative;
-// unless y lies within 2^-44 of a float rounding midpoint, rounding y to
-// float already gives the rounding of the exact logarithm -- and so of the
-// double log -- and only the remaining ~2^-20 of inputs evaluate the double
-// log.  Exhaustively equal to (float)log((double)x) over all positive floats
-// (vr_selftest_logf, tests/test_gpu_parity.py).
-__device__ __forceinline__ bool logf_fast(float x, float &r) {
+// (DESIGN.md section 3), for finite x > 0.  y = log x is evaluated in double
+// to ~2^-52 relative; unless y lies within 2^-44 |y| of a float rounding
+// midpoint, rounding y to float already gives the rounding of the exact
+// logarithm -- and so of the double log -- and only the remaining ~2^-20 of
+// inputs evaluate the double log.  Exhaustively equal to (float)log((double)x)
+// over all positive floats (vr_selftest_logf, tests/test_gpu_parity.py).
+//
+// Reduction (vr_logtab.h, tools/gen_logtab.py): x = m 2^e, m in [1, 2) (exact
+// frexpf), c = 1 + i/64 the nearest of 65 centres, d = m - c exact (Sterbenz),
+// r = d / c in double (|r| <= 2^-7), log x = e ln2 + log c + log1p r with log c
+// and ln 2 as double-doubles and log1p r = r + r^2 (-1/2 + r/3 - ... + r^5/7)
+// (truncation < r^8/8, 2^-52 relative to r).  The two largest terms add
+// exactly where they cancel (x near 1: c = 1, log c = 0; x just below 1:
+// i = 64, e = -1, log c = ln 2 split like e ln 2).  No f64 division; the
+// midpoint test reads y's low 29 mantissa bits (a float's half-ulp pattern is
+// 1 << 28 there whatever y's binade), instead of float/ldexp arithmetic.
+__device__ __forceinline__ bool logf_fast_tab(float x, float &r) {
+    int e;
+    float m = frexpf(x, &e);                   // x = m 2^e, m in [0.5, 1), also subnormal x
+    m = m * 2.0f;                              // [1, 2), exact
+    e -= 1;
+    const int i = (int)((m - 1.0f) * 64.0f + 0.5f);   // 0 .. 64
+    const float c = i == 64 ? 2.0f : 1.0f + (float)i * 0x1p-6f;
+    const float d = m - c;                     // exact, |d| <= 1/128
+    const LogEnt t = kLogTab[i];
+    const double rr = (double)d * t.inv;
+    double q = 1.0 / 7.0;
+    q = fma(q, rr, -1.0 / 6.0);
+    q = fma(q, rr, 1.0 / 5.0);
+    q = fma(q, rr, -1.0 / 4.0);
+    q = fma(q, rr, 1.0 / 3.0);
+    q = fma(q, rr, -0.5);
+    const double p = fma(rr * rr, q, rr);      // log1p(rr)
+    const double de = (double)e;
+    const double a = fma(de, kLn2Hi, t.hi);    // e ln2_hi exact; exact where it cancels
+    const double b = fma(de, kLn2Lo, t.lo) + p;
+    const double y = a + b;
+    r = (float)y;
+    const uint64_t lo29 = (uint64_t)__double_as_longlong(y) & 0x1FFFFFFFull;
+    const uint64_t dist = lo29 > 0x10000000ull ? lo29 - 0x10000000ull : 0x10000000ull - lo29;
+    return dist > 512u;                        // > 2^-44 |y| from a midpoint
+}
+
+// The round-1 form: atanh series of (m - 1)/(m + 1), one f64 division, no
+// table.  Kept for the kernels where the table's memory loads sit on the
+// critical path: the wave-staged and quad entropy marches (methods 3) measured
+// slower with the table (1024^3 x 8: C0 4.96 -> 5.33 ms, C1 11.4 -> 12.1), the
+// codec entropy (method 6, 8 decodes per sample) faster (C0 23.6 -> 12.5).
+__device__ __forceinline__ bool logf_fast_series(float x, float &r) {
     int e;
     double m = frexp((double)x, &e);  // x = m 2^e, m in [0.5, 1)
     if (m < 0.70710678118654752440) {
@@ -263,22 +306,23 @@ __device__ __forceinline__ bool logf_fast(float x, float &r) {
     return fabs(fabs(d) - half) > 0x1p-44 * fabs(y);
 }
 
+template <bool TAB = false>
 __device__ __forceinline__ float logf_canon(float x) {
     float r;
     if (x == 1.0f) return 0.0f;
-    if (logf_fast(x, r)) return r;
+    if (TAB ? logf_fast_tab(x, r) : logf_fast_series(x, r)) return r;
     return (float)log((double)x);
 }
 
 // K:761-769
-template <int B>
+template <int B, bool TAB = false>
 __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
     float ent = 0.0f;
 #pragma unroll
     for (int i = 0; i < B; i++) {
         const float pr = p[i];
         const double t =
-            pr <= 0 ? 0.0 : div_const((double)logf_canon(pr), VR_LN2_D, kLn2R);
+            pr <= 0 ? 0.0 : div_const((double)logf_canon<TAB>(pr), VR_LN2_D, kLn2R);
         ent = (float)((double)ent + (double)pr * t);
     }
     ent = -ent;
@@ -374,7 +418,7 @@ __device__ __forceinline__ float codec_stat_of(const float (&dec)[B], float enor
         }
         return div_var_f32(var);
     } else {
-        return entropy<B>(dec, enorm);
+        return entropy<B, true>(dec, enorm);  // table log: faster for the codec march
     }
 }
 

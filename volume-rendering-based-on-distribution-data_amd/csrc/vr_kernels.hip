@@ -1562,16 +1562,20 @@ __global__ __launch_bounds__(256) void k_popcount(const unsigned long long *__re
 }
 
 // Exhaustive check of logf_canon against (float)log((double)x) over every
-// positive finite float; cnt[0] = mismatches, cnt[1] = inputs that took the
-// double-log fallback.
+// positive finite float, for both fast forms (series and table); cnt[0] =
+// mismatches of either, cnt[1] = inputs either form left to the double-log
+// fallback (summed over the two).
 __global__ __launch_bounds__(256) void k_logcheck(unsigned long long *cnt) {
     unsigned long long bad = 0, slow = 0;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t b = 1 + blockIdx.x * blockDim.x + threadIdx.x; b < 0x7F800000u; b += stride) {
         const float x = __uint_as_float(b);
         float r;
-        slow += !logf_fast(x, r);
-        bad += __float_as_uint(logf_canon(x)) != __float_as_uint((float)log((double)x));
+        slow += !logf_fast_series(x, r);
+        slow += !logf_fast_tab(x, r);
+        const uint32_t want = __float_as_uint((float)log((double)x));
+        bad += __float_as_uint(logf_canon<false>(x)) != want;
+        bad += __float_as_uint(logf_canon<true>(x)) != want;
     }
     if (bad) atomicAdd(&cnt[0], bad);
     if (slow) atomicAdd(&cnt[1], slow);
