@@ -19,6 +19,8 @@
 
 static float M[12];
 static int PF = 0;
+static int ALIGN = 0; /* 1: per-step scopes count a ray's sample s at iteration s + its depth
+                         offset round((tnear - tnear_min of the tile) / 0.01) */
 static int LAYOUT = 0; /* 0: x-rows (4 records along x per line), 1: 2x2 (x,y) micro-bricks,
                           2: 2x1x2 (x,z) micro-bricks */
 
@@ -39,6 +41,8 @@ static void lin_axis(float u, int n, int *i0, int *i1) {
 }
 
 /* the 4 line ids (one per (y,z) combo; x0/x1 records share or straddle) */
+static float g_tn;  /* tnear of the last ray_lines call (per thread below) */
+#pragma omp threadprivate(g_tn)
 static int ray_lines(int x, int y, int nsteps, uint32_t *out /* 8 per step */) {
     float u = ((float)x / (float)W) * 2.0f - 1.0f, v = ((float)y / (float)H) * 2.0f - 1.0f;
     float ox = M[3], oy = M[7], oz = M[11];
@@ -53,6 +57,7 @@ static int ray_lines(int x, int y, int nsteps, uint32_t *out /* 8 per step */) {
     float tn = fmaxf(fmaxf(fminf(tx, bx), fminf(ty, by)), fmaxf(fminf(tx, bx), fminf(tz, bz)));
     float tf = fminf(fminf(fmaxf(tx, bx), fmaxf(ty, by)), fminf(fmaxf(tx, bx), fmaxf(tz, bz)));
     if (tn < 0) tn = 0;
+    g_tn = tn;
     /* PF=1: also the step the pipelined kernels prefetch after an early exit */
     if (PF && nsteps < 500) {
         float t = tn;
@@ -98,6 +103,7 @@ int main(int argc, char **argv) {
     memcpy(M, strcmp(argv[2], "C0") == 0 ? c0 : c1, sizeof M);
     if (getenv("LAYOUT")) LAYOUT = atoi(getenv("LAYOUT"));
     if (getenv("PF")) PF = atoi(getenv("PF"));
+    if (getenv("ALIGN")) ALIGN = atoi(getenv("ALIGN"));
     FILE *f = fopen(argv[1], "rb");
     if (!f) return 1;
     int32_t *steps = malloc(sizeof(int32_t) * W * H);
@@ -114,7 +120,8 @@ int main(int argc, char **argv) {
         int tx = t % TX, ty = t / TX;
         uint32_t *buf = malloc(sizeof(uint32_t) * 256 * 500 * 8);
         uint32_t *tmp = malloc(sizeof(uint32_t) * 256 * 8);
-        int lens[256];
+        int lens[256], off[256];
+        float tns[256];
         uint32_t *rl[256];
         size_t tot = 0;
         for (int i = 0; i < 256; i++) {
@@ -125,8 +132,15 @@ int main(int argc, char **argv) {
             int n = steps[(size_t)y * W + x];
             if (n <= 0) continue;
             lens[i] = ray_lines(x, y, n, rl[i]);
+            tns[i] = g_tn;
             tot += lens[i];
             samples += n;
+        }
+        {
+            float tmin = 1e30f;
+            for (int i = 0; i < 256; i++) if (lens[i] && tns[i] < tmin) tmin = tns[i];
+            for (int i = 0; i < 256; i++)
+                off[i] = (ALIGN && lens[i]) ? (int)lrintf((tns[i] - tmin) / 0.01f) : 0;
         }
         for (size_t k = 0; k < tot; k++) {
             uint32_t l = buf[k];
@@ -135,22 +149,26 @@ int main(int argc, char **argv) {
         }
         /* per wave (16x4 rows) per step, and per tile per step */
         int maxs = 0;
-        for (int i = 0; i < 256; i++) if (lens[i] / 8 > maxs) maxs = lens[i] / 8;
-        for (int s = 0; s < maxs; s++) {
+        for (int i = 0; i < 256; i++) if (lens[i] / 8 + off[i] > maxs) maxs = lens[i] / 8 + off[i];
+        for (int k = 0; k < maxs; k++) {
             size_t nt = 0;
             for (int w = 0; w < 4; w++) {
                 size_t nw = 0;
-                for (int i = w * 64; i < w * 64 + 64; i++)
-                    if (lens[i] / 8 > s)
+                for (int i = w * 64; i < w * 64 + 64; i++) {
+                    const int s = k - off[i];
+                    if (s >= 0 && lens[i] / 8 > s)
                         for (int c = 0; c < 8; c++) tmp[nw++] = rl[i][s * 8 + c];
+                }
                 uint32_t *cp = malloc(sizeof(uint32_t) * (nw + 1));
                 memcpy(cp, tmp, nw * 4);
                 per_wave_step += uniq(cp, nw);
                 free(cp);
             }
-            for (int i = 0; i < 256; i++)
-                if (lens[i] / 8 > s)
+            for (int i = 0; i < 256; i++) {
+                const int s = k - off[i];
+                if (s >= 0 && lens[i] / 8 > s)
                     for (int c = 0; c < 8; c++) tmp[nt++] = rl[i][s * 8 + c];
+            }
             per_tile_step += uniq(tmp, nt);
         }
         for (int w = 0; w < 4; w++) {
