@@ -21,6 +21,7 @@
 #include "vr_march.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 
 namespace vr {
@@ -1173,6 +1174,126 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
                                    (j & 4) ? m.cz : m.fz);
 }
 
+// ---- method 7, software-pipelined (B <= 8) ----
+// The corner cache of K:320-367 / 395-480 refreshes when a sample leaves the
+// cell [interPos[0], interPos[7]] (inInterpolation, K:253-270).  At 1024^3 a
+// step of 0.01 crosses ~5 voxels, so nearly every step refreshes and the march
+// is a chain of dependent 8-record gathers, like methods 1/2.  Here the 8
+// corner records of the NEXT position's cell are gathered before the current
+// sample is blended (two register sets, unrolled by two, as march_pipe_tile).
+// If the next sample stays inside the current cell, no refresh happens and
+// the gathered records -- the same cell's, cache hits -- are discarded; if it
+// leaves, the refresh at that position computes exactly that cell
+// (floor/ceil of the same float position), so it decodes the gathered
+// records.  Bit-identical to k_march_m7.
+struct M7Cell {
+    float fx, fy, fz, cx, cy, cz;
+};
+
+__device__ __forceinline__ M7Cell m7_cell(const Params &P, float px, float py, float pz) {
+    const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
+    M7Cell c;
+    c.fx = floorf(qx * (float)P.m7x) / (float)P.m7x;
+    c.cx = ceilf(qx * (float)P.m7x) / (float)P.m7x;
+    c.fy = floorf(qy * (float)P.m7y) / (float)P.m7y;
+    c.cy = ceilf(qy * (float)P.m7y) / (float)P.m7y;
+    c.fz = floorf(qz * (float)P.m7z) / (float)P.m7z;
+    c.cz = ceilf(qz * (float)P.m7z) / (float)P.m7z;
+    return c;
+}
+
+template <int B>
+__device__ __forceinline__ void m7_gather(const float *__restrict__ vol, const Params &P,
+                                          const M7Cell &c, float (&rec)[8][B]) {
+    const int x0 = point_axis(c.fx, P.nx), x1 = point_axis(c.cx, P.nx);
+    const int y0 = point_axis(c.fy, P.ny), y1 = point_axis(c.cy, P.ny);
+    const int z0 = point_axis(c.fz, P.nz), z1 = point_axis(c.cz, P.nz);
+    const int xs[2] = {x0, x1}, ys[2] = {y0, y1}, zs[2] = {z0, z1};
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        load_rec<B>(vol, (uint64_t)zs[j >> 2] * P.sz + (uint64_t)ys[(j >> 1) & 1] * P.sy +
+                             (uint64_t)xs[j & 1], rec[j]);
+}
+
+#ifndef VR_M7_PIPE_MAXWAVES
+#define VR_M7_PIPE_MAXWAVES 8
+#endif
+template <int B>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PIPE_MAXWAVES))) void k_march_m7_pipe(const float *__restrict__ vol, Params P) {
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    uint32_t lx, ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    if (x >= P.W || y >= P.H) return;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    if (!make_ray(P, x, y, r)) {
+        write_miss(P, o);
+        return;
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    M7Cell cur = m7_cell(P, px, py, pz), ca, cb;  // K:320-352 at the first sample
+    float mean[8];
+    float ra[8][B], rb[8][B];
+    m7_gather<B>(vol, P, cur, ra);
+#pragma unroll
+    for (int j = 0; j < 8; j++) mean[j] = raw_mean<B>(ra[j]);
+    ca = cur;
+    int n = 0;
+    bool alive = true;
+    // one step: sample at (px, py, pz) with the cell whose records are (cc, rc)
+    // if a refresh is due; gather the next position's cell into (cn, rn)
+    auto step = [&](int i, const M7Cell &cc, const float (&rc)[8][B], M7Cell &cn,
+                    float (&rn)[8][B]) {
+        const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
+        if (qx < cur.fx || qy < cur.fy || qz < cur.fz || qx > cur.cx || qy > cur.cy ||
+            qz > cur.cz) {  // inInterpolation, K:253-270, 396: refresh from (cc, rc)
+            cur = cc;
+#pragma unroll
+            for (int j = 0; j < 8; j++) mean[j] = raw_mean<B>(rc[j]);
+        }
+        const float tn = t + kTStep;                                 // K:701
+        const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);    // K:703, K:381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;    // K:706
+        cn = m7_cell(P, nx, ny, nz);
+        m7_gather<B>(vol, P, cn, rn);
+        const float xd = (px * 0.5f + 0.5f - cur.fx) / (cur.cx - cur.fx);
+        const float yd = (py * 0.5f + 0.5f - cur.fy) / (cur.cy - cur.fy);
+        const float zd = (pz * 0.5f + 0.5f - cur.fz) / (cur.cz - cur.fz);
+        const float m00 = (float)((double)mean[0] * (1.0 - (double)xd) + (double)(mean[1] * xd));
+        const float m10 = (float)((double)mean[2] * (1.0 - (double)xd) + (double)(mean[3] * xd));
+        const float m01 = (float)((double)mean[4] * (1.0 - (double)xd) + (double)(mean[5] * xd));
+        const float m11 = (float)((double)mean[6] * (1.0 - (double)xd) + (double)(mean[7] * xd));
+        const float m0 = (float)((double)m00 * (1.0 - (double)yd) + (double)(m10 * yd));
+        const float m1 = (float)((double)m01 * (1.0 - (double)yd) + (double)(m11 * yd));
+        const float im = (float)((double)m0 * (1.0 - (double)zd) + (double)(m1 * zd));
+        n = i + 1;
+        if (composite(P, im * 50.0f, sx, sy, sz, sw) || !cont) {    // K:479, K:698
+            alive = false;
+        } else {
+            t = tn;
+            px = nx;
+            py = ny;
+            pz = nz;
+        }
+    };
+    for (int i = 0; i < kMaxSteps; i += 2) {
+        step(i, ca, ra, cb, rb);
+        if (!alive) break;
+        step(i + 1, cb, rb, ca, ra);
+        if (!alive) break;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 // ---- methods 4/5/6: fractal/template codec volume ----
 // The reference pre-bakes the decoded statistics into fractalQueryTex
 // (K:775-871) and samples it with the texture trilinear (K:639-652); here, as
@@ -1682,6 +1803,20 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         // re-reads (1024^3x8 C1 9.94 -> 8.29 ms; row-aligned C0 is fastest
         // uncapped).  Keyed on the view, not on P.path, which
         // the B < 8 rewrite above has already changed.
+        if constexpr (B > 0 && B <= 8) {
+            // pipelined corner gathers (VR_M7_PIPE=0: the plain march)
+            static const bool pipe = !(std::getenv("VR_M7_PIPE") && std::atoi(std::getenv("VR_M7_PIPE")) == 0);
+            if (pipe) {
+                // oblique views at 2 workgroups per CU (1024^3x8 C1: 8.53 -> 7.45 ms;
+                // C0 is fastest uncapped, 1.53 ms; profiles/r02/m7_pipe.log)
+                note_kernel("k_march_m7_pipe", B, method);
+                hipLaunchKernelGGL((k_march_m7_pipe<B>), grid, block,
+                                   cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu
+                                                              : (P.oblique && B == 8 ? 2 : 0)),
+                                   s, vol, P);
+                break;
+            }
+        }
         hipLaunchKernelGGL((k_march_m7<B>), grid, block,
                            cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : (P.oblique && B == 8 ? 3 : 0)),
                            s, vol, P);
