@@ -150,7 +150,7 @@ def test_slab_chain_equals_whole_volume(orc, pkg, view, method):
     full = orc.render_gmm(wm, sg, dims, p)
     direction = pkg.slabs.march_direction(m, W, H)
     assert direction != 0
-    for n in (1, 2, 3, 7):
+    for n in (1, 2, 3, 7, dims[2]):  # down to one slice per slab
         bounds = pkg.slabs.slab_bounds(dims[2], n, direction)
         out, out_f, out_n = _chain(orc, wm, sg, dims, p, bounds)
         assert np.array_equal(out, full["out"]), f"{n} slabs: RGBA8 differs"
