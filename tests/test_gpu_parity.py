@@ -665,3 +665,22 @@ def test_flex_errors(pkg, orc, gpu):
     with pytest.raises(pkg.VRError, match="no table"):
         pkg.flex_process(4)
     pkg.freeCudaBuffers()
+
+
+@pytest.mark.parametrize("quad", ["1", "0"])
+def test_method7_oblique_kernels(pkg, orc, gpu, quad, monkeypatch):
+    """method 7 on oblique views: the quad-cooperative march (grid = volume) and the
+    one-lane pipelined march give the oracle's result bit for bit, including views
+    where neighbouring rays refresh their cells at different steps"""
+    import torch
+    monkeypatch.setenv("VR_M7_QUAD", quad)
+    vol = orc.synth_volume(30, 26, 22, 8)
+    pkg.init_distribution(vol)
+    for rot in ((30.0, 45.0), (-60.0, 110.0), (12.0, -70.0)):
+        m = pkg.camera.display_inv_view(rot)
+        for density in (0.05, 0.8):
+            got = gpu_render(pkg, None, 88, 60, m, 7, torch, density=density)
+            ref = orc.render(vol, orc.make_params(88, 60, m, query_method=7, density=density,
+                                                  m7_dims=(30, 26, 22)))[:3]
+            assert_parity(got, ref, f"m7 quad={quad} {rot} d={density}")
+    assert pkg.last_kernel().startswith("k_march_m7_quad" if quad == "1" else "k_march_m7_pipe")

@@ -1138,6 +1138,192 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
                 sw * P.brightness);
 }
 
+struct M7Cell {
+    float fx, fy, fz, cx, cy, cz;
+};
+
+__device__ __forceinline__ M7Cell m7_cell(const Params &P, float px, float py, float pz) {
+    const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
+    M7Cell c;
+    c.fx = floorf(qx * (float)P.m7x) / (float)P.m7x;
+    c.cx = ceilf(qx * (float)P.m7x) / (float)P.m7x;
+    c.fy = floorf(qy * (float)P.m7y) / (float)P.m7y;
+    c.cy = ceilf(qy * (float)P.m7y) / (float)P.m7y;
+    c.fz = floorf(qz * (float)P.m7z) / (float)P.m7z;
+    c.cz = ceilf(qz * (float)P.m7z) / (float)P.m7z;
+    return c;
+}
+
+// ---- method 7, quad-cooperative (B == 8, oblique views) ----
+// k_march_m7_pipe's corner cache with the quad march's gathers: the 4 lanes of
+// a quad read each of their 4 rays' cell corners as contiguous 64-byte x-pairs
+// (qc_gather), a pair swap gives lane g the records of corner (x = g>>1,
+// y = g&1) at z0 and z1, and lane g keeps the corner means of those two
+// corners for every ray of its quad (refreshed only when the ray leaves its
+// cell, K:253-270, 396).  The blend gathers a ray's 8 means inside the quad
+// (quad_perm broadcasts) and evaluates K:395-480's double lerps exactly as the
+// one-lane march.  The next position's cell is gathered group by group while
+// the current one blends (rolling prefetch); when no refresh follows, those
+// records are the current cell's (cache hits) and are discarded.  Used when the
+// method-7 grid equals the volume (cell corners then lie within 2 voxels).
+// A cell's corner voxels are point-sampled from its float bounds (K:359-364):
+// floor(floor(q N)/N * N) can come out one below floor(q N), so x1 - x0 (and
+// y, z) is 0, 1 or 2 -- the pair is not always adjacent.  The cell is packed
+// with both corners of every axis (w0 = x0 | x1 << 16, w1 = y0 | y1 << 16,
+// w2 = z0 | z1 << 16, w3 = live), and lane g reads 16-byte chunk g & 1 of
+// record x0 (g < 2) or x1 (g >= 2): one contiguous 64-byte run per combo when
+// the records are adjacent, the two halves otherwise.
+struct CellPacked {
+    int w0, w1, w2, w3;
+};
+
+__device__ __forceinline__ CellPacked pack_cell(const Params &P, const M7Cell &c, bool live) {
+    CellPacked p;
+    p.w0 = point_axis(c.fx, P.nx) | (point_axis(c.cx, P.nx) << 16);
+    p.w1 = point_axis(c.fy, P.ny) | (point_axis(c.cy, P.ny) << 16);
+    p.w2 = point_axis(c.fz, P.nz) | (point_axis(c.cz, P.nz) << 16);
+    p.w3 = live ? 1 : 0;
+    return p;
+}
+
+template <int G>
+__device__ __forceinline__ bool qc_gather_cell(const float *__restrict__ vol, const Params &P,
+                                               const CellPacked &cp, uint32_t g, float4 (&L)[4]) {
+    const bool live = bcast_g<G>(cp.w3) != 0;
+    if (live) {
+        const uint32_t w0 = (uint32_t)bcast_g<G>(cp.w0), w1 = (uint32_t)bcast_g<G>(cp.w1),
+                       w2 = (uint32_t)bcast_g<G>(cp.w2);
+        const uint64_t xr = g < 2 ? (w0 & 0xFFFFu) : (w0 >> 16);
+        const uint64_t y0 = w1 & 0xFFFFu, y1 = w1 >> 16, z0 = w2 & 0xFFFFu, z1 = w2 >> 16;
+        const uint32_t chunk = g & 1u;
+        L[0] = reinterpret_cast<const float4 *>(vol + (z0 * P.sz + y0 * P.sy + xr) * 8)[chunk];
+        L[1] = reinterpret_cast<const float4 *>(vol + (z0 * P.sz + y1 * P.sy + xr) * 8)[chunk];
+        L[2] = reinterpret_cast<const float4 *>(vol + (z1 * P.sz + y0 * P.sy + xr) * 8)[chunk];
+        L[3] = reinterpret_cast<const float4 *>(vol + (z1 * P.sz + y1 * P.sy + xr) * 8)[chunk];
+    }
+    return live;
+}
+
+template <int K>
+__device__ __forceinline__ float qbcast(float v) {
+    return qperm<K == 0 ? kQ0 : K == 1 ? kQ1 : K == 2 ? kQ2 : kQ3>(v);
+}
+
+template <int G>
+__device__ __forceinline__ float m7q_group(const float *__restrict__ vol, const Params &P,
+                                           bool refresh_any, int refresh_bits, float xd, float yd,
+                                           float zd, const CellPacked &fn, bool &ln, uint32_t g,
+                                           float4 (&L)[4], float (&mz)[2]) {
+    const bool odd = g & 1u;
+    float r0[8], r1[8];
+    pair_swap(L[0], L[1], odd, r0);  // corner (x = g>>1, y = g&1) at z0
+    pair_swap(L[2], L[3], odd, r1);  //                              at z1
+    ln = qc_gather_cell<G>(vol, P, fn, g, L);
+    if (refresh_any && ((refresh_bits >> G) & 1)) {  // ray G left its cell: its new means
+        mz[0] = raw_mean<8>(r0);
+        mz[1] = raw_mean<8>(r1);
+    }
+    // ray G's 8 corner means on every lane: lane 0 (x0,y0), 1 (x0,y1), 2 (x1,y0), 3 (x1,y1)
+    const float fxd = __int_as_float(bcast_g<G>(__float_as_int(xd)));
+    const float fyd = __int_as_float(bcast_g<G>(__float_as_int(yd)));
+    const float fzd = __int_as_float(bcast_g<G>(__float_as_int(zd)));
+    float mn[8];
+    mn[0] = qbcast<0>(mz[0]); mn[2] = qbcast<1>(mz[0]); mn[1] = qbcast<2>(mz[0]); mn[3] = qbcast<3>(mz[0]);
+    mn[4] = qbcast<0>(mz[1]); mn[6] = qbcast<1>(mz[1]); mn[5] = qbcast<2>(mz[1]); mn[7] = qbcast<3>(mz[1]);
+    const float m00 = (float)((double)mn[0] * (1.0 - (double)fxd) + (double)(mn[1] * fxd));
+    const float m10 = (float)((double)mn[2] * (1.0 - (double)fxd) + (double)(mn[3] * fxd));
+    const float m01 = (float)((double)mn[4] * (1.0 - (double)fxd) + (double)(mn[5] * fxd));
+    const float m11 = (float)((double)mn[6] * (1.0 - (double)fxd) + (double)(mn[7] * fxd));
+    const float m0 = (float)((double)m00 * (1.0 - (double)fyd) + (double)(m10 * fyd));
+    const float m1 = (float)((double)m01 * (1.0 - (double)fyd) + (double)(m11 * fyd));
+    return (float)((double)m0 * (1.0 - (double)fzd) + (double)(m1 * fzd));
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAVES, 8))) void k_march_m7_quad(const float *__restrict__ vol, Params P) {
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;  // uniform per workgroup
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t q = lane >> 2, g = lane & 3u;
+    const uint32_t lx = wave * 16u + q, ly = g;  // 16x4 block per wave, quad = a column
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    const bool hit = alive;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    // the home ray's cell (K:320-352): the first sample always takes its means
+    // from the records gathered here (the one-lane march's initial refresh)
+    M7Cell cur = m7_cell(P, px, py, pz);
+    bool first = true;
+    float4 L0[4], L1[4], L2[4], L3[4];
+    float mz0[2] = {0.f, 0.f}, mz1[2] = {0.f, 0.f}, mz2[2] = {0.f, 0.f}, mz3[2] = {0.f, 0.f};
+    const CellPacked fc = pack_cell(P, cur, alive);
+    bool lc[4];
+    lc[0] = qc_gather_cell<0>(vol, P, fc, g, L0);
+    lc[1] = qc_gather_cell<1>(vol, P, fc, g, L1);
+    lc[2] = qc_gather_cell<2>(vol, P, fc, g, L2);
+    lc[3] = qc_gather_cell<3>(vol, P, fc, g, L3);
+    for (int i = 0; i < kMaxSteps; i++) {
+        if (!wave_any(alive)) break;
+        // the home ray at its current sample: refresh due? (its new cell's
+        // records are the ones gathered for this position)
+        const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
+        bool refresh = false;
+        if (alive) {
+            refresh = first || qx < cur.fx || qy < cur.fy || qz < cur.fz || qx > cur.cx ||
+                      qy > cur.cy || qz > cur.cz;
+            if (refresh) cur = m7_cell(P, px, py, pz);
+        }
+        first = false;
+        const float xd = (qx - cur.fx) / (cur.cx - cur.fx);
+        const float yd = (qy - cur.fy) / (cur.cy - cur.fy);
+        const float zd = (qz - cur.fz) / (cur.cz - cur.fz);
+        const float tn = t + kTStep;                                        // K:701
+        const bool cont = alive && !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, 381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
+        const CellPacked fn = pack_cell(P, m7_cell(P, nx, ny, nz), cont);
+        // refresh flags of the quad's 4 rays, bit G = ray (G, q)
+        const int rb = refresh ? 1 << g : 0;
+        const int rbits = qpermi<kQ0>(rb) | qpermi<kQ1>(rb) | qpermi<kQ2>(rb) | qpermi<kQ3>(rb);
+        const bool rany = rbits != 0;
+        bool ln[4];
+        const float b0 = m7q_group<0>(vol, P, rany, rbits, xd, yd, zd, fn, ln[0], g, L0, mz0);
+        const float b1 = m7q_group<1>(vol, P, rany, rbits, xd, yd, zd, fn, ln[1], g, L1, mz1);
+        const float b2 = m7q_group<2>(vol, P, rany, rbits, xd, yd, zd, fn, ln[2], g, L2, mz2);
+        const float b3 = m7q_group<3>(vol, P, rany, rbits, xd, yd, zd, fn, ln[3], g, L3, mz3);
+        const float im = g == 0 ? b0 : (g == 1 ? b1 : (g == 2 ? b2 : b3));
+        if (alive) {
+            n = i + 1;
+            if (composite(P, im * 50.0f, sx, sy, sz, sw) || !cont) {  // K:479, K:698
+                alive = false;
+            } else {
+                t = tn;
+                px = nx;
+                py = ny;
+                pz = nz;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) lc[k] = ln[k];
+    }
+    (void)lc;
+    if (!valid) return;
+    if (!hit) {
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 // ---- method 7: software trilinear of corner means, K:320-367, 395-480 ----
 struct M7 {
     float fx, fy, fz, cx, cy, cz;  // interPos[0] and interPos[7]
@@ -1186,22 +1372,6 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
 // leaves, the refresh at that position computes exactly that cell
 // (floor/ceil of the same float position), so it decodes the gathered
 // records.  Bit-identical to k_march_m7.
-struct M7Cell {
-    float fx, fy, fz, cx, cy, cz;
-};
-
-__device__ __forceinline__ M7Cell m7_cell(const Params &P, float px, float py, float pz) {
-    const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
-    M7Cell c;
-    c.fx = floorf(qx * (float)P.m7x) / (float)P.m7x;
-    c.cx = ceilf(qx * (float)P.m7x) / (float)P.m7x;
-    c.fy = floorf(qy * (float)P.m7y) / (float)P.m7y;
-    c.cy = ceilf(qy * (float)P.m7y) / (float)P.m7y;
-    c.fz = floorf(qz * (float)P.m7z) / (float)P.m7z;
-    c.cz = ceilf(qz * (float)P.m7z) / (float)P.m7z;
-    return c;
-}
-
 template <int B>
 __device__ __forceinline__ void m7_gather(const float *__restrict__ vol, const Params &P,
                                           const M7Cell &c, float (&rec)[8][B]) {
@@ -1803,9 +1973,22 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         // re-reads (1024^3x8 C1 9.94 -> 8.29 ms; row-aligned C0 is fastest
         // uncapped).  Keyed on the view, not on P.path, which
         // the B < 8 rewrite above has already changed.
+        if constexpr (B == 8) {
+            // oblique views with the method-7 grid equal to the volume: the
+            // quad-cooperative march (VR_M7_QUAD=0 disables), 2 workgroups per CU
+            const char *eq = std::getenv("VR_M7_QUAD");
+            const bool quad = !(eq && std::atoi(eq) == 0);
+            if (quad && P.oblique && P.m7x == P.nx && P.m7y == P.ny && P.m7z == P.nz) {
+                note_kernel("k_march_m7_quad", B, method);
+                hipLaunchKernelGGL(k_march_m7_quad, grid, block,
+                                   cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2), s, vol, P);
+                break;
+            }
+        }
         if constexpr (B > 0 && B <= 8) {
             // pipelined corner gathers (VR_M7_PIPE=0: the plain march)
-            static const bool pipe = !(std::getenv("VR_M7_PIPE") && std::atoi(std::getenv("VR_M7_PIPE")) == 0);
+            const char *ep = std::getenv("VR_M7_PIPE");
+            const bool pipe = !(ep && std::atoi(ep) == 0);
             if (pipe) {
                 // oblique views at 2 workgroups per CU (1024^3x8 C1: 8.53 -> 7.45 ms;
                 // C0 is fastest uncapped, 1.53 ms; profiles/r02/m7_pipe.log)
