@@ -244,7 +244,7 @@ __device__ __forceinline__ float raw_variance(const float (&p)[B], float mean) {
 // i = 64, e = -1, log c = ln 2 split like e ln 2).  No f64 division; the
 // midpoint test reads y's low 29 mantissa bits (a float's half-ulp pattern is
 // 1 << 28 there whatever y's binade), instead of float/ldexp arithmetic.
-__device__ __forceinline__ bool logf_fast_tab(float x, float &r) {
+__device__ __forceinline__ bool logf_fast_tabp(float x, float &r, const LogEnt *tab) {
     int e;
     float m = frexpf(x, &e);                   // x = m 2^e, m in [0.5, 1), also subnormal x
     m = m * 2.0f;                              // [1, 2), exact
@@ -252,7 +252,7 @@ __device__ __forceinline__ bool logf_fast_tab(float x, float &r) {
     const int i = (int)((m - 1.0f) * 64.0f + 0.5f);   // 0 .. 64
     const float c = i == 64 ? 2.0f : 1.0f + (float)i * 0x1p-6f;
     const float d = m - c;                     // exact, |d| <= 1/128
-    const LogEnt t = kLogTab[i];
+    const LogEnt t = tab[i];
     const double rr = (double)d * t.inv;
     double q = 1.0 / 7.0;
     q = fma(q, rr, -1.0 / 6.0);
@@ -269,6 +269,17 @@ __device__ __forceinline__ bool logf_fast_tab(float x, float &r) {
     const uint64_t lo29 = (uint64_t)__double_as_longlong(y) & 0x1FFFFFFFull;
     const uint64_t dist = lo29 > 0x10000000ull ? lo29 - 0x10000000ull : 0x10000000ull - lo29;
     return dist > 512u;                        // > 2^-44 |y| from a midpoint
+}
+
+// the table in constant memory / a copy in the kernel's LDS (copy_logtab)
+__device__ __forceinline__ bool logf_fast_tab(float x, float &r) {
+    return logf_fast_tabp(x, r, kLogTab);
+}
+
+// Copies the log table into LDS (65 x 32 bytes); the workgroup must then
+// __syncthreads() before the first use.
+__device__ __forceinline__ void copy_logtab(LogEnt *dst) {
+    if (threadIdx.x < 65) dst[threadIdx.x] = kLogTab[threadIdx.x];
 }
 
 // The round-1 form: atanh series of (m - 1)/(m + 1), one f64 division, no
@@ -314,6 +325,28 @@ __device__ __forceinline__ float logf_canon(float x) {
     return (float)log((double)x);
 }
 
+__device__ __forceinline__ float logf_canon_p(float x, const LogEnt *tab) {
+    float r;
+    if (x == 1.0f) return 0.0f;
+    if (logf_fast_tabp(x, r, tab)) return r;
+    return (float)log((double)x);
+}
+
+// K:761-769 with the log table at `tab` (an LDS copy)
+template <int B>
+__device__ __forceinline__ float entropy_p(const float (&p)[B], float enorm, const LogEnt *tab) {
+    float ent = 0.0f;
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+        const float pr = p[i];
+        const double t =
+            pr <= 0 ? 0.0 : div_const((double)logf_canon_p(pr, tab), VR_LN2_D, kLn2R);
+        ent = (float)((double)ent + (double)pr * t);
+    }
+    ent = -ent;
+    return ent / enorm;
+}
+
 // K:761-769
 template <int B, bool TAB = false>
 __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
@@ -340,6 +373,13 @@ __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
     } else {
         return entropy<B>(p, enorm);
     }
+}
+
+// record_stat with the entropy's log table in LDS (tab: copy_logtab)
+template <int B, int M>
+__device__ __forceinline__ float record_stat_p(const float (&p)[B], float enorm, const LogEnt *tab) {
+    if constexpr (M == 3) return entropy_p<B>(p, enorm, tab);
+    else return record_stat<B, M>(p, enorm);
 }
 
 // ---- fractal/template codec, methods 4/5/6 (K:195-222, 775-871) ----

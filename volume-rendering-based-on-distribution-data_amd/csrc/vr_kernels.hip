@@ -524,9 +524,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
     __shared__ uint2 s_rows[4][kWsRows];  // x: ry | rz << 10 | loff << 20,  y: xmin
     __shared__ int s_mark[4][kWsRec];
     __shared__ float s_stat[4][kWsRec];
+    extern __shared__ __attribute__((aligned(32))) LogEnt s_lt[];  // entropy's log table (M == 3)
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // whole workgroup uniform
+    if constexpr (M == 3) {
+        copy_logtab(s_lt);
+        __syncthreads();
+    }
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     int *xmn = s_xmn[wave], *xmx = s_xmx[wave], *toff = s_toff[wave], *mark = s_mark[wave];
     uint2 *rowv = s_rows[wave];
@@ -659,7 +664,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                     }
 #pragma unroll
                     for (int u = 0; u < U; u++)
-                        if (li[u] >= 0) stat[li[u]] = record_stat<B, M>(rr[u], P.enorm);
+                        if (li[u] >= 0) stat[li[u]] = record_stat_p<B, M>(rr[u], P.enorm, s_lt);
                 }
                 wave_sync();
                 WG_PROF_T(9)
@@ -1049,7 +1054,8 @@ __device__ __forceinline__ float qc_blend(const FootPacked &fp, float s0, float 
 template <int G, int M>
 __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const Params &P,
                                           const FootPacked &fc, bool lc, const FootPacked &fn,
-                                          bool &ln, uint32_t g, float4 (&L)[4]) {
+                                          bool &ln, uint32_t g, float4 (&L)[4],
+                                          const LogEnt *lt) {
     // this step's records of ray (G, q) out of the chunk registers ...
     const bool odd = g & 1u;
     float r0[8], r1[8];
@@ -1059,8 +1065,8 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
     ln = qc_gather<G>(vol, P, fn, g, L);
     float s0 = 0.0f, s1 = 0.0f;
     if (lc) {
-        s0 = record_stat<8, M>(r0, P.enorm);
-        s1 = record_stat<8, M>(r1, P.enorm);
+        s0 = record_stat_p<8, M>(r0, P.enorm, lt);
+        s1 = record_stat_p<8, M>(r1, P.enorm, lt);
     }
     return qc_blend<G>(fc, s0, s1);
 }
@@ -1070,9 +1076,17 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
 #endif
 template <int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAVES, 8))) void k_march_quad(const float *__restrict__ vol, Params P) {
+    // entropy: the exact log's table in LDS (the launch's occupancy request
+    // reserves far more than its 2 KiB); a load from there is an LDS read, not
+    // a constant-memory gather on the march's critical path
+    extern __shared__ __attribute__((aligned(32))) LogEnt s_lt[];
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // uniform per workgroup
+    if constexpr (M == 3) {
+        copy_logtab(s_lt);
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 2, g = lane & 3u;
 #if VR_QUAD_MAP == 1  // wave = one 64-pixel row, quad = 4 consecutive pixels
@@ -1109,10 +1123,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
         const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
         const FootPacked fn = pack_foot(footprint(P, nx, ny, nz), cont);
         bool ln[4];
-        const float b0 = qc_group<0, M>(vol, P, fc, lc[0], fn, ln[0], g, L0);
-        const float b1 = qc_group<1, M>(vol, P, fc, lc[1], fn, ln[1], g, L1);
-        const float b2 = qc_group<2, M>(vol, P, fc, lc[2], fn, ln[2], g, L2);
-        const float b3 = qc_group<3, M>(vol, P, fc, lc[3], fn, ln[3], g, L3);
+        const float b0 = qc_group<0, M>(vol, P, fc, lc[0], fn, ln[0], g, L0, s_lt);
+        const float b1 = qc_group<1, M>(vol, P, fc, lc[1], fn, ln[1], g, L1, s_lt);
+        const float b2 = qc_group<2, M>(vol, P, fc, lc[2], fn, ln[2], g, L2, s_lt);
+        const float b3 = qc_group<3, M>(vol, P, fc, lc[3], fn, ln[3], g, L3, s_lt);
         const float sample = g == 0 ? b0 : (g == 1 ? b1 : (g == 2 ? b2 : b3));
         if (alive) {
             n = i + 1;
@@ -1534,7 +1548,14 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
         __syncthreads();
     }
     // this thread's error scratch column, after the (16-byte aligned) template table
-    float *scr = s_lds + (TL ? ((uint32_t)P.tpl_lds / 4 + 3u) & ~3u : 0u) + threadIdx.x;
+    const uint32_t scr0 = TL ? ((uint32_t)P.tpl_lds / 4 + 3u) & ~3u : 0u;
+    float *scr = s_lds + scr0 + threadIdx.x;
+    // entropy (C == 2): the exact log's table after the scratch (32-byte aligned)
+    LogEnt *lt = reinterpret_cast<LogEnt *>(s_lds + ((scr0 + (uint32_t)B * 256u + 7u) & ~7u));
+    if constexpr (C == 2) {
+        copy_logtab(lt);
+        __syncthreads();
+    }
     uint32_t lx, ly;
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
@@ -1590,7 +1611,7 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
             float dec[B];
             codec_decode_scr<B, TL>(P, s_lds, scr, c[j], pre[j],
                                     P.err + v[j] * (uint64_t)P.err_slots, dec);
-            sv[j] = codec_stat_of<B, C>(dec, P.enorm);
+            sv[j] = C == 2 ? entropy_p<B>(dec, P.enorm, lt) : codec_stat_of<B, C>(dec, P.enorm);
         }
         n = i + 1;
         if (composite(P, blend8(sv, f), sx, sy, sz, sw)) break;
@@ -1610,7 +1631,8 @@ static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream
     if (!COUNT) note_kernel("k_march_codec", B, method);
     // template table (if staged) at the front of the request, then the error
     // scratch (B floats per thread); VR_WG_PER_CU caps
-    const size_t need = (((size_t)P.tpl_lds + 15) & ~(size_t)15) + (size_t)B * 256u * 4u;
+    const size_t need = (((((size_t)P.tpl_lds + 15) & ~(size_t)15) + (size_t)B * 256u * 4u + 31) &
+                         ~(size_t)31) + (method == 6 ? 65 * sizeof(LogEnt) : 0);
     const size_t lds = cap_lds(P, P.wg_per_cu, need);
     const bool tl = P.tpl_lds != 0;
     switch (method * 2 + (tl ? 1 : 0)) {
@@ -1946,7 +1968,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             switch (method) {
             case 1: hipLaunchKernelGGL((k_march_ws<B, 1>), grid, block, 0, s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_ws<B, 2>), grid, block, 0, s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_ws<B, 3>), grid, block, 0, s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_ws<B, 3>), grid, block, 65 * sizeof(LogEnt), s, vol, P); break;
             }
             return hipGetLastError();
         }
