@@ -165,8 +165,9 @@ def main_gmm(args):
     launch per frame.  N > 1: rank r holds z-slab r (in the view's march order)
     and the frame is a chain: receive the previous slab's alive rays, march,
     send the survivors on (RCCL point-to-point over xGMI), then the ranks'
-    frames are summed on rank 0.  Ranks run ahead frame by frame (a pipeline,
-    one frame in flight per rank)."""
+    frames are summed on rank 0 by an asynchronous reduce on a separate group.
+    Ranks run ahead frame by frame: the chain is a pipeline whose period is the
+    slowest rank's (receive + march + send), not the sum over ranks."""
     import torch
     import torch.distributed as dist
     import __graft_entry__ as graft
@@ -207,18 +208,35 @@ def main_gmm(args):
         z_lo, z_hi = pkg.slabs.slab_bounds(n, world, direction)[rank]
         zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
         pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
-    frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
-    desc = pkg.make_desc(frame, W, H, m, query_method=args.method, volume_size=(1, 1, 1))
+    # Frames: a ring of 2N buffers.  Each frame's assembly (a SUM reduce on its
+    # own process group, hence its own RCCL stream) is issued asynchronously
+    # right after the frame's march, so no rank waits for the whole chain: rank 0
+    # can march frame f+1 while the last rank still marches frame f, and a ring
+    # buffer is reused only after its reduce has consumed it.
+    R = 2 * world if world > 1 else 1
+    frames = [torch.zeros(W * H, dtype=torch.int32, device=dev) for _ in range(R)]
+    descs = [pkg.make_desc(f, W, H, m, query_method=args.method, volume_size=(1, 1, 1))
+             for f in frames]
+    desc = descs[0]
+    asm_group = None
     if world > 1:
         rays_in = torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device=dev)
         rays_out = torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device=dev)
         cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        asm_group = dist.new_group(list(range(world)))
     torch.cuda.synchronize()
     ev, alive = [], []
     balanced = False
+    works = [None] * R
+    nframe = [0]
 
     def step(timed):
+        b = nframe[0] % R
+        nframe[0] += 1
+        frame = frames[b]
         with torch.cuda.stream(stream):
+            if works[b] is not None:
+                works[b].wait()  # this buffer's previous frame has been reduced
             frame.zero_()  # C:208
             n_in = 0
             if world > 1:
@@ -229,11 +247,11 @@ def main_gmm(args):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
             if world == 1:
-                pkg.render_gmm(desc)
+                pkg.render_gmm(descs[b])
             else:
-                pkg.render_gmm(desc, pkg.gmm_slab(z_lo, z_hi, rays_out, cnt,
-                                                  d_rays_in=rays_in if rank > 0 else None,
-                                                  n_rays_in=n_in))
+                pkg.render_gmm(descs[b], pkg.gmm_slab(z_lo, z_hi, rays_out, cnt,
+                                                      d_rays_in=rays_in if rank > 0 else None,
+                                                      n_rays_in=n_in))
             if timed:
                 e1.record(stream)
                 ev.append((e0, e1))
@@ -243,7 +261,13 @@ def main_gmm(args):
                     alive.append(n_out)
                 if rank < world - 1:
                     pkg.slabs.send_alive(rays_out, n_out, rank + 1, dist)
-                pkg.slabs.reduce_frame(frame, dist)
+                works[b] = pkg.slabs.reduce_frame(frame, dist, group=asm_group, async_op=True)
+
+    def drain():
+        for w in works:
+            if w is not None:
+                w.wait()
+        torch.cuda.synchronize()
 
     if world > 1 and not args.no_balance:
         # Cost-balanced slabs (untimed, once per view): early ray termination
@@ -252,7 +276,7 @@ def main_gmm(args):
         # minimised, each slab within the smallest rank's free HBM), then
         # generate their new slab (slabs.bounds_by_cost).
         step(True)
-        torch.cuda.synchronize()
+        drain()
         ms = ev[-1][0].elapsed_time(ev[-1][1])
         ev.clear()
         alive.clear()
@@ -276,14 +300,14 @@ def main_gmm(args):
         balanced = True
     for _ in range(args.warmup):
         step(False)
-    torch.cuda.synchronize()
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    torch.cuda.synchronize()
+    drain()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -295,7 +319,8 @@ def main_gmm(args):
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if args.dump_frame and rank == 0:
-        np.save(args.dump_frame, frame.cpu().numpy().view(np.uint32).reshape(H, W))
+        last = frames[(nframe[0] - 1) % R]
+        np.save(args.dump_frame, last.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
     u = pkg.gmm_count_footprint(desc) if world == 1 else None
     alg_bytes = u * rec_bytes + W * H * 4 if u is not None else None

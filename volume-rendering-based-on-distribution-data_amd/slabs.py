@@ -159,16 +159,25 @@ def recv_alive(src: int, out, dist) -> int:
     return n
 
 
-def reduce_frame(frame, dist) -> None:
+class _Done:
+    def wait(self):
+        return True
+
+
+def reduce_frame(frame, dist, group=None, async_op=False):
     """Sum the ranks' frames on rank 0: each pixel was written by the one slab
-    where its ray ended (or by none: a miss), every other rank holds 0 there."""
+    where its ray ended (or by none: a miss), every other rank holds 0 there.
+    async_op (RCCL): returns the work handle; its wait() makes the calling
+    stream wait for the reduce.  gloo (staged through host memory) completes
+    before returning."""
     if _staged(dist) and frame.is_cuda:
         h = frame.cpu()
-        dist.reduce(h, 0, op=dist.ReduceOp.SUM)
+        dist.reduce(h, 0, op=dist.ReduceOp.SUM, group=group)
         if dist.get_rank() == 0:
             frame.copy_(h)
-    else:
-        dist.reduce(frame, 0, op=dist.ReduceOp.SUM)
+        return _Done()
+    w = dist.reduce(frame, 0, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return w if async_op else _Done()
 
 
 def chain_frame(rank: int, world: int, render_slab, rays_in, n_in: Optional[int], dist):
