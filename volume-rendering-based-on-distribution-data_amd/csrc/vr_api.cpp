@@ -492,6 +492,15 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     if (along_rows && d->d_tile_list && (d->query_method == 1 || d->query_method == 2) &&
         (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= seg_rays)
         P.path = 7;
+    // Oblique views of a volume coarse for the frame (>= 4 pixels per voxel of
+    // the x-y face, e.g. 512^3 at 1080p): neighbouring rays share most records,
+    // the launch is bound by the per-ray step chain rather than HBM, and the
+    // pipelined 2-lane segmented march beats the quad march (512^3 x 8 C1: m1
+    // 2.05 -> 1.77 ms, m2 1.87 -> 1.63; at 1024^3, 2 pixels per voxel, the quad
+    // march stays ahead: 3.49 vs 5.23 ms; profiles/r02/paths_512x8.log).
+    if (!along_rows && g.nb == 8 && (d->query_method == 1 || d->query_method == 2) &&
+        (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
+        P.path = 7;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
         if (v >= 0 && v <= 9) P.path = v;
