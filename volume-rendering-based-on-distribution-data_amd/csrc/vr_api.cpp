@@ -1139,6 +1139,10 @@ int check_gmm_shape(vr_extent dims, int K, int z_base, int nzs) {
     if (dims.width == 0 || dims.height == 0 || dims.depth == 0 || dims.width > 65536 ||
         dims.height > 65536 || dims.depth > 65536)
         return fail(VR_ERR_ARG, "GMM volume: bad dims");
+    // a slice must stay below 2^31 voxels: the march offsets corners by 32-bit slice strides
+    if ((uint64_t)dims.width * dims.height >= (1ull << 31))
+        return fail(VR_ERR_ARG, "GMM volume: a slice of %zu x %zu voxels is too large", dims.width,
+                    dims.height);
     if (z_base < 0 || nzs < 1 || (size_t)z_base + (size_t)nzs > dims.depth)
         return fail(VR_ERR_ARG, "GMM volume: resident slices [%d, %d) outside [0, %zu)", z_base,
                     z_base + nzs, dims.depth);
