@@ -1625,6 +1625,162 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
                 sw * P.brightness);
 }
 
+// ---- methods 4/5/6, quad-cooperative (B == 8, oblique views) ----
+// The codec march with the quad march's lane roles (k_march_quad): the 4
+// lanes of a quad take turns on their 4 rays; for ray G, lane g fetches and
+// decodes the two corners (x = g>>1, y = g&1) at z0 and z1 -- codebook entry
+// plus the first 4 error pairs each -- so a quad's loads land on two rows of
+// adjacent voxels instead of the 8 scattered corners one lane would fetch
+// for its own ray, and every corner is decoded once.  The blend runs inside
+// the quad (qc_blend, the reference's lerp order); the next step's corner
+// data of group G is fetched into the registers group G has just released.
+struct CqPart {
+    int4 c[2];
+    float4 e[2][2];
+};
+
+template <int G>
+__device__ __forceinline__ bool cq_gather(const Params &P, const FootPacked &fp, uint32_t g,
+                                          bool pre16, int npre, CqPart &d) {
+    const int w0 = bcast_g<G>(fp.w0), w1 = bcast_g<G>(fp.w1);
+    const bool live = (w1 >> 19) & 1;
+    if (live) {
+        const uint64_t x = ((uint32_t)w0 & 0xFFFFu) + (g >> 1) * (((uint32_t)w1 >> 16) & 1u);
+        const uint64_t y = ((uint32_t)w0 >> 16) + (g & 1u) * (((uint32_t)w1 >> 17) & 1u);
+        const uint64_t z0 = (uint32_t)w1 & 0xFFFFu;
+        const uint64_t v0 = z0 * P.sz + y * P.sy + x;
+        const uint64_t v1 = v0 + (((uint32_t)w1 >> 18) & 1u) * P.sz;
+        const uint64_t v[2] = {v0, v1};
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            d.c[k] = P.cb[v[k]];
+            const float2 *e = P.err + v[k] * (uint64_t)P.err_slots;
+            if (pre16) {
+                d.e[k][0] = reinterpret_cast<const float4 *>(e)[0];
+                d.e[k][1] = reinterpret_cast<const float4 *>(e)[1];
+            } else {
+                float2 q[kCodecPre];
+#pragma unroll
+                for (int j = 0; j < kCodecPre; j++) q[j] = j < npre ? e[j] : make_float2(0.f, 0.f);
+                d.e[k][0] = make_float4(q[0].x, q[0].y, q[1].x, q[1].y);
+                d.e[k][1] = make_float4(q[2].x, q[2].y, q[3].x, q[3].y);
+            }
+        }
+    }
+    return live;
+}
+
+template <int C, bool TL>
+__device__ __forceinline__ float cq_stat(const Params &P, const float *s_tpl, float *scr,
+                                         const LogEnt *lt, const int4 c, const float4 (&pre)[2],
+                                         uint64_t vox) {
+    float dec[8];
+    codec_decode_scr<8, TL>(P, s_tpl, scr, c, pre, P.err + vox * (uint64_t)P.err_slots, dec);
+    if constexpr (C == 2) return entropy_p<8>(dec, P.enorm, lt);
+    else return codec_stat_of<8, C>(dec, P.enorm);
+}
+
+template <int G, int C, bool TL>
+__device__ __forceinline__ float cq_group(const Params &P, const float *s_tpl, float *scr,
+                                          const LogEnt *lt, const FootPacked &fc, bool lc,
+                                          const FootPacked &fn, bool &ln, uint32_t g, bool pre16,
+                                          int npre, CqPart &D) {
+    // this step's corner data of ray (G, q) out of the registers ...
+    const CqPart cur = D;
+    // ... which then take the next step's fetches of the same group
+    ln = cq_gather<G>(P, fn, g, pre16, npre, D);
+    float s0 = 0.0f, s1 = 0.0f;
+    if (lc) {
+        // the corners' voxel indices again (errors beyond the first 4 pairs are read directly)
+        const int w0 = bcast_g<G>(fc.w0), w1 = bcast_g<G>(fc.w1);
+        const uint64_t x = ((uint32_t)w0 & 0xFFFFu) + (g >> 1) * (((uint32_t)w1 >> 16) & 1u);
+        const uint64_t y = ((uint32_t)w0 >> 16) + (g & 1u) * (((uint32_t)w1 >> 17) & 1u);
+        const uint64_t v0 = ((uint32_t)w1 & 0xFFFFu) * P.sz + y * P.sy + x;
+        const uint64_t v1 = v0 + (((uint32_t)w1 >> 18) & 1u) * P.sz;
+        s0 = cq_stat<C, TL>(P, s_tpl, scr, lt, cur.c[0], cur.e[0], v0);
+        s1 = cq_stat<C, TL>(P, s_tpl, scr, lt, cur.c[1], cur.e[1], v1);
+    }
+    return qc_blend<G>(fc, s0, s1);
+}
+
+template <int C, bool TL>
+__global__ __launch_bounds__(256) void k_march_codec_quad(const float *__restrict__ unused, Params P) {
+    (void)unused;
+    extern __shared__ __attribute__((aligned(16))) float s_lds[];
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;  // uniform per workgroup
+    if constexpr (TL) {
+        const uint32_t n = (uint32_t)P.tpl_lds / 4;
+        for (uint32_t i = threadIdx.x; i < n; i += 256) s_lds[i] = P.tpl[i];
+    }
+    const uint32_t scr0 = TL ? ((uint32_t)P.tpl_lds / 4 + 3u) & ~3u : 0u;
+    float *scr = s_lds + scr0 + threadIdx.x;
+    LogEnt *lt = reinterpret_cast<LogEnt *>(s_lds + ((scr0 + 8u * 256u + 7u) & ~7u));
+    if constexpr (C == 2) copy_logtab(lt);
+    if constexpr (TL || C == 2) __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t q = lane >> 2, g = lane & 3u;
+    const uint32_t lx = wave * 16u + q, ly = g;  // 16x4 block per wave, quad = a column
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    // every lane stays to the end: quads cooperate on each other's rays
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    const bool hit = alive;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    const bool pre16 = P.err_slots >= kCodecPre && (P.err_slots & 1) == 0;
+    const int npre = P.err_slots < kCodecPre ? P.err_slots : kCodecPre;
+    int n = 0;
+    CqPart D0, D1, D2, D3;
+    FootPacked fc = pack_foot(footprint(P, px, py, pz), alive);
+    bool lc[4];
+    lc[0] = cq_gather<0>(P, fc, g, pre16, npre, D0);
+    lc[1] = cq_gather<1>(P, fc, g, pre16, npre, D1);
+    lc[2] = cq_gather<2>(P, fc, g, pre16, npre, D2);
+    lc[3] = cq_gather<3>(P, fc, g, pre16, npre, D3);
+    for (int i = 0; i < kMaxSteps; i++) {
+        if (!wave_any(alive)) break;
+        const float tn = t + kTStep;                                        // K:701
+        const bool cont = alive && !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, 381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
+        const FootPacked fn = pack_foot(footprint(P, nx, ny, nz), cont);
+        bool ln[4];
+        const float b0 = cq_group<0, C, TL>(P, s_lds, scr, lt, fc, lc[0], fn, ln[0], g, pre16, npre, D0);
+        const float b1 = cq_group<1, C, TL>(P, s_lds, scr, lt, fc, lc[1], fn, ln[1], g, pre16, npre, D1);
+        const float b2 = cq_group<2, C, TL>(P, s_lds, scr, lt, fc, lc[2], fn, ln[2], g, pre16, npre, D2);
+        const float b3 = cq_group<3, C, TL>(P, s_lds, scr, lt, fc, lc[3], fn, ln[3], g, pre16, npre, D3);
+        const float sample = g == 0 ? b0 : (g == 1 ? b1 : (g == 2 ? b2 : b3));
+        if (alive) {
+            n = i + 1;
+            if (composite(P, sample, sx, sy, sz, sw) || !cont) {
+                alive = false;
+            } else {
+                t = tn;
+                px = nx;
+                py = ny;
+                pz = nz;
+            }
+        }
+        fc = fn;
+#pragma unroll
+        for (int k = 0; k < 4; k++) lc[k] = ln[k];
+    }
+    if (!valid) return;
+    if (!hit) {
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 template <int B, bool COUNT>
 static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream_t s) {
     const dim3 grid(nslots), block(256);
@@ -1635,6 +1791,23 @@ static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream
                          ~(size_t)31) + (method == 6 ? 65 * sizeof(LogEnt) : 0);
     const size_t lds = cap_lds(P, P.wg_per_cu, need);
     const bool tl = P.tpl_lds != 0;
+    if constexpr (B == 8 && !COUNT) {
+        // oblique views: the quad-cooperative codec march (VR_CODEC_QUAD=0 disables)
+        const char *eq = std::getenv("VR_CODEC_QUAD");
+        if (P.oblique && !(eq && std::atoi(eq) == 0)) {
+            note_kernel("k_march_codec_quad", B, method);
+            switch (method * 2 + (tl ? 1 : 0)) {
+            case 8: hipLaunchKernelGGL((k_march_codec_quad<0, false>), grid, block, lds, s, nullptr, P); break;
+            case 9: hipLaunchKernelGGL((k_march_codec_quad<0, true>), grid, block, lds, s, nullptr, P); break;
+            case 10: hipLaunchKernelGGL((k_march_codec_quad<1, false>), grid, block, lds, s, nullptr, P); break;
+            case 11: hipLaunchKernelGGL((k_march_codec_quad<1, true>), grid, block, lds, s, nullptr, P); break;
+            case 12: hipLaunchKernelGGL((k_march_codec_quad<2, false>), grid, block, lds, s, nullptr, P); break;
+            case 13: hipLaunchKernelGGL((k_march_codec_quad<2, true>), grid, block, lds, s, nullptr, P); break;
+            default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+        }
+    }
     switch (method * 2 + (tl ? 1 : 0)) {
     case 8: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT, false>), grid, block, lds, s, nullptr, P); break;
     case 9: hipLaunchKernelGGL((k_march_codec<B, 0, COUNT, true>), grid, block, lds, s, nullptr, P); break;
