@@ -87,6 +87,31 @@ def main_flex(orc, cam):
         print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
 
 
+def gmm_scenes(cam):
+    c0, c1 = cam.single_test_inv_view(), cam.display_inv_view((30.0, 45.0))
+    return [(f"gmm14x12x10x16_{c}_m{m}", (14, 12, 10, 16), (48, 40), mat, m)
+            for c, mat in (("c0", c0), ("c1", c1)) for m in (1, 2)]
+
+
+def main_gmm(orc, cam):
+    """GMM volumes (config 5 record type): the mixture planes are
+    regenerated from the seed; their checksums pin the generator"""
+    for name, (nx, ny, nz, K), (W, H), m, method in gmm_scenes(cam):
+        wm, sg = orc.synth_gmm(nx, ny, nz, K, SEED)
+        p = orc.make_params(W, H, m, density=0.3, query_method=method)
+        r = orc.render_gmm(wm, sg, (nx, ny, nz), p)
+        n = r["out_n"]
+        np.savez_compressed(
+            os.path.join(HERE, name + ".npz"), gmm_dims=np.array([nx, ny, nz, K]),
+            seed=np.uint64(SEED),
+            wm_crc=np.uint32(np.bitwise_xor.reduce(wm.view(np.uint32).ravel())),
+            sg_crc=np.uint32(np.bitwise_xor.reduce(sg.view(np.uint32).ravel())),
+            image=np.array([W, H]), inv_view=np.asarray(m, np.float32), density=np.float32(0.3),
+            brightness=np.float32(1.0), toff=np.float32(0.0), tscale=np.float32(1.0),
+            method=np.int32(method), rgba8=r["out"], steps=n.astype(np.int16), rgba_f=r["out_f"])
+        print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
+
+
 def main():
     orc = graft.load_oracle()
     cam = graft.load_package().camera
@@ -107,7 +132,11 @@ def main():
         print(name, "hit", int(np.sum(n >= 0)), "samples", int(np.sum(n[n > 0])))
     main_codec(orc, cam)
     main_flex(orc, cam)
+    main_gmm(orc, cam)
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["gmm"]:  # only the GMM fixtures
+        main_gmm(graft.load_oracle(), graft.load_package().camera)
+    else:
+        main()

@@ -169,3 +169,24 @@ def test_gmm_errors(pkg, orc, gpu):
         pkg.synthesize_gmm(dims, 12)  # K must be 8, 16 or 32
     torch.cuda.synchronize()
     pkg.free_gmm()
+
+
+def test_gmm_golden_fixtures(pkg, gpu):
+    """the GPU march against the committed GMM fixtures (tests/golden/gmm*.npz), the
+    volume generated on the device from the fixture's seed"""
+    import glob
+    import os
+    import torch
+    files = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "gmm*.npz")))
+    assert len(files) == 4
+    for path in files:
+        z = np.load(path, allow_pickle=False)
+        nx, ny, nz, K = (int(v) for v in z["gmm_dims"])
+        pkg.synthesize_gmm((nx, ny, nz), K, seed=int(z["seed"]))
+        W, H = (int(v) for v in z["image"])
+        got = gmm_render(pkg, W, H, z["inv_view"], int(z["method"]), torch,
+                         density=float(z["density"]))
+        ref = {"out": z["rgba8"], "out_f": z["rgba_f"], "out_n": z["steps"].astype(np.int32)}
+        # out_n: the fixture holds -2 for pixels outside any ray (none here) like the render
+        check(got, ref, os.path.basename(path))
+    pkg.free_gmm()

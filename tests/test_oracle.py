@@ -180,6 +180,18 @@ def test_golden_fixture(orc, path):
         assert np.array_equal(out, z["rgba8"]) and np.array_equal(f, z["rgba_f"])
         assert np.array_equal(n, z["steps"].astype(np.int32))
         return
+    if "gmm_dims" in z.files:  # GMM volume regenerated from its seed, checksums pinned
+        nx, ny, nz, K = (int(v) for v in z["gmm_dims"])
+        wm, sg = orc.synth_gmm(nx, ny, nz, K, int(z["seed"]))
+        assert int(z["wm_crc"]) == int(np.bitwise_xor.reduce(wm.view(np.uint32).ravel()))
+        assert int(z["sg_crc"]) == int(np.bitwise_xor.reduce(sg.view(np.uint32).ravel()))
+        W, H = (int(v) for v in z["image"])
+        p = orc.make_params(W, H, z["inv_view"], float(z["density"]), float(z["brightness"]),
+                            float(z["toff"]), float(z["tscale"]), int(z["method"]))
+        r = orc.render_gmm(wm, sg, (nx, ny, nz), p)
+        assert np.array_equal(r["out"], z["rgba8"]) and np.array_equal(r["out_f"], z["rgba_f"])
+        assert np.array_equal(r["out_n"], z["steps"].astype(np.int32))
+        return
     if "codebook" in z.files:  # methods 4/5/6: inputs stored in the fixture
         W, H = (int(v) for v in z["image"])
         p = orc.make_params(W, H, z["inv_view"], float(z["density"]), float(z["brightness"]),
