@@ -121,6 +121,26 @@ def test_method7_grid_differs_from_volume(pkg, orc, gpu):
     got = gpu_render(pkg, vol, 64, 64, m, 7, torch, m7=(10, 12, 20))
     ref = orc.render(vol, orc.make_params(64, 64, m, query_method=7, m7_dims=(10, 12, 20)))[:3]
     assert_parity(got, ref, "m7 grid 10x12x20 over 16^3")
+    # B = 8, oblique, grid != volume: the quad march does not apply
+    vol8 = orc.synth_volume(16, 16, 16, 8)
+    got = gpu_render(pkg, vol8, 64, 64, m, 7, torch, m7=(10, 12, 20))
+    ref = orc.render(vol8, orc.make_params(64, 64, m, query_method=7, m7_dims=(10, 12, 20)))[:3]
+    assert_parity(got, ref, "m7 grid 10x12x20 over 16^3 x 8")
+    assert pkg.last_kernel().startswith("k_march_m7_pipe")
+
+
+def test_oblique_coarse_volume_takes_segmented_march(pkg, orc, gpu):
+    """>= 4 pixels per voxel of the x-y face on an oblique view: methods 1/2 take the
+    pipelined 2-lane segmented march, bit-identical"""
+    import torch
+    vol = orc.synth_volume(20, 18, 16, 8)
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    for method, W, H, kern in ((1, 96, 64, "k_march_segp2"), (2, 96, 64, "k_march_segp2"),
+                               (1, 32, 24, "k_march_quad")):
+        got = gpu_render(pkg, vol, W, H, m, method, torch)
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+        assert_parity(got, ref, f"coarse oblique m{method} {W}x{H}")
+        assert pkg.last_kernel().startswith(kern), pkg.last_kernel()
 
 
 def test_edge_images(pkg, orc, gpu):
