@@ -501,6 +501,17 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     if (!along_rows && g.nb == 8 && (d->query_method == 1 || d->query_method == 2) &&
         (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
         P.path = 7;
+    // Row-aligned full frames of such a coarse volume: a wave's 64 rays cover
+    // ~16 voxel columns, so staging the wave's footprint box in LDS (path 1,
+    // each record fetched and decoded once per wave) beats the one-lane
+    // pipelined march (512^3 x 8 C0 1080p: m1 1.00 -> 0.88 ms, m2 1.00 -> 0.73;
+    // it loses for entropy, oblique views, 1024^3 and launches of <= 262 K
+    // rays: profiles/r02/paths_coarse_rows.log).
+    if (along_rows && !d->d_tile_list && g.nb == 8 &&
+        (d->query_method == 1 || d->query_method == 2) &&
+        (uint64_t)d->width * d->height > seg_rays &&
+        (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
+        P.path = 1;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
         if (v >= 0 && v <= 9) P.path = v;
