@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--config", default="1024x8", choices=sorted(CONFIGS) + sorted(GMM_CONFIGS))
     ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 4, 5, 6, 7])
     ap.add_argument("--camera", default="C0", choices=["C0", "C1"])
+    ap.add_argument("--baked", action="store_true",
+                    help="basicDataProcessing first: frames filter the baked statistics "
+                         "planes (vr_stats.hip) instead of decoding records per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-balance", action="store_true",
                     help="N > 1: keep the estimate-dealt tile lists (no measured-cost re-deal)")
@@ -381,6 +384,8 @@ def main_gmm(args):
 def main():
     args = parse()
     if args.config in GMM_CONFIGS:
+        if args.baked:
+            raise SystemExit("--baked applies to the histogram / codec volumes (DESIGN.md s12)")
         return main_gmm(args)
     import torch
     import torch.distributed as dist
@@ -415,6 +420,12 @@ def main():
         pkg.synthesize_codec((n, n, n), nb, CODEC_TEMPLATES, CODEC_SLOTS, SEED)
     else:
         pkg.synthesize((n, n, n), nb, SEED)
+    bake_ms = None
+    if args.baked:  # once per volume, outside the timed frames (C:1200-1203)
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        pkg.bake_stats()
+        bake_ms = (time.perf_counter() - tb) * 1e3
 
     lists = pkg.tiles.tile_lists(W, H, world, m)
     if world > 1 and not args.no_balance:
@@ -503,8 +514,11 @@ def main():
     # under the footprints (U*S_rec; codec: codebook + used error pairs) + pixels*4
     pixels = W * H if world == 1 else int(np.sum(lists[rank] != pkg.tiles.PAD)) * 256
     u = pkg.count_footprint(desc) if args.method in (1, 2, 3) else None
-    vol_bytes = (u * nb * 4 if u is not None
-                 else pkg.footprint_bytes(desc) if args.method in (4, 5, 6) else None)
+    # baked frames read one f32 statistic per footprint voxel instead of the record
+    rec_bytes = 4 if args.baked else nb * 4
+    vol_bytes = (u * rec_bytes if u is not None
+                 else pkg.footprint_bytes(desc) if args.method in (4, 5, 6) and not args.baked
+                 else None)
     alg_bytes = (vol_bytes + pixels * 4) if vol_bytes is not None else None
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
 
@@ -545,6 +559,9 @@ def main():
                             f"{args.camera}, queryMethod {args.method}",
                 "volume": [n, n, n], "bins": nb, "image": [W, H], "camera": args.camera,
                 "query_method": args.method, "density": 0.05,
+                "statistics": ("baked once by basicDataProcessing (3 f32 planes)"
+                               if args.baked else "decoded from the records at every step"),
+                "bake_ms": round(bake_ms, 3) if bake_ms is not None else None,
                 "tile_deal": (None if world == 1 else "estimate" if args.no_balance
                               else "measured cost (one untimed frame)"),
                 "parallelism": f"image tiles x{world}" + (

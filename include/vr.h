@@ -84,9 +84,14 @@ void freeCudaBuffers(void);
 void setTextureFilterMode(bool bLinearFilter);
 
 /* Replaces basicDataProcessing, K:1798-1887.  The reference pre-bakes per-voxel
- * mean/variance/entropy into a float4 texture; this library decodes the
- * statistic from the distribution records at every step inside the march, so
- * there is nothing to pre-bake.  Validates that a volume is resident. */
+ * mean/variance/entropy of the raw volume (originalQueryTex, K:722-773) and of
+ * the codec volume (fractalQueryTex, K:775-871) into float4 textures.  Here the
+ * same statistics are baked once into three float planes per resident volume
+ * (vr_bake_stats); frames of methods 1-6 then filter the planes instead of
+ * decoding the 8 corner records at every step -- bit-identical output, 4 bytes
+ * per corner voxel read instead of a whole record.  Without it (or after
+ * vr_release_stats) the march decodes the records per step.  Errors (no
+ * volume, out of memory) go to vr_last_error(); the per-step decode stays. */
 void basicDataProcessing(void);
 
 /* Replaces dataProcessing, K:1735-1796: the flexible-block pre-pass of
@@ -101,6 +106,20 @@ void dataProcessing(void);
 #define VR_ERR_STATE -2
 #define VR_ERR_HIP -3
 #define VR_ERR_UNSUPPORTED -4
+
+/* Baked statistics (basicDataProcessing).  vr_bake_stats bakes the planes of
+ * the resident raw and codec volumes that are not baked yet: 3 planes of
+ * slice_pitch * depth floats for the raw volume (mean, variance, entropy at
+ * record index z * slice_pitch + y * row_pitch + x, vr_volume_layout) and 3
+ * planes of X * Y * Z floats for the codec volume (methods 4/5/6, dense voxel
+ * order).  Re-uploading or releasing a volume drops its planes; a volume
+ * modified in place through vr_volume_info's pointer must be re-baked
+ * (vr_release_stats, then vr_bake_stats).  vr_stats_info: device pointers
+ * (nullptr = not baked) and plane lengths in floats. */
+int vr_bake_stats(void);
+int vr_release_stats(void);
+int vr_stats_info(const float **d_raw, uint64_t *raw_plane, const float **d_codec,
+                  uint64_t *codec_plane);
 
 /* last error message ("" if none); vr_clear_error resets it */
 const char *vr_last_error(void);

@@ -1,0 +1,168 @@
+"""GPU parity of the baked-statistics path (basicDataProcessing, vr_stats.hip).
+
+basicDataProcessing bakes each voxel's mean / variance / entropy once into float
+planes (the reference's originalQueryTex / fractalQueryTex, K:722-871); frames
+of methods 1-6 then filter the planes.  Bar: the planes equal the oracle's
+per-record statistics bit for bit, and every baked frame equals the oracle's
+render (packed RGBA8 identical, float RGBA within 1e-4, samples identical).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_parity, codec_render, gpu_render
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def baked(pkg):
+    yield
+    pkg.release_stats()
+
+
+def _d2h(ptr, n):
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = np.zeros(n, np.float32)
+    torch.cuda.synchronize()
+    assert hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr),
+                         ctypes.c_size_t(out.nbytes), 2) == 0
+    return out
+
+
+@pytest.mark.parametrize("nb", [1, 3, 4, 8, 32])
+def test_planes_equal_oracle_stats(pkg, orc, gpu, baked, nb, monkeypatch):
+    """plane k at record index z*slice_pitch + y*row_pitch + x = statistic k+1 of that
+    record (orc_record_stats), bit for bit, also with padded rows / slices"""
+    monkeypatch.setenv("VR_PAD", "3,5")
+    nx, ny, nz = 9, 7, 5
+    vol = orc.synth_volume(nx, ny, nz, nb)
+    pkg.init_distribution(vol)
+    assert pkg.stats_info()[0][0] is None
+    pkg.basicDataProcessing()
+    (ptr, plane), _ = pkg.stats_info()
+    sy, sz = pkg.volume_layout()
+    assert ptr and plane == sz * nz and sy == nx + 3 and sz == sy * ny + 5
+    got = _d2h(ptr, 3 * plane).reshape(3, plane)
+    for z in range(nz):
+        for y in range(ny):
+            for x in range(nx):
+                want = orc.record_stats(vol[z, y, x])
+                have = got[:, z * sz + y * sy + x]
+                assert np.array_equal(have.view(np.uint32), want.view(np.uint32)), (x, y, z)
+
+
+@pytest.mark.parametrize("nb", [1, 4, 5, 8, 32])
+def test_baked_render_parity(pkg, orc, gpu, baked, nb):
+    """methods 1/2/3 on both cameras from the baked planes: the oracle's frame"""
+    import torch
+    vol = orc.synth_volume(24, 20, 16, nb)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    for cam in ("C0", "C1"):
+        m = pkg.camera.single_test_inv_view() if cam == "C0" else pkg.camera.display_inv_view()
+        for method in (1, 2, 3):
+            got = gpu_render(pkg, None, 96, 72, m, method, torch)
+            ref = orc.render(vol, orc.make_params(96, 72, m, query_method=method))[:3]
+            assert_parity(got, ref, f"baked 24x20x16x{nb} {cam} m{method}")
+            want = "k_march_pipe<B=1,M=0>" if cam == "C0" else "k_march_seg4<B=1,M=0>"
+            assert pkg.last_kernel() == want, pkg.last_kernel()
+
+
+@pytest.mark.parametrize("path,env", [
+    ("1", {}), ("1", {"VR_BOX_MAX": "64"}), ("7", {"VR_SEG": "-2"}), ("7", {"VR_SEG": "4"}),
+    ("7", {"VR_SEG": "-8"}), ("2", {"VR_WG_PER_CU": "2"}), ("7", {"VR_SEG": "1"}),
+])
+def test_baked_paths(pkg, orc, gpu, baked, path, env, monkeypatch):
+    """every kernel a baked frame can take (VR_PATH 1 / 2 / 7) is bit-identical"""
+    import torch
+    monkeypatch.setenv("VR_PATH", path)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    vol = orc.synth_volume(20, 18, 16, 8)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))):
+        for method in (1, 3):
+            got = gpu_render(pkg, None, 80, 64, cam, method, torch)
+            ref = orc.render(vol, orc.make_params(80, 64, cam, query_method=method))[:3]
+            assert_parity(got, ref, f"baked path {path} {env} m{method}")
+            assert "M=0" in pkg.last_kernel() or "M=-1" in pkg.last_kernel(), pkg.last_kernel()
+
+
+def test_baked_tile_lists(pkg, orc, gpu, baked):
+    """multi-GPU tile lists over the baked planes (segmented march for short lists):
+    packed tiles unscatter to the oracle's frame"""
+    import torch
+    vol = orc.synth_volume(20, 18, 16, 8)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    W, H, world = 130, 70, 3
+    m = pkg.camera.single_test_inv_view()
+    lists = pkg.tiles.tile_lists(W, H, world)
+    n_slots = lists.shape[1]
+    packed = torch.full((world, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    for r in range(world):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=2, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+        assert "M=0" in pkg.last_kernel()
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    ref = orc.render(vol, orc.make_params(W, H, m, query_method=2), want_float=False,
+                     want_steps=False)[0]
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref)
+
+
+@pytest.mark.parametrize("nb", [4, 8, 32])
+def test_baked_codec(pkg, orc, gpu, baked, nb):
+    """methods 4/5/6: codec voxels decoded once into planes (fractalQueryTex, K:775-871)"""
+    import torch
+    cb, t, e = orc.synth_codec(22, 18, 14, nb, seed=nb)
+    pkg.init_codec(cb, t, e)
+    pkg.basicDataProcessing()
+    _, (ptr, plane) = pkg.stats_info()
+    assert ptr and plane == 22 * 18 * 14
+    got = _d2h(ptr, 3 * plane).reshape(3, plane)
+    for v in range(0, plane, 7):
+        want = orc.codec_stats(cb, t, e, v)
+        assert np.array_equal(got[:, v].view(np.uint32), want.view(np.uint32)), v
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view()):
+        for method in (4, 5, 6):
+            got_f = codec_render(pkg, 72, 56, cam, method, torch)
+            ref = orc.render_codec(cb, t, e, orc.make_params(72, 56, cam, query_method=method))[:3]
+            assert_parity(got_f, ref, f"baked codec nb={nb} m{method}")
+            assert "B=1,M=0>" in pkg.last_kernel(), pkg.last_kernel()
+
+
+def test_release_reupload_and_errors(pkg, orc, gpu, baked):
+    """release_stats returns to the per-step decode; a new volume drops stale planes;
+    methods 7 / 8 / 9 / 0 never read the planes; no volume -> VRError"""
+    import torch
+    vol = orc.synth_volume(16, 16, 16, 8)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    m = pkg.camera.single_test_inv_view()
+    gpu_render(pkg, None, 64, 48, m, 1, torch)
+    assert pkg.last_kernel() == "k_march_pipe<B=1,M=0>"
+    got = gpu_render(pkg, None, 64, 48, m, 7, torch, m7=(16, 16, 16))
+    ref = orc.render(vol, orc.make_params(64, 48, m, query_method=7, m7_dims=(16, 16, 16)))[:3]
+    assert_parity(got, ref, "m7 with baked planes resident")
+    assert "M=7" in pkg.last_kernel()
+    pkg.release_stats()
+    assert pkg.stats_info()[0][0] is None
+    gpu_render(pkg, None, 64, 48, m, 1, torch)
+    assert "M=1" in pkg.last_kernel()
+    pkg.bake_stats()
+    vol2 = orc.synth_volume(12, 10, 8, 4, seed=7)
+    pkg.init_distribution(vol2)  # re-upload: the old planes must not be used
+    assert pkg.stats_info()[0][0] is None
+    got = gpu_render(pkg, None, 64, 48, m, 1, torch)
+    ref = orc.render(vol2, orc.make_params(64, 48, m, query_method=1))[:3]
+    assert_parity(got, ref, "re-uploaded volume")
+    pkg.freeCudaBuffers()
+    with pytest.raises(pkg.VRError):
+        pkg.bake_stats()

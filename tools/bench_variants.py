@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--cameras", default="C0,C1")
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--variants", default="")
+    ap.add_argument("--baked", action="store_true",
+                    help="bake the statistics planes (basicDataProcessing) before timing")
     ap.add_argument("--pads", nargs="*", default=[""],
                     help="VR_PAD layouts to synthesize in turn, e.g. '' '4,0' '4,64'")
     ap.add_argument("--env", nargs="*", default=[""],
@@ -74,6 +76,9 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
     first.vr_volume_info(None, None, ctypes.byref(ptr))
     for L in list(libs.values())[1:]:  # other variants adopt the same (dense) volume
         assert L.vr_init_distribution(ptr, ext, nb, 2) == 0
+    if args.baked:
+        for L in libs.values():
+            assert L.vr_bake_stats() == 0, L.vr_last_error()
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     cams = {"C0": pkg.camera.single_test_inv_view(),
             "C1": pkg.camera.display_inv_view((30.0, 45.0))}
@@ -113,7 +118,8 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
         print(f"round {rnd} done", file=sys.stderr, flush=True)
     os.environ.clear()
     os.environ.update(base_env)
-    print(f"config {args.config} method {args.method} pad '{pad}'")
+    print(f"config {args.config} method {args.method} pad '{pad}'"
+          + (" baked" if args.baked else ""))
     for i, (name, env, cam) in enumerate(configs):
         t = np.array(times[i])
         envs_s = ",".join(f"{k}={v}" for k, v in env.items()) or "-"

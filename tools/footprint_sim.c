@@ -24,7 +24,12 @@ static int ALIGN = 0; /* 1: per-step scopes count a ray's sample s at iteration 
 static int LAYOUT = 0; /* 0: x-rows (4 records along x per line), 1: 2x2 (x,y) micro-bricks,
                           2: 2x1x2 (x,z) micro-bricks */
 
+/* LAYOUT=10: baked statistics planes, 4-B voxels, 32 per line, bricks of
+   BX x BY x BZ voxels (BX*BY*BZ = 32; default 32x1x1 = x-rows) */
+static uint32_t BX = 32, BY = 1, BZ = 1;
 static uint32_t line_of(uint32_t x, uint32_t y, uint32_t z) {
+    if (LAYOUT == 10)
+        return (uint32_t)(((uint64_t)(z / BZ) * (N / BY) + y / BY) * (N / BX) + x / BX);
     if (LAYOUT == 1)
         return (uint32_t)(((uint64_t)z * (N / 2) + (y >> 1)) * (N / 2) + (x >> 1));
     if (LAYOUT == 2)
@@ -104,6 +109,9 @@ int main(int argc, char **argv) {
     if (getenv("LAYOUT")) LAYOUT = atoi(getenv("LAYOUT"));
     if (getenv("PF")) PF = atoi(getenv("PF"));
     if (getenv("ALIGN")) ALIGN = atoi(getenv("ALIGN"));
+    if (getenv("BRICK") && sscanf(getenv("BRICK"), "%ux%ux%u", &BX, &BY, &BZ) == 3 &&
+        BX * BY * BZ != 32)
+        return 2;
     FILE *f = fopen(argv[1], "rb");
     if (!f) return 1;
     int32_t *steps = malloc(sizeof(int32_t) * W * H);

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--no-lpt", action="store_true", help="tile lists without longest-first order")
+    ap.add_argument("--baked", action="store_true", help="bake the statistics planes first")
+    ap.add_argument("--env", default="", help="NAME=VALUE[,NAME=VALUE] set for the renders")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
@@ -31,6 +33,11 @@ def main():
     pkg = g.load_package()
     n, nb, W, H = bench.CONFIGS[args.config]
     pkg.synthesize((n, n, n), nb, bench.SEED)
+    if args.baked:
+        pkg.bake_stats()
+    for kv in filter(None, args.env.split(",")):
+        k, v = kv.split("=")
+        os.environ[k] = v
     m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
          else pkg.camera.display_inv_view((30.0, 45.0)))
 

@@ -97,7 +97,7 @@ EXPORTS = [
     "vr_parse_span_list", "vr_parse_fractal_histogram", "vr_parse_simple_histogram",
     "vr_load_flex_files", "vr_debug_wave_clock",
     "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_render_gmm",
-    "vr_gmm_count_footprint",
+    "vr_gmm_count_footprint", "vr_bake_stats", "vr_release_stats", "vr_stats_info",
 ]
 
 _lib = None
@@ -206,6 +206,12 @@ def load() -> ctypes.CDLL:
     L.vr_render_gmm.restype = i32
     L.vr_gmm_count_footprint.argtypes = [ctypes.POINTER(RenderDesc)]
     L.vr_gmm_count_footprint.restype = ctypes.c_int64
+    L.vr_bake_stats.argtypes = []
+    L.vr_bake_stats.restype = i32
+    L.vr_release_stats.argtypes = []
+    L.vr_release_stats.restype = i32
+    L.vr_stats_info.argtypes = [vp] * 4
+    L.vr_stats_info.restype = i32
     _lib = L
     return L
 

@@ -229,9 +229,30 @@ def setTextureFilterMode(bLinearFilter: bool) -> None:
 
 
 def basicDataProcessing() -> None:
-    """basicDataProcessing, K:1798-1887: nothing to pre-bake (decoded per step)."""
+    """basicDataProcessing, K:1798-1887: bakes the per-voxel statistics of the resident
+    raw / codec volumes (originalQueryTex / fractalQueryTex, K:722-871) into float
+    planes; methods 1-6 then filter the planes (bit-identical to the per-step decode)."""
     _lib.load().basicDataProcessing()
     check_last()
+
+
+def bake_stats() -> None:
+    """vr_bake_stats: basicDataProcessing with a status (raises VRError)."""
+    check(_lib.load().vr_bake_stats())
+
+
+def release_stats() -> None:
+    """Drop the baked planes: methods 1-6 decode the records per step again."""
+    check(_lib.load().vr_release_stats())
+
+
+def stats_info():
+    """((d_raw, raw_plane_floats), (d_codec, codec_plane_floats)); pointer None = not baked"""
+    a, c = ctypes.c_void_p(), ctypes.c_void_p()
+    na, nc = ctypes.c_uint64(), ctypes.c_uint64()
+    check(_lib.load().vr_stats_info(ctypes.byref(a), ctypes.byref(na), ctypes.byref(c),
+                                    ctypes.byref(nc)))
+    return (a.value, na.value), (c.value, nc.value)
 
 
 def dataProcessing() -> None:
@@ -450,6 +471,6 @@ __all__ = [
     "volume_layout",
     "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "version",
     "init_gmm", "synthesize_gmm", "gmm_info", "free_gmm", "gmm_slab", "render_gmm",
-    "gmm_count_footprint",
+    "gmm_count_footprint", "bake_stats", "release_stats", "stats_info",
     "VRError", "PAD",
 ]

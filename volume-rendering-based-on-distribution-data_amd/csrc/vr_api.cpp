@@ -63,6 +63,12 @@ struct State {
         bool owned = false;
         int nx = 0, ny = 0, nz = 0, K = 0, z_base = 0, nzs = 0;
     } gmm;
+    // baked statistics (basicDataProcessing / vr_bake_stats, vr_stats.hip):
+    // three planes of stats_plane floats for the raw volume (methods 1/2/3) and
+    // of cstats_plane floats for the codec volume (methods 4/5/6); nullptr =
+    // not baked, the march decodes the records at every step
+    float *stats = nullptr, *cstats = nullptr;
+    uint64_t stats_plane = 0, cstats_plane = 0;
     // bumped whenever a resident volume / codec / flexible-block set is
     // released, so an order learned on old data is not reused (the order is a
     // scheduling hint only: any order renders the same image)
@@ -92,7 +98,20 @@ int hip_fail(hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_fail(e_, #call);   \
     } while (0)
 
+void release_stats() {
+    if (g.stats) (void)hipFree(g.stats);
+    g.stats = nullptr;
+    g.stats_plane = 0;
+}
+
+void release_cstats() {
+    if (g.cstats) (void)hipFree(g.cstats);
+    g.cstats = nullptr;
+    g.cstats_plane = 0;
+}
+
 void release_volume() {
+    release_stats();
     g.volume_epoch++;
     if (g.vol && g.owned) (void)hipFree(g.vol);
     g.vol = nullptr;
@@ -127,6 +146,7 @@ uint32_t tiles_x(uint32_t w) { return (w + vr::kTileW - 1) / vr::kTileW; }
 uint32_t tiles_y(uint32_t h) { return (h + vr::kTileH - 1) / vr::kTileH; }
 
 void release_codec() {
+    release_cstats();
     g.volume_epoch++;
     if (g.cb) (void)hipFree(g.cb);
     if (g.tpl) (void)hipFree(g.tpl);
@@ -384,6 +404,13 @@ void device_lds(int &per_cu, int &per_wg) {
     per_wg = wg;
 }
 
+// gather8's 32-bit addressing of a baked plane: pitches and depth fit 24-bit
+// multiplies and the byte offset of every element fits 32 bits (a 1024^3 plane,
+// 2^30 floats, does: the last element sits at 2^32 - 4)
+int narrow_index(uint64_t sy, uint64_t sz, uint64_t nz) {
+    return sy < (1u << 24) && sz < (1u << 24) && nz < (1u << 24) && sz * nz <= (1ull << 30);
+}
+
 int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
                 bool for_render = false) {
     if (!d) return fail(VR_ERR_ARG, "null render descriptor");
@@ -539,6 +566,92 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
             P.path = 9;
             P.hyb_tiles = (int)std::min<uint64_t>((uint64_t)k & ~7ull, nslots & ~7u);
         }
+    }
+    return VR_OK;
+}
+
+// Kernel of a baked-statistics frame (measured at 512^3 and 1024^3 x 8, 1080p,
+// profiles/r02/baked_paths.log).  A baked step is a few dozen VALU operations
+// and 4 pair loads, so the frame is bound by gather issue and line traffic,
+// not by decode: row-aligned views take the one-lane pipelined march (path 2,
+// 1024^3 C0 0.375 ms); oblique views, whose lanes' loads touch many lines per
+// instruction, split each ray over 4 lanes (path 7, VR_SEG 4: 1024^3 C1 2.02
+// -> 1.32 ms).  A deeper look-ahead ring (2-8 steps in flight per lane) was
+// slower everywhere but 512^3 C1 (within 3 %).  VR_PATH (1 / 2 / 7) overrides;
+// P.seg_lanes keeps a VR_SEG setting.
+int baked_path(const vr_render_desc *d, vr::Params &P) {
+    const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
+    int path = along_rows ? 2 : 7;
+    int seg = 4;
+    // A rank's tile list (multi-GPU) has few rays, so its longest step chains
+    // set the time: row-aligned lists split rays too (cost-dealt 1024^3 C0
+    // lists, max over ranks: N = 4 (~520 K rays) pipelined 2-lane windows
+    // 0.149 ms vs 0.185 one-lane, N = 8 (~260 K) 4 lanes 0.105 vs 0.165;
+    // N = 2 stays one-lane, 0.233 vs 0.281; tools/rank_sim.py --baked).
+    if (along_rows && d->d_tile_list) {
+        const uint64_t rays = (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH;
+        if (rays <= 400000) path = 7;
+        else if (rays <= 700000) path = 7, seg = -2;
+    }
+    if (path == 7 && !std::getenv("VR_SEG")) P.seg_lanes = seg;
+    if (const char *e = std::getenv("VR_PATH")) {
+        const int v = std::atoi(e);
+        if (v == 1 || v == 2 || v == 7) path = v;
+    }
+    return path;
+}
+
+// Bakes the statistics planes of the resident raw and codec volumes (whichever
+// are resident and not yet baked).  On an allocation failure nothing changes:
+// the march keeps decoding records per step.
+int bake_stats() {
+    if (!g.vol && !g.cb) return fail(VR_ERR_STATE, "no volume resident (initCuda / vr_init_* first)");
+    vr::Params P;
+    std::memset(&P, 0, sizeof P);
+    if (g.vol && !g.stats) {
+        P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
+        P.sy = g.sy; P.sz = g.sz;
+        P.nb = g.nb;
+        P.enorm = entropy_norm(g.nb);
+        const uint64_t plane = g.sz * (uint64_t)g.nz;
+        float *buf = nullptr;  // + 4 floats: the pair loads of the march read x0 + 1
+        VR_HIP(hipMalloc(&buf, (3 * plane + 4) * sizeof(float)));
+        hipError_t e = hipMemsetAsync(buf, 0, (3 * plane + 4) * sizeof(float), g.stream);
+        if (e == hipSuccess) e = vr::launch_bake_raw(g.vol, P, buf, plane, g.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+        if (e != hipSuccess) {
+            (void)hipFree(buf);
+            return hip_fail(e, "basicDataProcessing(k_bake_raw)");
+        }
+        g.stats = buf;
+        g.stats_plane = plane;
+    }
+    if (g.cb && !g.cstats) {
+        std::memset(&P, 0, sizeof P);
+        P.nx = g.cnx; P.ny = g.cny; P.nz = g.cnz;
+        P.sy = (uint64_t)g.cnx;
+        P.sz = (uint64_t)g.cnx * (uint64_t)g.cny;
+        P.nb = g.cnb;
+        P.enorm = entropy_norm(g.cnb);
+        P.cb = g.cb;
+        P.tpl = g.tpl;
+        P.err = g.cerr;
+        P.ntpl = g.ntpl;
+        P.err_slots = g.err_slots;
+        const uint64_t plane = P.sz * (uint64_t)g.cnz;
+        float *buf = nullptr;  // + 4 floats as above
+        VR_HIP(hipMalloc(&buf, (3 * plane + 4) * sizeof(float)));
+        hipError_t e = hipMemsetAsync(buf, 0, (3 * plane + 4) * sizeof(float), g.stream);
+        if (e == hipSuccess) e = vr::launch_bake_codec(P, buf, plane, g.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+        if (e != hipSuccess) {
+            (void)hipFree(buf);
+            if (e == hipErrorInvalidValue)
+                return fail(VR_ERR_UNSUPPORTED, "baking codec volumes with %d bins", g.cnb);
+            return hip_fail(e, "basicDataProcessing(k_bake_codec)");
+        }
+        g.cstats = buf;
+        g.cstats_plane = plane;
     }
     return VR_OK;
 }
@@ -1044,7 +1157,17 @@ int vr_render(const vr_render_desc *desc) {
     int rc = fill_params(desc, P, nslots, true);
     if (rc != VR_OK) return rc;
     hipError_t e;
-    if (is_flex_method(desc->query_method)) {
+    const int qm = desc->query_method;
+    const float *baked = (qm >= 1 && qm <= 3 && g.stats)   ? g.stats + (uint64_t)(qm - 1) * g.stats_plane
+                         : (qm >= 4 && qm <= 6 && g.cstats) ? g.cstats + (uint64_t)(qm - 4) * g.cstats_plane
+                                                            : nullptr;
+    if (baked) {
+        // one float per corner voxel, the same filter and composite (vr_stats.hip)
+        P.nb = 1;
+        P.path = baked_path(desc, P);
+        const bool narrow = narrow_index(P.sy, P.sz, (uint64_t)P.nz);
+        e = vr::launch_march(1, narrow ? 0 : -1, baked, P, nslots, false, g.stream);
+    } else if (is_flex_method(desc->query_method)) {
         e = vr::launch_march_flex(desc->query_method, P, nslots, g.stream);
     } else if (desc->query_method >= 4 && desc->query_method <= 6) {
         e = vr::launch_march_codec(P.nb, desc->query_method, P, nslots, false, g.stream);
@@ -1488,7 +1611,27 @@ void freeCudaBuffers(void) {
 void setTextureFilterMode(bool bLinearFilter) { g.linear_filter = bLinearFilter; }
 
 void basicDataProcessing(void) {
-    if (!g.vol) fail(VR_ERR_STATE, "basicDataProcessing: no volume resident");
+    // d_basicDataProcessing (K:1798-1887) fills originalQueryTex / fractalQueryTex
+    // once; here the planes of vr_stats.hip.  Errors go to vr_last_error(); a
+    // failed bake leaves the per-step decode in place.
+    (void)bake_stats();
+}
+
+int vr_bake_stats(void) { return bake_stats(); }
+
+int vr_release_stats(void) {
+    release_stats();
+    release_cstats();
+    return VR_OK;
+}
+
+int vr_stats_info(const float **d_raw, uint64_t *raw_plane, const float **d_codec,
+                  uint64_t *codec_plane) {
+    if (d_raw) *d_raw = g.stats;
+    if (raw_plane) *raw_plane = g.stats_plane;
+    if (d_codec) *d_codec = g.cstats;
+    if (codec_plane) *codec_plane = g.cstats_plane;
+    return VR_OK;
 }
 
 void dataProcessing(void) {

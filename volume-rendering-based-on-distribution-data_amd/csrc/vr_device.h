@@ -362,10 +362,15 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
     return ent / enorm;
 }
 
-// the statistic a method samples, K:758-769 (M: 1 mean, 2 variance, 3 entropy)
+// the statistic a method samples, K:758-769 (M: 1 mean, 2 variance, 3 entropy;
+// 0 / -1: the record is a statistic already baked by basicDataProcessing, B = 1,
+// gathered with 32-bit / 64-bit addressing, vr_march.h gather8)
 template <int B, int M>
 __device__ __forceinline__ float record_stat(const float (&p)[B], float enorm) {
-    if constexpr (M == 1) {
+    if constexpr (M <= 0) {
+        static_assert(B == 1, "baked statistics are one float per voxel");
+        return p[0];
+    } else if constexpr (M == 1) {
         return div_to_float(raw_mean<B>(p), kMeanR);
     } else if constexpr (M == 2) {
         const float mean = raw_mean<B>(p);

@@ -80,6 +80,11 @@ hipError_t launch_march_gmm(int K, int method, const Params &P, uint32_t nblocks
                             hipStream_t s);
 hipError_t launch_synth_gmm(float *wm, float *sg, const SynthArgs &a, int K, int z_base, int nzs,
                             hipStream_t s);
+// ---- baked statistics (basicDataProcessing, vr_stats.hip): three planes of
+// `plane` floats each, statistic k+1 (raw) / C = k (codec) at the volume's record index
+hipError_t launch_bake_raw(const float *vol, const Params &P, float *out, uint64_t plane,
+                           hipStream_t s);
+hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,

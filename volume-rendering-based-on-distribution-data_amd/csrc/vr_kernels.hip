@@ -2146,9 +2146,24 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             return hipGetLastError();
         }
         if (B < 8 && P.path == 0) P.path = 2;  // per-ray pipelined for narrow records
-        if (P.path == 2 && method >= 1 && method <= 3) {
+        if constexpr (B == 1) {  // baked statistics (vr_stats.hip): paths 1, 2, 7 only
+            if (method <= 0 && P.path != 1) P.path = 2;
+        }
+        if (P.path == 2 && method >= -1 && method <= 3) {
             note_kernel("k_march_pipe", B, method);
             switch (method) {
+            case 0:
+                if constexpr (B == 1) {
+                    hipLaunchKernelGGL((k_march_pipe<1, 0>), grid, block, occupancy_lds(P), s, vol, P);
+                    break;
+                }
+                return hipErrorInvalidValue;
+            case -1:
+                if constexpr (B == 1) {
+                    hipLaunchKernelGGL((k_march_pipe<1, -1>), grid, block, occupancy_lds(P), s, vol, P);
+                    break;
+                }
+                return hipErrorInvalidValue;
             case 1: hipLaunchKernelGGL((k_march_pipe<B, 1>), grid, block, occupancy_lds(P), s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_pipe<B, 2>), grid, block, occupancy_lds(P), s, vol, P); break;
             case 3: hipLaunchKernelGGL((k_march_pipe<B, 3>), grid, block, occupancy_lds(P), s, vol, P); break;
@@ -2158,6 +2173,13 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     }
     if (!COUNT) note_kernel(method == 7 ? "k_march_m7" : "k_march", B, method);
     switch (method) {
+    case 0:
+    case -1:  // baked statistics: the box / direct march addresses in 64 bits either way
+        if constexpr (B == 1 && !COUNT) {
+            hipLaunchKernelGGL((k_march<1, -1, false>), grid, block, lds, s, vol, P);
+            break;
+        }
+        return hipErrorInvalidValue;
     case 1: hipLaunchKernelGGL((k_march<B, 1, COUNT>), grid, block, lds, s, vol, P); break;
     case 2: hipLaunchKernelGGL((k_march<B, 2, COUNT>), grid, block, lds, s, vol, P); break;
     case 3: hipLaunchKernelGGL((k_march<B, 3, COUNT>), grid, block, lds, s, vol, P); break;

@@ -149,9 +149,59 @@ __device__ __forceinline__ float blend8(const float (&s)[8], const Foot &f) {
     const float c1 = lerpq(c01, c11, f.ay);
     return lerpq(c0, c1, f.az);
 }
-template <int B>
+// NARROW (the baked statistics planes, B = 1, method template 0): indices
+// from 24-bit multiplies and loads at a 32-bit byte offset from the uniform
+// base (global_load with an SGPR base) instead of 64-bit address arithmetic
+// per corner -- the march over a baked plane is VALU-heavy, its records are 4
+// bytes.  The caller guarantees pitches and depth < 2^24 and every byte offset
+// < 2^32 (vr_api.cpp narrow_index).
+__device__ __forceinline__ float load_at(const float *__restrict__ vol, uint32_t i) {
+    return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(vol) + (i << 2));
+}
+// statistics i and i+1 in one 8-byte load at 4-byte alignment (one address per
+// lane for both x corners; the plane is allocated one float long so i+1 exists)
+typedef float vr_f2a4 __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ vr_f2a4 load_pair(const float *__restrict__ vol, uint32_t i) {
+    return *reinterpret_cast<const vr_f2a4 *>(reinterpret_cast<const char *>(vol) + (i << 2));
+}
+template <int B, bool NARROW = false>
 __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Params &P,
                                         const Foot &f, float (&rec)[8][B]) {
+    if constexpr (NARROW) {
+        static_assert(B == 1, "narrow addressing is for one-float records");
+        {
+            const uint32_t sy = (uint32_t)P.sy, sz = (uint32_t)P.sz;
+            const uint32_t i0 = __umul24((uint32_t)f.z0, sz) + __umul24((uint32_t)f.y0, sy) +
+                                (uint32_t)f.x0;
+            const uint32_t ox = (uint32_t)(f.x1 - f.x0);
+            const uint32_t oy = __umul24((uint32_t)(f.y1 - f.y0), sy);
+            const uint32_t oz = __umul24((uint32_t)(f.z1 - f.z0), sz);
+#ifdef VR_BAKED_SINGLE  // A/B builds only: one 4-byte load per corner
+            rec[0][0] = load_at(vol, i0);
+            rec[1][0] = load_at(vol, i0 + ox);
+            rec[2][0] = load_at(vol, i0 + oy);
+            rec[3][0] = load_at(vol, i0 + oy + ox);
+            rec[4][0] = load_at(vol, i0 + oz);
+            rec[5][0] = load_at(vol, i0 + oz + ox);
+            rec[6][0] = load_at(vol, i0 + oz + oy);
+            rec[7][0] = load_at(vol, i0 + oz + oy + ox);
+#else
+            // x corners as one pair load per (y, z) row: half the gather
+            // instructions; x1 == x0 (clamped edge) takes the pair's first value
+            const vr_f2a4 a = load_pair(vol, i0), b = load_pair(vol, i0 + oy);
+            const vr_f2a4 c = load_pair(vol, i0 + oz), d = load_pair(vol, i0 + oz + oy);
+            rec[0][0] = a.x;
+            rec[1][0] = ox ? a.y : a.x;
+            rec[2][0] = b.x;
+            rec[3][0] = ox ? b.y : b.x;
+            rec[4][0] = c.x;
+            rec[5][0] = ox ? c.y : c.x;
+            rec[6][0] = d.x;
+            rec[7][0] = ox ? d.y : d.x;
+#endif
+            return;
+        }
+    }
     const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
     const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
     const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
@@ -205,7 +255,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
     bool alive = true;
     Foot fa = footprint(P, px, py, pz), fb;
     float ra[8][B], rb[8][B];
-    gather8<B>(vol, P, fa, ra);
+    gather8<B, M == 0>(vol, P, fa, ra);
     // one step: decode (fc, rc) while the gathers of the next step go to (fn, rn)
     auto step = [&](int i, const Foot &fc, const float (&rc)[8][B], Foot &fn,
                     float (&rn)[8][B]) {
@@ -221,7 +271,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
         // footprint instead -- cache hits -- measured 2.4 ms against 1.36:
         // the select changed the schedule again.)
         fn = footprint(P, nx, ny, nz);
-        gather8<B>(vol, P, fn, rn);
+        gather8<B, M == 0>(vol, P, fn, rn);
         const float sample = decode8<B, M>(P, rc, fc);
         n = i + 1;
         if (composite(P, sample, sx, sy, sz, sw) || !cont) {

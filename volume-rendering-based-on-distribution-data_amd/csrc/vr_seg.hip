@@ -123,7 +123,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
             if (valid) {
                 const Foot f = footprint(P, px, py, pz);
                 float rec[8][B];
-                gather8<B>(vol, P, f, rec);
+                gather8<B, M == 0>(vol, P, f, rec);
                 smp = decode8<B, M>(P, rec, f);
             }
             const uint64_t vm = __ballot(valid);
@@ -138,7 +138,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
         bool va = geom((int)k, t), vb = false;
         if (va) {
             fa = footprint(P, px, py, pz);
-            gather8<B>(vol, P, fa, ra);
+            gather8<B, M == 0>(vol, P, fa, ra);
         }
         // one window: gather the next into (fn, rn, vn) while (fc, rc, vc) decodes
         auto window = [&](const Foot &fc, const float (&rc)[8][B], bool vc, Foot &fn,
@@ -148,7 +148,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
             vn = alive && geom(base + S + (int)k, tn);
             if (vn) {
                 fn = footprint(P, nx, ny, nz);
-                gather8<B>(vol, P, fn, rn);
+                gather8<B, M == 0>(vol, P, fn, rn);
             }
             float smp = 0.0f;
             if (vc && alive) smp = decode8<B, M>(P, rc, fc);
@@ -259,6 +259,18 @@ static hipError_t seg_launch(int method, const float *vol, const Params &P, uint
                              hipStream_t s) {
     const dim3 grid(((nslots + 7u) / 8u) * 8u * S), block(256);
     switch (method) {
+    case 0:  // baked statistics, one float per voxel (vr_stats.hip), 32-bit offsets
+        if constexpr (B == 1) {
+            hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P);
+            break;
+        }
+        return hipErrorInvalidValue;
+    case -1:  // baked, 64-bit offsets
+        if constexpr (B == 1) {
+            hipLaunchKernelGGL((k_march_seg<1, -1, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P);
+            break;
+        }
+        return hipErrorInvalidValue;
     case 1: hipLaunchKernelGGL((k_march_seg<B, 1, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P); break;
     case 2: hipLaunchKernelGGL((k_march_seg<B, 2, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P); break;
     case 3: hipLaunchKernelGGL((k_march_seg<B, 3, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P); break;
@@ -286,7 +298,7 @@ static bool seg_b(int method, int S, const float *vol, const Params &P, uint32_t
 
 bool launch_march_seg(int nb, int method, int S, const float *vol, const Params &P,
                       uint32_t nslots, hipStream_t s, hipError_t &err) {
-    if (method < 1 || method > 3) return false;
+    if (method < (nb == 1 ? -1 : 1) || method > 3) return false;
     bool ok = false;
     switch (nb) {
     case 1: ok = seg_b<1>(method, S, vol, P, nslots, s, err); break;

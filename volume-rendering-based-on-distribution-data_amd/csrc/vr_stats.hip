@@ -1,0 +1,104 @@
+// vr_stats.hip -- basicDataProcessing (K:1798-1887): per-voxel statistics baked
+// once into float planes, the build's counterpart of the reference's
+// originalQueryTex / fractalQueryTex (d_basicDataProcessing, K:722-871).
+//
+// The march decodes a statistic from the 8 corner records of every sample
+// (methods 1-6); that statistic is a pure function of one
+// record, so decoding it once per voxel into a plane and blending the plane's
+// 8 corners with the same filter gives the same float for every sample, bit
+// for bit.  A baked frame reads 4 bytes per corner voxel instead of B * 4
+// (raw records) or a codebook entry + errors (codec), so the march is no
+// longer bound by the distribution bytes.  Planes use the volume's pitches:
+// plane k of the raw volume holds statistic k+1 at record index
+// z * slice_pitch + y * row_pitch + x (the codec volume: dense voxel order).
+#include "vr_internal.h"
+
+namespace vr {
+
+// One thread per voxel of an x-row (grid: x blocks of 256, y rows, z slices);
+// each record is read once, coalesced, and its three statistics written to
+// the three planes.  The same functions as the march (record_stat), so the
+// planes hold exactly the per-corner values the march would decode; the
+// entropy's exact logarithm uses the LDS table (both logarithm forms are
+// exact, vr_selftest_logf).
+template <int B>
+__global__ __launch_bounds__(256) void k_bake_raw(const float *__restrict__ vol, Params P,
+                                                  float *__restrict__ out, uint64_t plane) {
+    __shared__ LogEnt tab[65];
+    copy_logtab(tab);
+    __syncthreads();
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    if (x >= (uint32_t)P.nx) return;
+    const uint64_t off = (uint64_t)blockIdx.z * P.sz + (uint64_t)blockIdx.y * P.sy + x;
+    float m, v, e;
+    if constexpr (B > 0) {
+        float p[B];
+        load_rec<B>(vol, off, p);
+        m = record_stat<B, 1>(p, P.enorm);
+        v = record_stat<B, 2>(p, P.enorm);
+        e = entropy_p<B>(p, P.enorm, tab);
+    } else {
+        const float *p = vol + off * (uint64_t)P.nb;
+        m = record_stat_rt<1>(p, P.nb, P.enorm);
+        v = record_stat_rt<2>(p, P.nb, P.enorm);
+        e = record_stat_rt<3>(p, P.nb, P.enorm);
+    }
+    out[off] = m;
+    out[plane + off] = v;
+    out[2 * plane + off] = e;
+}
+
+// codec voxels (methods 4/5/6, K:775-871): decode once, statistics C = 0, 1, 2
+template <int B>
+__global__ __launch_bounds__(256) void k_bake_codec(Params P, float *__restrict__ out,
+                                                    uint64_t plane) {
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    if (x >= (uint32_t)P.nx) return;
+    const uint64_t off = (uint64_t)blockIdx.z * P.sz + (uint64_t)blockIdx.y * P.sy + x;
+    float dec[B];
+    codec_decode<B>(P, off, dec);
+    out[off] = codec_stat_of<B, 0>(dec, P.enorm);
+    out[plane + off] = codec_stat_of<B, 1>(dec, P.enorm);
+    out[2 * plane + off] = codec_stat_of<B, 2>(dec, P.enorm);
+}
+
+static bool bake_grid(const Params &P, dim3 &grid) {
+    if (P.nx <= 0 || P.ny <= 0 || P.nz <= 0 || P.ny > 65535 || P.nz > 65535) return false;
+    grid = dim3((uint32_t)(P.nx + 255) / 256u, (uint32_t)P.ny, (uint32_t)P.nz);
+    return true;
+}
+
+hipError_t launch_bake_raw(const float *vol, const Params &P, float *out, uint64_t plane,
+                           hipStream_t s) {
+    dim3 grid;
+    if (!bake_grid(P, grid)) return hipErrorInvalidValue;
+    const dim3 block(256);
+    switch (P.nb) {
+    case 1: hipLaunchKernelGGL((k_bake_raw<1>), grid, block, 0, s, vol, P, out, plane); break;
+    case 2: hipLaunchKernelGGL((k_bake_raw<2>), grid, block, 0, s, vol, P, out, plane); break;
+    case 4: hipLaunchKernelGGL((k_bake_raw<4>), grid, block, 0, s, vol, P, out, plane); break;
+    case 8: hipLaunchKernelGGL((k_bake_raw<8>), grid, block, 0, s, vol, P, out, plane); break;
+    case 16: hipLaunchKernelGGL((k_bake_raw<16>), grid, block, 0, s, vol, P, out, plane); break;
+    case 32: hipLaunchKernelGGL((k_bake_raw<32>), grid, block, 0, s, vol, P, out, plane); break;
+    default: hipLaunchKernelGGL((k_bake_raw<0>), grid, block, 0, s, vol, P, out, plane); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, hipStream_t s) {
+    dim3 grid;
+    if (!bake_grid(P, grid)) return hipErrorInvalidValue;
+    const dim3 block(256);
+    switch (P.nb) {
+    case 1: hipLaunchKernelGGL((k_bake_codec<1>), grid, block, 0, s, P, out, plane); break;
+    case 2: hipLaunchKernelGGL((k_bake_codec<2>), grid, block, 0, s, P, out, plane); break;
+    case 4: hipLaunchKernelGGL((k_bake_codec<4>), grid, block, 0, s, P, out, plane); break;
+    case 8: hipLaunchKernelGGL((k_bake_codec<8>), grid, block, 0, s, P, out, plane); break;
+    case 16: hipLaunchKernelGGL((k_bake_codec<16>), grid, block, 0, s, P, out, plane); break;
+    case 32: hipLaunchKernelGGL((k_bake_codec<32>), grid, block, 0, s, P, out, plane); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace vr
