@@ -87,8 +87,8 @@ void setTextureFilterMode(bool bLinearFilter);
  * mean/variance/entropy of the raw volume (originalQueryTex, K:722-773) and of
  * the codec volume (fractalQueryTex, K:775-871) into float4 textures.  Here the
  * same statistics are baked once into three float planes per resident volume
- * (vr_bake_stats); frames of methods 1-6 then filter the planes instead of
- * decoding the 8 corner records at every step -- bit-identical output, 4 bytes
+ * (vr_bake_stats); frames of methods 1-7 then read the planes instead of
+ * decoding the corner records at every step -- bit-identical output, 4 bytes
  * per corner voxel read instead of a whole record.  Without it (or after
  * vr_release_stats) the march decodes the records per step.  Errors (no
  * volume, out of memory) go to vr_last_error(); the per-step decode stays. */
@@ -108,9 +108,10 @@ void dataProcessing(void);
 #define VR_ERR_UNSUPPORTED -4
 
 /* Baked statistics (basicDataProcessing).  vr_bake_stats bakes the planes of
- * the resident raw and codec volumes that are not baked yet: 3 planes of
- * slice_pitch * depth floats for the raw volume (mean, variance, entropy at
- * record index z * slice_pitch + y * row_pitch + x, vr_volume_layout) and 3
+ * the resident raw and codec volumes that are not baked yet: 4 planes of
+ * slice_pitch * depth floats for the raw volume (mean, variance, entropy and
+ * method 7's undivided corner mean at record index
+ * z * slice_pitch + y * row_pitch + x, vr_volume_layout) and 3
  * planes of X * Y * Z floats for the codec volume (methods 4/5/6, dense voxel
  * order).  Re-uploading or releasing a volume drops its planes; a volume
  * modified in place through vr_volume_info's pointer must be re-baked

@@ -34,8 +34,9 @@ def _d2h(ptr, n):
 
 @pytest.mark.parametrize("nb", [1, 3, 4, 8, 32])
 def test_planes_equal_oracle_stats(pkg, orc, gpu, baked, nb, monkeypatch):
-    """plane k at record index z*slice_pitch + y*row_pitch + x = statistic k+1 of that
-    record (orc_record_stats), bit for bit, also with padded rows / slices"""
+    """plane k < 3 at record index z*slice_pitch + y*row_pitch + x = statistic k+1 of that
+    record (orc_record_stats), plane 3 = method 7's corner mean (orc_corner_mean), bit for
+    bit, also with padded rows / slices"""
     monkeypatch.setenv("VR_PAD", "3,5")
     nx, ny, nz = 9, 7, 5
     vol = orc.synth_volume(nx, ny, nz, nb)
@@ -45,11 +46,12 @@ def test_planes_equal_oracle_stats(pkg, orc, gpu, baked, nb, monkeypatch):
     (ptr, plane), _ = pkg.stats_info()
     sy, sz = pkg.volume_layout()
     assert ptr and plane == sz * nz and sy == nx + 3 and sz == sy * ny + 5
-    got = _d2h(ptr, 3 * plane).reshape(3, plane)
+    got = _d2h(ptr, 4 * plane).reshape(4, plane)
     for z in range(nz):
         for y in range(ny):
             for x in range(nx):
-                want = orc.record_stats(vol[z, y, x])
+                want = np.append(orc.record_stats(vol[z, y, x]),
+                                 np.float32(orc.corner_mean(vol[z, y, x]))).astype(np.float32)
                 have = got[:, z * sz + y * sy + x]
                 assert np.array_equal(have.view(np.uint32), want.view(np.uint32)), (x, y, z)
 
@@ -140,7 +142,7 @@ def test_baked_codec(pkg, orc, gpu, baked, nb):
 
 def test_release_reupload_and_errors(pkg, orc, gpu, baked):
     """release_stats returns to the per-step decode; a new volume drops stale planes;
-    methods 7 / 8 / 9 / 0 never read the planes; no volume -> VRError"""
+    no volume -> VRError"""
     import torch
     vol = orc.synth_volume(16, 16, 16, 8)
     pkg.init_distribution(vol)
@@ -150,8 +152,8 @@ def test_release_reupload_and_errors(pkg, orc, gpu, baked):
     assert pkg.last_kernel() == "k_march_pipe<B=1,M=0>"
     got = gpu_render(pkg, None, 64, 48, m, 7, torch, m7=(16, 16, 16))
     ref = orc.render(vol, orc.make_params(64, 48, m, query_method=7, m7_dims=(16, 16, 16)))[:3]
-    assert_parity(got, ref, "m7 with baked planes resident")
-    assert "M=7" in pkg.last_kernel()
+    assert_parity(got, ref, "m7 from the baked corner means")
+    assert pkg.last_kernel() == "k_march_m7<B=1,M=-7>", pkg.last_kernel()
     pkg.release_stats()
     assert pkg.stats_info()[0][0] is None
     gpu_render(pkg, None, 64, 48, m, 1, torch)
@@ -166,3 +168,21 @@ def test_release_reupload_and_errors(pkg, orc, gpu, baked):
     pkg.freeCudaBuffers()
     with pytest.raises(pkg.VRError):
         pkg.bake_stats()
+
+
+@pytest.mark.parametrize("nb", [1, 4, 8, 32])
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_baked_method7(pkg, orc, gpu, baked, nb, pipe, monkeypatch):
+    """method 7 from the baked corner means (plane 3): the corner cache and double lerps of
+    K:395-480 over 4-byte corners, both m7 kernels, grid = volume and grid != volume"""
+    import torch
+    monkeypatch.setenv("VR_M7_PIPE", pipe)
+    vol = orc.synth_volume(18, 16, 14, nb)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))):
+        for grid in ((18, 16, 14), (10, 12, 20)):
+            got = gpu_render(pkg, None, 72, 56, cam, 7, torch, m7=grid)
+            ref = orc.render(vol, orc.make_params(72, 56, cam, query_method=7, m7_dims=grid))[:3]
+            assert_parity(got, ref, f"baked m7 nb={nb} grid {grid}")
+            assert "B=1,M=-7>" in pkg.last_kernel(), pkg.last_kernel()

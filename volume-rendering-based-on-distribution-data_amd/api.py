@@ -231,7 +231,7 @@ def setTextureFilterMode(bLinearFilter: bool) -> None:
 def basicDataProcessing() -> None:
     """basicDataProcessing, K:1798-1887: bakes the per-voxel statistics of the resident
     raw / codec volumes (originalQueryTex / fractalQueryTex, K:722-871) into float
-    planes; methods 1-6 then filter the planes (bit-identical to the per-step decode)."""
+    planes; methods 1-7 then read the planes (bit-identical to the per-step decode)."""
     _lib.load().basicDataProcessing()
     check_last()
 
@@ -242,7 +242,7 @@ def bake_stats() -> None:
 
 
 def release_stats() -> None:
-    """Drop the baked planes: methods 1-6 decode the records per step again."""
+    """Drop the baked planes: methods 1-7 decode the records per step again."""
     check(_lib.load().vr_release_stats())
 
 

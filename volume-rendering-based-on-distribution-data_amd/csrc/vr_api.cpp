@@ -64,7 +64,8 @@ struct State {
         int nx = 0, ny = 0, nz = 0, K = 0, z_base = 0, nzs = 0;
     } gmm;
     // baked statistics (basicDataProcessing / vr_bake_stats, vr_stats.hip):
-    // three planes of stats_plane floats for the raw volume (methods 1/2/3) and
+    // four planes of stats_plane floats for the raw volume (methods 1/2/3 and
+    // method 7's corner mean) and
     // of cstats_plane floats for the codec volume (methods 4/5/6); nullptr =
     // not baked, the march decodes the records at every step
     float *stats = nullptr, *cstats = nullptr;
@@ -615,8 +616,8 @@ int bake_stats() {
         P.enorm = entropy_norm(g.nb);
         const uint64_t plane = g.sz * (uint64_t)g.nz;
         float *buf = nullptr;  // + 4 floats: the pair loads of the march read x0 + 1
-        VR_HIP(hipMalloc(&buf, (3 * plane + 4) * sizeof(float)));
-        hipError_t e = hipMemsetAsync(buf, 0, (3 * plane + 4) * sizeof(float), g.stream);
+        VR_HIP(hipMalloc(&buf, (4 * plane + 4) * sizeof(float)));
+        hipError_t e = hipMemsetAsync(buf, 0, (4 * plane + 4) * sizeof(float), g.stream);
         if (e == hipSuccess) e = vr::launch_bake_raw(g.vol, P, buf, plane, g.stream);
         if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
         if (e != hipSuccess) {
@@ -1161,7 +1162,12 @@ int vr_render(const vr_render_desc *desc) {
     const float *baked = (qm >= 1 && qm <= 3 && g.stats)   ? g.stats + (uint64_t)(qm - 1) * g.stats_plane
                          : (qm >= 4 && qm <= 6 && g.cstats) ? g.cstats + (uint64_t)(qm - 4) * g.cstats_plane
                                                             : nullptr;
-    if (baked) {
+    if (qm == 7 && g.stats) {
+        // method 7 from the baked corner means (plane 3): the same corner cache
+        // and double lerps (K:395-480), 4 bytes per corner refresh
+        P.nb = 1;
+        e = vr::launch_march(1, -7, g.stats + 3 * g.stats_plane, P, nslots, false, g.stream);
+    } else if (baked) {
         // one float per corner voxel, the same filter and composite (vr_stats.hip)
         P.nb = 1;
         P.path = baked_path(desc, P);

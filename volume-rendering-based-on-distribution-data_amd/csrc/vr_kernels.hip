@@ -1344,7 +1344,19 @@ struct M7 {
     float mean[8];
 };
 
-template <int B>
+// the corner mean of one record (K:347-367); BK: the record is the corner mean
+// itself, baked by basicDataProcessing (plane 3, vr_stats.hip; B = 1)
+template <int B, bool BK>
+__device__ __forceinline__ float m7_rec_mean(const float (&rec)[B]) {
+    if constexpr (BK) {
+        static_assert(B == 1, "baked corner means are one float per voxel");
+        return rec[0];
+    } else {
+        return raw_mean<B>(rec);
+    }
+}
+
+template <int B, bool BK = false>
 __device__ __forceinline__ float corner_mean(const float *__restrict__ vol, const Params &P,
                                              float ux, float uy, float uz) {
     const int ix = point_axis(ux, P.nx), iy = point_axis(uy, P.ny), iz = point_axis(uz, P.nz);
@@ -1352,13 +1364,13 @@ __device__ __forceinline__ float corner_mean(const float *__restrict__ vol, cons
     if constexpr (B > 0) {
         float rec[B];
         load_rec<B>(vol, vidx, rec);
-        return raw_mean<B>(rec);
+        return m7_rec_mean<B, BK>(rec);
     } else {
         return raw_mean_rt(vol + vidx * (uint64_t)P.nb, P.nb);
     }
 }
 
-template <int B>
+template <int B, bool BK = false>
 __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float px, float py,
                            float pz, M7 &m) {
     const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
@@ -1370,8 +1382,8 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
     m.cz = ceilf(qz * (float)P.m7z) / (float)P.m7z;
 #pragma unroll
     for (int j = 0; j < 8; j++)
-        m.mean[j] = corner_mean<B>(vol, P, (j & 1) ? m.cx : m.fx, (j & 2) ? m.cy : m.fy,
-                                   (j & 4) ? m.cz : m.fz);
+        m.mean[j] = corner_mean<B, BK>(vol, P, (j & 1) ? m.cx : m.fx, (j & 2) ? m.cy : m.fy,
+                                       (j & 4) ? m.cz : m.fz);
 }
 
 // ---- method 7, software-pipelined (B <= 8) ----
@@ -1402,7 +1414,7 @@ __device__ __forceinline__ void m7_gather(const float *__restrict__ vol, const P
 #ifndef VR_M7_PIPE_MAXWAVES
 #define VR_M7_PIPE_MAXWAVES 8
 #endif
-template <int B>
+template <int B, bool BK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PIPE_MAXWAVES))) void k_march_m7_pipe(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
@@ -1428,7 +1440,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PI
     float ra[8][B], rb[8][B];
     m7_gather<B>(vol, P, cur, ra);
 #pragma unroll
-    for (int j = 0; j < 8; j++) mean[j] = raw_mean<B>(ra[j]);
+    for (int j = 0; j < 8; j++) mean[j] = m7_rec_mean<B, BK>(ra[j]);
     ca = cur;
     int n = 0;
     bool alive = true;
@@ -1441,7 +1453,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PI
             qz > cur.cz) {  // inInterpolation, K:253-270, 396: refresh from (cc, rc)
             cur = cc;
 #pragma unroll
-            for (int j = 0; j < 8; j++) mean[j] = raw_mean<B>(rc[j]);
+            for (int j = 0; j < 8; j++) mean[j] = m7_rec_mean<B, BK>(rc[j]);
         }
         const float tn = t + kTStep;                                 // K:701
         const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);    // K:703, K:381
@@ -1884,7 +1896,7 @@ hipError_t launch_codec_check(const int4 *cb, uint64_t n, int ntpl, int nb, int 
     return hipGetLastError();
 }
 
-template <int B>
+template <int B, bool BK = false>
 __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
@@ -1906,12 +1918,12 @@ __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol,
     float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
     const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
     M7 m;
-    m7_refresh<B>(vol, P, px, py, pz, m);
+    m7_refresh<B, BK>(vol, P, px, py, pz, m);
     int n = 0;
     for (int i = 0; i < kMaxSteps; i++) {
         const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
         if (qx < m.fx || qy < m.fy || qz < m.fz || qx > m.cx || qy > m.cy || qz > m.cz)
-            m7_refresh<B>(vol, P, px, py, pz, m);  // inInterpolation, K:253-270, 396
+            m7_refresh<B, BK>(vol, P, px, py, pz, m);  // inInterpolation, K:253-270, 396
         const float xd = (px * 0.5f + 0.5f - m.fx) / (m.cx - m.fx);
         const float yd = (py * 0.5f + 0.5f - m.fy) / (m.cy - m.fy);
         const float zd = (pz * 0.5f + 0.5f - m.fz) / (m.cz - m.fz);
@@ -2183,6 +2195,25 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     case 1: hipLaunchKernelGGL((k_march<B, 1, COUNT>), grid, block, lds, s, vol, P); break;
     case 2: hipLaunchKernelGGL((k_march<B, 2, COUNT>), grid, block, lds, s, vol, P); break;
     case 3: hipLaunchKernelGGL((k_march<B, 3, COUNT>), grid, block, lds, s, vol, P); break;
+    case -7:  // method 7 over the baked corner means (plane 3, vr_stats.hip)
+        if constexpr (B == 1 && !COUNT) {
+            // 4-byte corners: the plain march (the look-ahead gather of
+            // k_march_m7_pipe, VR_M7_PIPE=1, only adds loads), 4 workgroups per CU
+            // on row-aligned views, 2 on oblique ones (1024^3 C0 0.68 -> 0.64 ms,
+            // C1 2.03 -> 1.67; profiles/r02/baked_m7.log)
+            const char *ep = std::getenv("VR_M7_PIPE");
+            const size_t lds =
+                cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : (P.oblique ? 2 : 4));
+            if (ep && std::atoi(ep) != 0) {
+                note_kernel("k_march_m7_pipe", B, method);
+                hipLaunchKernelGGL((k_march_m7_pipe<1, true>), grid, block, lds, s, vol, P);
+            } else {
+                note_kernel("k_march_m7", B, method);
+                hipLaunchKernelGGL((k_march_m7<1, true>), grid, block, lds, s, vol, P);
+            }
+            break;
+        }
+        return hipErrorInvalidValue;
     case 7:
         if (COUNT) return hipErrorInvalidValue;
         // oblique views run method 7 at 3 workgroups per CU when B = 8 (the

@@ -9,15 +9,16 @@
 // for bit.  A baked frame reads 4 bytes per corner voxel instead of B * 4
 // (raw records) or a codebook entry + errors (codec), so the march is no
 // longer bound by the distribution bytes.  Planes use the volume's pitches:
-// plane k of the raw volume holds statistic k+1 at record index
-// z * slice_pitch + y * row_pitch + x (the codec volume: dense voxel order).
+// plane k < 3 of the raw volume holds statistic k+1 at record index
+// z * slice_pitch + y * row_pitch + x, plane 3 method 7's corner mean (the
+// codec volume: 3 planes, dense voxel order).
 #include "vr_internal.h"
 
 namespace vr {
 
 // One thread per voxel of an x-row (grid: x blocks of 256, y rows, z slices);
-// each record is read once, coalesced, and its three statistics written to
-// the three planes.  The same functions as the march (record_stat), so the
+// each record is read once, coalesced, and its statistics written to the four
+// planes (mean, variance, entropy; plane 3: method 7's undivided corner mean).  The same functions as the march (record_stat), so the
 // planes hold exactly the per-corner values the march would decode; the
 // entropy's exact logarithm uses the LDS table (both logarithm forms are
 // exact, vr_selftest_logf).
@@ -30,22 +31,25 @@ __global__ __launch_bounds__(256) void k_bake_raw(const float *__restrict__ vol,
     const uint32_t x = blockIdx.x * 256u + threadIdx.x;
     if (x >= (uint32_t)P.nx) return;
     const uint64_t off = (uint64_t)blockIdx.z * P.sz + (uint64_t)blockIdx.y * P.sy + x;
-    float m, v, e;
+    float m, v, e, c;
     if constexpr (B > 0) {
         float p[B];
         load_rec<B>(vol, off, p);
         m = record_stat<B, 1>(p, P.enorm);
         v = record_stat<B, 2>(p, P.enorm);
         e = entropy_p<B>(p, P.enorm, tab);
+        c = raw_mean<B>(p);
     } else {
         const float *p = vol + off * (uint64_t)P.nb;
         m = record_stat_rt<1>(p, P.nb, P.enorm);
         v = record_stat_rt<2>(p, P.nb, P.enorm);
         e = record_stat_rt<3>(p, P.nb, P.enorm);
+        c = raw_mean_rt(p, P.nb);
     }
     out[off] = m;
     out[plane + off] = v;
     out[2 * plane + off] = e;
+    out[3 * plane + off] = c;  // method 7's corner mean (K:347-367), before the / 0.0217
 }
 
 // codec voxels (methods 4/5/6, K:775-871): decode once, statistics C = 0, 1, 2
