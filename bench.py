@@ -528,7 +528,8 @@ def main():
     traffic = None
     if world == 1 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
-            entry = json.load(f).get(f"{args.config}|{args.camera}|m{args.method}")
+            entry = json.load(f).get(f"{args.config}|{args.camera}|m{args.method}"
+                                     + ("|baked" if args.baked else ""))
         if entry and entry.get("kernel") == kernel:
             traffic = entry.get("hbm_bytes_per_launch")
 
