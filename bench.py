@@ -560,7 +560,7 @@ def main():
                             f"{args.camera}, queryMethod {args.method}",
                 "volume": [n, n, n], "bins": nb, "image": [W, H], "camera": args.camera,
                 "query_method": args.method, "density": 0.05,
-                "statistics": ("baked once by basicDataProcessing (3 f32 planes)"
+                "statistics": ("baked once by basicDataProcessing (f32 statistics planes)"
                                if args.baked else "decoded from the records at every step"),
                 "bake_ms": round(bake_ms, 3) if bake_ms is not None else None,
                 "tile_deal": (None if world == 1 else "estimate" if args.no_balance
