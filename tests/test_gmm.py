@@ -257,3 +257,20 @@ def test_bounds_by_cost(pkg):
     assert [hi - lo for lo, hi in nb] == [25, 25, 25, 25]
     with pytest.raises(ValueError):
         S.bounds_by_cost(100, 2, 1, [(0, 50), (50, 100)], [1, 1], max_slices=40)
+
+
+def test_stream_bounds(pkg):
+    """streamed slabs: fixed thickness, the last thinner, march order, full cover"""
+    sb = pkg.stream.stream_bounds
+    assert sb(10, 4, 1) == [(0, 4), (4, 8), (8, 10)]
+    assert sb(10, 4, -1) == [(8, 10), (4, 8), (0, 4)]
+    assert sb(3, 8, 1) == [(0, 3)]
+    for nz in (1, 7, 64):
+        for S in (1, 3, 64):
+            b = sb(nz, S, 1)
+            assert b[0][0] == 0 and b[-1][1] == nz
+            assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+    with pytest.raises(ValueError):
+        sb(10, 0, 1)
+    with pytest.raises(ValueError):
+        sb(10, 4, 0)

@@ -190,3 +190,40 @@ def test_gmm_golden_fixtures(pkg, gpu):
         # out_n: the fixture holds -2 for pixels outside any ray (none here) like the render
         check(got, ref, os.path.basename(path))
     pkg.free_gmm()
+
+
+@pytest.mark.parametrize("c", ["C0", "below", "C1"])
+@pytest.mark.parametrize("S,method", [(1, 1), (4, 2), (7, 1), (40, 2)])
+def test_gmm_streamed_slabs(pkg, orc, gpu, c, S, method):
+    """host-pinned slabs streamed through a 2-buffer HBM ring (stream.GmmStream): the
+    frame equals the oracle's whole-volume render bit for bit, for slabs of 1 slice up
+    to one slab (S >= nz), rays marching towards -z and +z"""
+    import torch
+    dims = (24, 20, 17)
+    K = 16
+    wm, sg = orc.synth_gmm(*dims, K, seed=3)
+    st = pkg.stream.GmmStream(torch.from_numpy(wm.copy()), torch.from_numpy(sg.copy()), S)
+    m = cam(pkg, c)
+    if pkg.slabs.march_direction(m, 72, 56) == 0:
+        pytest.skip("view crosses z both ways")
+    W, H = 72, 56
+    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    out_f = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+    steps = torch.full((H * W,), -2, dtype=torch.int32, device="cuda")
+    d = pkg.make_desc(out, W, H, m, query_method=method, volume_size=(1, 1, 1), d_output_f=out_f,
+                      d_steps=steps)
+    s = torch.cuda.Stream()
+    info = st.render(d, s)
+    torch.cuda.synchronize()
+    assert info["slabs"] == -(-dims[2] // S)
+    got = (out.cpu().numpy().view(np.uint32).reshape(H, W), out_f.cpu().numpy().reshape(H, W, 4),
+           steps.cpu().numpy().reshape(H, W))
+    ref = orc.render_gmm(wm, sg, dims, orc.make_params(W, H, m, query_method=method))
+    check(got, ref, f"streamed S={S} m{method} {c}")
+    # a second frame reuses the ring (buffers, events) and gives the same image
+    first = out.clone()
+    out.zero_()
+    st.render(d, s)
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
+    pkg.set_stream(None)

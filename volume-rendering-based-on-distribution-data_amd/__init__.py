@@ -8,7 +8,7 @@ reference's volumeRender.cpp API plus the multi-GPU tile split.
 The directory name is not a Python identifier; load it with
 ``_load_package()`` of __graft_entry__.py (module name ``vrdd_amd``).
 """
-from . import _lib, api, camera, slabs, tiles  # noqa: F401
+from . import _lib, api, camera, slabs, stream, tiles  # noqa: F401
 from ._lib import VRError  # noqa: F401
 from .api import *  # noqa: F401,F403
 
