@@ -1,0 +1,116 @@
+"""Seeded random parity sweep: every case draws a volume shape, bin count, camera
+(any rotation, translations that put the eye outside, at the edge of or inside
+the volume), image size, method, render parameters, kernel path override and
+statistics source (per-step decode / baked), renders through the C-ABI and
+compares with the oracle.  Same bar as test_gpu_parity.py: packed RGBA8 and
+samples per pixel identical, float RGBA within 1e-4.  Cases are reproducible
+from their seed (printed in the failure message)."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_parity, codec_render, gpu_render
+
+pytestmark = pytest.mark.gpu
+
+# kernel-path overrides a case may take (vr_api.cpp fill_params / baked_path)
+PATHS = [{}, {}, {"VR_PATH": "0"}, {"VR_PATH": "1"}, {"VR_PATH": "1", "VR_BOX_MAX": "64"},
+         {"VR_PATH": "2"}, {"VR_PATH": "4"}, {"VR_PATH": "3"}, {"VR_PATH": "7", "VR_SEG": "-2"},
+         {"VR_PATH": "7", "VR_SEG": "4"}, {"VR_PATH": "5"}, {"VR_WG_PER_CU": "2"}]
+
+
+def draw_camera(pkg, rng):
+    kind = rng.integers(0, 4)
+    if kind == 0:  # row-aligned (runSingleTest family), shifted / zoomed
+        return pkg.camera.display_inv_view(
+            (0.0, 0.0), (rng.uniform(-0.6, 0.6), rng.uniform(-0.6, 0.6), -rng.uniform(1.2, 6.0)))
+    if kind == 1:  # axis-aligned quarter turns
+        rx, ry = (float(rng.choice([0, 90, 180, 270])) for _ in range(2))
+        return pkg.camera.display_inv_view((rx, ry), (0.0, 0.0, -rng.uniform(2.5, 5.0)))
+    if kind == 2:  # eye inside the volume
+        return pkg.camera.display_inv_view(
+            (rng.uniform(-180, 180), rng.uniform(-180, 180)),
+            (rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5)))
+    return pkg.camera.display_inv_view(
+        (rng.uniform(-180, 180), rng.uniform(-180, 180)),
+        (rng.uniform(-0.4, 0.4), rng.uniform(-0.4, 0.4), -rng.uniform(1.5, 6.0)))
+
+
+def draw_params(rng):
+    return dict(density=float(np.float32(rng.uniform(0.01, 1.0))),
+                brightness=float(np.float32(rng.uniform(0.5, 2.0))),
+                toff=float(np.float32(rng.uniform(-0.2, 0.2))),
+                tscale=float(np.float32(rng.uniform(0.5, 2.0))))
+
+
+@pytest.mark.parametrize("seed", range(200))
+def test_random_histogram_case(pkg, orc, gpu, seed, monkeypatch):
+    import torch
+    rng = np.random.default_rng(1000 + seed)
+    dims = tuple(int(v) for v in rng.integers(2, 41, 3))
+    nb = int(rng.choice([1, 2, 3, 4, 5, 8, 8, 8, 16, 32]))
+    W, H = int(rng.integers(1, 161)), int(rng.integers(1, 121))
+    method = int(rng.choice([1, 2, 3, 7]))
+    m = draw_camera(pkg, rng)
+    prm = draw_params(rng)
+    env = PATHS[int(rng.integers(0, len(PATHS)))]
+    baked = bool(rng.integers(0, 3) == 0)
+    m7 = tuple(int(v) for v in rng.integers(2, 41, 3)) if rng.integers(0, 2) else dims
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    vol = orc.synth_volume(*dims, nb, seed=seed)
+    pkg.init_distribution(vol)
+    if baked:
+        pkg.bake_stats()
+    try:
+        got = gpu_render(pkg, None, W, H, m, method, torch, m7=m7 if method == 7 else None, **prm)
+        ref = orc.render(vol, orc.make_params(
+            W, H, m, density=prm["density"], brightness=prm["brightness"],
+            transfer_offset=prm["toff"], transfer_scale=prm["tscale"], query_method=method,
+            m7_dims=m7))[:3]
+        assert_parity(got, ref, f"seed {seed}: {dims}x{nb} {W}x{H} m{method} env {env} "
+                                f"baked {baked} kernel {pkg.last_kernel()}")
+    finally:
+        pkg.release_stats()
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_random_codec_case(pkg, orc, gpu, seed):
+    import torch
+    rng = np.random.default_rng(2000 + seed)
+    dims = tuple(int(v) for v in rng.integers(2, 33, 3))
+    nb = int(rng.choice([1, 2, 4, 8, 16, 32]))
+    W, H = int(rng.integers(1, 129)), int(rng.integers(1, 97))
+    method = int(rng.choice([4, 5, 6]))
+    m = draw_camera(pkg, rng)
+    baked = bool(rng.integers(0, 3) == 0)
+    cb, t, e = orc.synth_codec(*dims, nb, ntemplates=int(rng.integers(1, 40)),
+                               slots=int(rng.integers(0, nb + 1)), seed=seed)
+    pkg.init_codec(cb, t, e)
+    if baked:
+        pkg.bake_stats()
+    try:
+        got = codec_render(pkg, W, H, m, method, torch)
+        ref = orc.render_codec(cb, t, e, orc.make_params(W, H, m, query_method=method))[:3]
+        assert_parity(got, ref, f"seed {seed}: codec {dims}x{nb} {W}x{H} m{method} baked {baked}")
+    finally:
+        pkg.release_stats()
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_gmm_case(pkg, orc, gpu, seed):
+    import torch
+    from test_gpu_gmm import check, gmm_render
+    rng = np.random.default_rng(3000 + seed)
+    dims = tuple(int(v) for v in rng.integers(2, 31, 3))
+    K = int(rng.choice([8, 16, 32]))
+    W, H = int(rng.integers(1, 129)), int(rng.integers(1, 97))
+    method = int(rng.choice([1, 2]))
+    m = draw_camera(pkg, rng)
+    density = float(np.float32(rng.uniform(0.02, 0.8)))
+    wm, sg = orc.synth_gmm(*dims, K, seed=seed)
+    pkg.init_gmm(wm, sg)
+    got = gmm_render(pkg, W, H, m, method, torch, density=density)
+    ref = orc.render_gmm(wm, sg, dims, orc.make_params(W, H, m, query_method=method,
+                                                       density=density))
+    check(got, ref, f"seed {seed}: GMM {dims} K={K} {W}x{H} m{method}")
+    pkg.free_gmm()
