@@ -577,7 +577,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
 // not by decode: row-aligned views take the one-lane pipelined march (path 2,
 // 1024^3 C0 0.375 ms); oblique views, whose lanes' loads touch many lines per
 // instruction, split each ray over 4 lanes (path 7, VR_SEG 4: 1024^3 C1 2.02
-// -> 1.32 ms).  A deeper look-ahead ring (2-8 steps in flight per lane) was
+// -> 1.32 ms, 1.11 at 4 workgroups per CU).  A deeper look-ahead ring (2-8 steps in flight per lane) was
 // slower everywhere but 512^3 C1 (within 3 %).  VR_PATH (1 / 2 / 7) overrides;
 // P.seg_lanes keeps a VR_SEG setting.
 int baked_path(const vr_render_desc *d, vr::Params &P) {
@@ -595,6 +595,13 @@ int baked_path(const vr_render_desc *d, vr::Params &P) {
         else if (rays <= 700000) path = 7, seg = -2;
     }
     if (path == 7 && !std::getenv("VR_SEG")) P.seg_lanes = seg;
+    // oblique full frames of a fine volume (< 4 pixels per voxel of the x-y
+    // face): 4 workgroups per CU, fewer rays' lines in flight per L2 (1024^3
+    // C1 1.28 -> 1.11 ms; 2-3 per CU 1.25, 6 1.19); coarse volumes (512^3:
+    // 0.67 uncapped vs 0.73) and row-aligned views run uncapped
+    if (!along_rows && !d->d_tile_list && P.wg_per_cu == 0 &&
+        (uint64_t)d->width * d->height < 4ull * (uint64_t)P.nx * (uint64_t)P.ny)
+        P.wg_per_cu = 4;
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
         if (v == 1 || v == 2 || v == 7) path = v;
