@@ -301,6 +301,8 @@ def main_gmm(args):
         pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
         torch.cuda.synchronize()
         balanced = True
+    # U before the warm-up (as in main(): the counting pass warms clocks and translation)
+    u = pkg.gmm_count_footprint(desc) if world == 1 else None
     for _ in range(args.warmup):
         step(False)
     drain()
@@ -325,7 +327,6 @@ def main_gmm(args):
         last = frames[(nframe[0] - 1) % R]
         np.save(args.dump_frame, last.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
-    u = pkg.gmm_count_footprint(desc) if world == 1 else None
     alg_bytes = u * rec_bytes + W * H * 4 if u is not None else None
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
     ms_per_step = elapsed / args.steps * 1e3
@@ -451,6 +452,21 @@ def main():
     assemble = torch.cuda.Stream(device=dev) if world > 1 else None
     works, assembled = [None, None], [None, None]
 
+    # algorithmic bytes of one launch on this rank (SURVEY.md 8(d)): the volume bytes
+    # under the footprints (U*S_rec; codec: codebook + used error pairs) + pixels*4.
+    # Counted before the warm-up: the counting pass marches the same footprints once,
+    # so the frames that follow start with the clocks and the address translation
+    # of a running frame loop (profiles/r02/loop_timing.log)
+    pixels = W * H if world == 1 else int(np.sum(lists[rank] != pkg.tiles.PAD)) * 256
+    u = pkg.count_footprint(desc) if args.method in (1, 2, 3) else None
+    # baked frames read one f32 statistic per footprint voxel instead of the record
+    rec_bytes = 4 if args.baked else nb * 4
+    vol_bytes = (u * rec_bytes if u is not None
+                 else pkg.footprint_bytes(desc) if args.method in (4, 5, 6) and not args.baked
+                 else None)
+    alg_bytes = (vol_bytes + pixels * 4) if vol_bytes is not None else None
+    torch.cuda.synchronize()
+
     ev = []
     nframe = [0]
 
@@ -510,16 +526,6 @@ def main():
         np.save(args.dump_frame, frame.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
 
-    # algorithmic bytes of one launch on this rank (SURVEY.md 8(d)): the volume bytes
-    # under the footprints (U*S_rec; codec: codebook + used error pairs) + pixels*4
-    pixels = W * H if world == 1 else int(np.sum(lists[rank] != pkg.tiles.PAD)) * 256
-    u = pkg.count_footprint(desc) if args.method in (1, 2, 3) else None
-    # baked frames read one f32 statistic per footprint voxel instead of the record
-    rec_bytes = 4 if args.baked else nb * 4
-    vol_bytes = (u * rec_bytes if u is not None
-                 else pkg.footprint_bytes(desc) if args.method in (4, 5, 6) and not args.baked
-                 else None)
-    alg_bytes = (vol_bytes + pixels * 4) if vol_bytes is not None else None
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
 
     # HBM bytes per launch from the committed PMC passes of this same workload
