@@ -720,3 +720,41 @@ def test_method7_oblique_kernels(pkg, orc, gpu, quad, monkeypatch):
                                                   m7_dims=(30, 26, 22)))[:3]
             assert_parity(got, ref, f"m7 quad={quad} {rot} d={density}")
     assert pkg.last_kernel().startswith("k_march_m7_quad" if quad == "1" else "k_march_m7_pipe")
+
+
+@pytest.mark.parametrize("dims", [(26, 22, 18), (25, 21, 17), (1, 3, 5), (7, 1, 4)])
+@pytest.mark.parametrize("brick", ["1", "0"])
+def test_quad_march_brick_layout(pkg, orc, gpu, dims, brick, monkeypatch):
+    """oblique views of 8-bin volumes: the quad march reads the library's 2x2 (x, y)
+    micro-brick copy of the records (odd widths / heights are padded to even in the
+    copy); VR_BRICK=0 keeps the x rows.  Both bit-identical to the oracle, also for
+    the tile lists of a multi-GPU rank"""
+    import torch
+    monkeypatch.setenv("VR_PATH", "0")
+    monkeypatch.setenv("VR_BRICK", brick)
+    vol = orc.synth_volume(*dims, 8)
+    pkg.init_distribution(vol)
+    want = "k_march_quad_brick<" if brick == "1" else "k_march_quad<"
+    for rot in ((30.0, 45.0), (-60.0, 110.0), (12.0, -70.0)):
+        m = pkg.camera.display_inv_view(rot)
+        for method in (1, 2, 3):
+            got = gpu_render(pkg, None, 88, 60, m, method, torch)
+            ref = orc.render(vol, orc.make_params(88, 60, m, query_method=method))[:3]
+            assert_parity(got, ref, f"{dims} brick={brick} {rot} m{method}")
+            assert pkg.last_kernel().startswith(want)
+    W, H = 136, 72
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    full = gpu_render(pkg, None, W, H, m, 1, torch)[0]
+    world = 3
+    lists = pkg.tiles.tile_lists(W, H, world, m)
+    n_slots = lists.shape[1]
+    packed = torch.full((world, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    for r in range(world):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+        assert pkg.last_kernel().startswith(want)
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), full)

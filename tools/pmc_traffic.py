@@ -33,7 +33,7 @@ def per_dispatch(dirs):
             rows = collections.defaultdict(dict)
             for r in csv.DictReader(open(f)):
                 k = r["Kernel_Name"]
-                if "vr::k_march" not in k or ", true>" in k:
+                if "vr::k_march" not in k or ("vr::k_march<" in k and ", true>" in k):
                     continue  # the march only (not the footprint-counting variant)
                 rows[(k, r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
             for (k, _), cs in rows.items():

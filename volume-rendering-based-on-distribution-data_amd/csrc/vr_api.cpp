@@ -70,6 +70,10 @@ struct State {
     // not baked, the march decodes the records at every step
     float *stats = nullptr, *cstats = nullptr;
     uint64_t stats_plane = 0, cstats_plane = 0;
+    // 2x2 (x, y) micro-brick copy of an owned 8-bin volume for the quad march
+    // of oblique views (ensure_brick, brick_index); nullptr = not made
+    float *brick = nullptr;
+    uint64_t bsy = 0, bsz = 0;
     // bumped whenever a resident volume / codec / flexible-block set is
     // released, so an order learned on old data is not reused (the order is a
     // scheduling hint only: any order renders the same image)
@@ -111,8 +115,15 @@ void release_cstats() {
     g.cstats_plane = 0;
 }
 
+void release_brick() {
+    if (g.brick) (void)hipFree(g.brick);
+    g.brick = nullptr;
+    g.bsy = g.bsz = 0;
+}
+
 void release_volume() {
     release_stats();
+    release_brick();
     g.volume_epoch++;
     if (g.vol && g.owned) (void)hipFree(g.vol);
     g.vol = nullptr;
@@ -681,6 +692,46 @@ void blob_axis(int n, double c, double s, float *out) {
     }
 }
 
+// Oblique views of an 8-bin volume (the quad march, path 0) read a 2x2 (x, y)
+// micro-brick copy of the records: a footprint's four (x, y) corners share
+// one 128-B line when x0 and y0 are even, so a wave step touches fewer lines
+// than in x rows.  Made on the first such frame of an owned
+// volume (a caller-owned buffer adopted by vr_init_distribution may change
+// behind the library's back), only if HBM keeps 1 GiB free after it; without
+// it the quad march reads the x rows.  VR_BRICK=0 disables it.
+bool ensure_brick() {
+    if (const char *e = std::getenv("VR_BRICK"))
+        if (std::atoi(e) == 0) return false;
+    if (g.brick) return true;
+    if (!g.vol || !g.owned || g.nb != 8) return false;
+    const uint64_t nxp = (uint64_t)g.nx + (g.nx & 1), nyp = (uint64_t)g.ny + (g.ny & 1);
+    const uint64_t bsy = 2 * nxp, bsz = nxp * nyp;
+    const uint64_t bytes = bsz * (uint64_t)g.nz * 8 * sizeof(float);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (1ull << 30)) {
+        (void)hipGetLastError();
+        return false;
+    }
+    float *buf = nullptr;
+    if (hipMalloc(&buf, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    vr::Params P;
+    std::memset(&P, 0, sizeof P);
+    P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
+    P.sy = g.sy; P.sz = g.sz;
+    if (vr::launch_brick8(g.vol, P, buf, bsy, bsz, g.stream) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(buf);
+        return false;
+    }
+    g.brick = buf;
+    g.bsy = bsy;
+    g.bsz = bsz;
+    return true;
+}
+
 }  // namespace
 
 namespace vr {
@@ -1188,7 +1239,14 @@ int vr_render(const vr_render_desc *desc) {
             return fail(VR_ERR_UNSUPPORTED, "codec volumes with %d bins (compiled: 1,2,4,8,16,32)",
                         P.nb);
     } else {
-        e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
+        const float *vol = g.vol;
+        if (P.path == 0 && g.nb == 8 && qm >= 1 && qm <= 3 && ensure_brick()) {
+            vol = g.brick;
+            P.brick = 1;
+            P.sy = g.bsy;
+            P.sz = g.bsz;
+        }
+        e = vr::launch_march(g.nb, desc->query_method, vol, P, nslots, false, g.stream);
     }
     if (e != hipSuccess) return hip_fail(e, "launch(k_march)");
     if (P.tile_cost) g.cost_recorded = true;

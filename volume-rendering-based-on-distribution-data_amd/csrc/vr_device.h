@@ -46,6 +46,8 @@ struct Params {
     int lds_cu, lds_wg;          // LDS bytes per CU / per workgroup (device attributes)
     int oblique;                 // view's screen x does not run along voxel rows
     int path;                    // kernel variant (vr_api.cpp fill_params)
+    int brick;                   // quad march: vol is the 2x2 (x, y) micro-brick copy,
+                                 // sy / sz its brick-row / slice pitches (brick_index)
     // fractal/template codec (methods 4/5/6): codebook int4 per voxel, templates
     // [ntpl][nb], (bin, value) errors [voxel][err_slots]
     const int4 *cb;
@@ -77,6 +79,14 @@ struct Params {
     uint4 *rays_out;             // alive rays leaving the slab (nullptr: slab = whole volume)
     uint32_t *n_rays_out;
 };
+
+// Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one
+// 128-B line = the 4 records of an even (x, y) pair of rows, 8 bins): bsy
+// records per brick row (2 * the even-padded width), bsz per slice.
+__host__ __device__ __forceinline__ uint64_t brick_index(uint64_t x, uint64_t y, uint64_t z,
+                                                         uint64_t bsy, uint64_t bsz) {
+    return z * bsz + (y >> 1) * bsy + (x >> 1) * 4u + (y & 1u) * 2u + (x & 1u);
+}
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)
 

@@ -85,6 +85,10 @@ hipError_t launch_synth_gmm(float *wm, float *sg, const SynthArgs &a, int K, int
 hipError_t launch_bake_raw(const float *vol, const Params &P, float *out, uint64_t plane,
                            hipStream_t s);
 hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, hipStream_t s);
+// 2x2 (x, y) micro-brick copy of an 8-bin volume (oblique views, vr_stats.hip):
+// pitches bsy (records per brick row) and bsz (records per slice), brick_index
+hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t bsy,
+                         uint64_t bsz, hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,

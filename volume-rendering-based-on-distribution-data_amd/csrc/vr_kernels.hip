@@ -1000,12 +1000,30 @@ __device__ __forceinline__ FootPacked pack_foot(const Foot &f, bool live) {
 
 // Gather ray (G, q)'s four x-pairs: L[c] = chunk g of the pair at combo c =
 // (y = c & 1, z = c >> 1).  A pair clamped at the x edge (x1 == x0) repeats x0.
-template <int G>
+// BR: the volume is the 2x2 (x, y) micro-brick copy (P.brick): lane g reads
+// half g & 1 of record x0 (g < 2) or x1 (g >= 2) of each (y, z) combo, so a
+// footprint's four (x, y) corners at one z share a line when x0 and y0 are
+// even (oblique views: fewer distinct lines per wave step).
+template <int G, bool BR = false>
 __device__ __forceinline__ bool qc_gather(const float *__restrict__ vol, const Params &P,
                                           const FootPacked &fp, uint32_t g, float4 (&L)[4]) {
     const int w0 = bcast_g<G>(fp.w0), w1 = bcast_g<G>(fp.w1);
     const bool live = (w1 >> 19) & 1;
-    if (live) {
+    if (BR && live) {
+        const uint64_t x0 = (uint32_t)w0 & 0xFFFFu, y0 = (uint32_t)w0 >> 16;
+        const uint64_t z0 = (uint32_t)w1 & 0xFFFFu;
+        const uint64_t ddx = (w1 >> 16) & 1, ddy = (w1 >> 17) & 1, ddz = (w1 >> 18) & 1;
+        const uint64_t xg = x0 + (ddx & (g >> 1)), y1 = y0 + ddy;
+        const uint64_t bx = (xg >> 1) * 4u + (xg & 1u);
+        const uint64_t ry0 = (y0 >> 1) * P.sy + (y0 & 1u) * 2u + bx;
+        const uint64_t ry1 = (y1 >> 1) * P.sy + (y1 & 1u) * 2u + bx;
+        const uint64_t rz0 = z0 * P.sz, rz1 = rz0 + ddz * P.sz;
+        const uint32_t half = g & 1u;
+        L[0] = reinterpret_cast<const float4 *>(vol + (rz0 + ry0) * 8)[half];
+        L[1] = reinterpret_cast<const float4 *>(vol + (rz0 + ry1) * 8)[half];
+        L[2] = reinterpret_cast<const float4 *>(vol + (rz1 + ry0) * 8)[half];
+        L[3] = reinterpret_cast<const float4 *>(vol + (rz1 + ry1) * 8)[half];
+    } else if (live) {
         const uint64_t x0 = (uint32_t)w0 & 0xFFFFu, y0 = (uint32_t)w0 >> 16;
         const uint64_t z0 = (uint32_t)w1 & 0xFFFFu;
         const uint64_t ddy = (w1 >> 17) & 1, ddz = (w1 >> 18) & 1;
@@ -1051,7 +1069,7 @@ __device__ __forceinline__ float qc_blend(const FootPacked &fp, float s0, float 
     return lerpq(c0, c1, az);
 }
 
-template <int G, int M>
+template <int G, int M, bool BR>
 __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const Params &P,
                                           const FootPacked &fc, bool lc, const FootPacked &fn,
                                           bool &ln, uint32_t g, float4 (&L)[4],
@@ -1062,7 +1080,7 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
     pair_swap(L[0], L[1], odd, r0);  // combo (y = g&1, z0)
     pair_swap(L[2], L[3], odd, r1);  // combo (y = g&1, z1)
     // ... which frees them for the next step's gathers of the same group
-    ln = qc_gather<G>(vol, P, fn, g, L);
+    ln = qc_gather<G, BR>(vol, P, fn, g, L);
     float s0 = 0.0f, s1 = 0.0f;
     if (lc) {
         s0 = record_stat_p<8, M>(r0, P.enorm, lt);
@@ -1074,7 +1092,7 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
 #ifndef VR_QUAD_WAVES
 #define VR_QUAD_WAVES 1  // minimum waves per SIMD the register allocation must allow
 #endif
-template <int M>
+template <int M, bool BR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAVES, 8))) void k_march_quad(const float *__restrict__ vol, Params P) {
     // entropy: the exact log's table in LDS (the launch's occupancy request
     // reserves far more than its 2 KiB); a load from there is an LDS read, not
@@ -1111,10 +1129,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
     float4 L0[4], L1[4], L2[4], L3[4];  // chunk registers of groups 0..3
     FootPacked fc = pack_foot(footprint(P, px, py, pz), alive);
     bool lc[4];
-    lc[0] = qc_gather<0>(vol, P, fc, g, L0);
-    lc[1] = qc_gather<1>(vol, P, fc, g, L1);
-    lc[2] = qc_gather<2>(vol, P, fc, g, L2);
-    lc[3] = qc_gather<3>(vol, P, fc, g, L3);
+    lc[0] = qc_gather<0, BR>(vol, P, fc, g, L0);
+    lc[1] = qc_gather<1, BR>(vol, P, fc, g, L1);
+    lc[2] = qc_gather<2, BR>(vol, P, fc, g, L2);
+    lc[3] = qc_gather<3, BR>(vol, P, fc, g, L3);
     for (int i = 0; i < kMaxSteps; i++) {
         if (!wave_any(alive)) break;
         // next step of this lane's own ray (speculative: assumes no early exit)
@@ -1123,10 +1141,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
         const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
         const FootPacked fn = pack_foot(footprint(P, nx, ny, nz), cont);
         bool ln[4];
-        const float b0 = qc_group<0, M>(vol, P, fc, lc[0], fn, ln[0], g, L0, s_lt);
-        const float b1 = qc_group<1, M>(vol, P, fc, lc[1], fn, ln[1], g, L1, s_lt);
-        const float b2 = qc_group<2, M>(vol, P, fc, lc[2], fn, ln[2], g, L2, s_lt);
-        const float b3 = qc_group<3, M>(vol, P, fc, lc[3], fn, ln[3], g, L3, s_lt);
+        const float b0 = qc_group<0, M, BR>(vol, P, fc, lc[0], fn, ln[0], g, L0, s_lt);
+        const float b1 = qc_group<1, M, BR>(vol, P, fc, lc[1], fn, ln[1], g, L1, s_lt);
+        const float b2 = qc_group<2, M, BR>(vol, P, fc, lc[2], fn, ln[2], g, L2, s_lt);
+        const float b3 = qc_group<3, M, BR>(vol, P, fc, lc[3], fn, ln[3], g, L3, s_lt);
         const float sample = g == 0 ? b0 : (g == 1 ? b1 : (g == 2 ? b2 : b3));
         if (alive) {
             n = i + 1;
@@ -2106,16 +2124,24 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             P.path = 2;
         }
         if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {
-            note_kernel("k_march_quad", B, method);
+            note_kernel(P.brick ? "k_march_quad_brick" : "k_march_quad", B, method);
             // The quad march uses no LDS; an LDS request caps it at 2 workgroups
             // (2 waves per SIMD) per CU, which trims the oblique view's line
             // re-reads: 1024^3x8 C1 3.73 -> 3.52 ms (3 per CU by registers, 1 per
             // CU 3.91).  VR_WG_PER_CU overrides.
             const size_t qlds = cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2);
-            switch (method) {
-            case 1: hipLaunchKernelGGL((k_march_quad<1>), grid, block, qlds, s, vol, P); break;
-            case 2: hipLaunchKernelGGL((k_march_quad<2>), grid, block, qlds, s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_quad<3>), grid, block, qlds, s, vol, P); break;
+            if (P.brick) {
+                switch (method) {
+                case 1: hipLaunchKernelGGL((k_march_quad<1, true>), grid, block, qlds, s, vol, P); break;
+                case 2: hipLaunchKernelGGL((k_march_quad<2, true>), grid, block, qlds, s, vol, P); break;
+                case 3: hipLaunchKernelGGL((k_march_quad<3, true>), grid, block, qlds, s, vol, P); break;
+                }
+            } else {
+                switch (method) {
+                case 1: hipLaunchKernelGGL((k_march_quad<1, false>), grid, block, qlds, s, vol, P); break;
+                case 2: hipLaunchKernelGGL((k_march_quad<2, false>), grid, block, qlds, s, vol, P); break;
+                case 3: hipLaunchKernelGGL((k_march_quad<3, false>), grid, block, qlds, s, vol, P); break;
+                }
             }
             return hipGetLastError();
         }

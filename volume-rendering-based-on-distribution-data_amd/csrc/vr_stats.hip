@@ -105,4 +105,33 @@ hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, hipStr
     return hipGetLastError();
 }
 
+// ---- 2x2 (x, y) micro-brick copy of an 8-bin volume (oblique views) ----
+// One 128-B line holds the records (x, y), (x+1, y), (x, y+1), (x+1, y+1) of
+// an even (x, y): record (x, y, z) sits at z*bsz + (y>>1)*bsy + (x>>1)*4 +
+// (y&1)*2 + (x&1) (brick_index).  Like a cudaArray, the copy is the
+// library's own layout of the uploaded records (K:1913-1918); the quad march
+// of oblique views reads it.  One thread per record.
+__global__ __launch_bounds__(256) void k_brick8(const float *__restrict__ vol, Params P,
+                                                float *__restrict__ out, uint64_t bsy,
+                                                uint64_t bsz) {
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    if (x >= (uint32_t)P.nx) return;
+    const uint32_t y = blockIdx.y, z = blockIdx.z;
+    const uint64_t src = (uint64_t)z * P.sz + (uint64_t)y * P.sy + x;
+    const uint64_t dst = brick_index(x, y, z, bsy, bsz);
+    const float4 *s4 = reinterpret_cast<const float4 *>(vol + src * 8);
+    float4 *d4 = reinterpret_cast<float4 *>(out + dst * 8);
+    const float4 a = s4[0], b = s4[1];
+    d4[0] = a;
+    d4[1] = b;
+}
+
+hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t bsy,
+                         uint64_t bsz, hipStream_t s) {
+    dim3 grid;
+    if (!bake_grid(P, grid)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_brick8, grid, dim3(256), 0, s, vol, P, out, bsy, bsz);
+    return hipGetLastError();
+}
+
 }  // namespace vr
