@@ -737,11 +737,13 @@ def test_quad_march_brick_layout(pkg, orc, gpu, dims, brick, monkeypatch):
     want = "k_march_quad_brick<" if brick == "1" else "k_march_quad<"
     for rot in ((30.0, 45.0), (-60.0, 110.0), (12.0, -70.0)):
         m = pkg.camera.display_inv_view(rot)
-        for method in (1, 2, 3):
+        for method in (1, 2, 3, 7):
             got = gpu_render(pkg, None, 88, 60, m, method, torch)
-            ref = orc.render(vol, orc.make_params(88, 60, m, query_method=method))[:3]
+            ref = orc.render(vol, orc.make_params(88, 60, m, query_method=method,
+                                                  m7_dims=dims))[:3]
             assert_parity(got, ref, f"{dims} brick={brick} {rot} m{method}")
-            assert pkg.last_kernel().startswith(want)
+            assert pkg.last_kernel().startswith(want if method != 7 else
+                                                want.replace("quad", "m7_quad"))
     W, H = 136, 72
     m = pkg.camera.display_inv_view((30.0, 45.0))
     full = gpu_render(pkg, None, W, H, m, 1, torch)[0]

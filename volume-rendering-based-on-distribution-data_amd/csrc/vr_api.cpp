@@ -1239,14 +1239,17 @@ int vr_render(const vr_render_desc *desc) {
             return fail(VR_ERR_UNSUPPORTED, "codec volumes with %d bins (compiled: 1,2,4,8,16,32)",
                         P.nb);
     } else {
-        const float *vol = g.vol;
-        if (P.path == 0 && g.nb == 8 && qm >= 1 && qm <= 3 && ensure_brick()) {
-            vol = g.brick;
-            P.brick = 1;
-            P.sy = g.bsy;
-            P.sz = g.bsz;
+        // the quad marches of oblique views (methods 1/2/3 on path 0; method 7
+        // when its grid is the volume's) read the micro-brick copy
+        const char *eq = std::getenv("VR_M7_QUAD");
+        const bool m7_quad = qm == 7 && P.oblique && P.m7x == P.nx && P.m7y == P.ny &&
+                             P.m7z == P.nz && !(eq && std::atoi(eq) == 0);
+        if (g.nb == 8 && ((P.path == 0 && qm >= 1 && qm <= 3) || m7_quad) && ensure_brick()) {
+            P.bvol = g.brick;
+            P.bsy = g.bsy;
+            P.bsz = g.bsz;
         }
-        e = vr::launch_march(g.nb, desc->query_method, vol, P, nslots, false, g.stream);
+        e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
     }
     if (e != hipSuccess) return hip_fail(e, "launch(k_march)");
     if (P.tile_cost) g.cost_recorded = true;

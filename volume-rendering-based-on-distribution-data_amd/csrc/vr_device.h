@@ -46,8 +46,11 @@ struct Params {
     int lds_cu, lds_wg;          // LDS bytes per CU / per workgroup (device attributes)
     int oblique;                 // view's screen x does not run along voxel rows
     int path;                    // kernel variant (vr_api.cpp fill_params)
-    int brick;                   // quad march: vol is the 2x2 (x, y) micro-brick copy,
-                                 // sy / sz its brick-row / slice pitches (brick_index)
+    // 2x2 (x, y) micro-brick copy of the 8-bin records for the quad marches of
+    // oblique views (nullptr: none), bsy / bsz its brick-row / slice pitches
+    // in records (brick_index); the launch passes it as vol with sy / sz = bsy / bsz
+    const float *bvol;
+    uint64_t bsy, bsz;
     // fractal/template codec (methods 4/5/6): codebook int4 per voxel, templates
     // [ntpl][nb], (bin, value) errors [voxel][err_slots]
     const int4 *cb;

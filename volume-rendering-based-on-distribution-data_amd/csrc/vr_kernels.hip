@@ -1000,7 +1000,7 @@ __device__ __forceinline__ FootPacked pack_foot(const Foot &f, bool live) {
 
 // Gather ray (G, q)'s four x-pairs: L[c] = chunk g of the pair at combo c =
 // (y = c & 1, z = c >> 1).  A pair clamped at the x edge (x1 == x0) repeats x0.
-// BR: the volume is the 2x2 (x, y) micro-brick copy (P.brick): lane g reads
+// BR: the volume is the 2x2 (x, y) micro-brick copy (P.bvol): lane g reads
 // half g & 1 of record x0 (g < 2) or x1 (g >= 2) of each (y, z) combo, so a
 // footprint's four (x, y) corners at one z share a line when x0 and y0 are
 // even (oblique views: fewer distinct lines per wave step).
@@ -1218,7 +1218,8 @@ __device__ __forceinline__ CellPacked pack_cell(const Params &P, const M7Cell &c
     return p;
 }
 
-template <int G>
+// BR: vol is the 2x2 (x, y) micro-brick copy (brick_index; P.sy / P.sz are its pitches)
+template <int G, bool BR = false>
 __device__ __forceinline__ bool qc_gather_cell(const float *__restrict__ vol, const Params &P,
                                                const CellPacked &cp, uint32_t g, float4 (&L)[4]) {
     const bool live = bcast_g<G>(cp.w3) != 0;
@@ -1228,10 +1229,21 @@ __device__ __forceinline__ bool qc_gather_cell(const float *__restrict__ vol, co
         const uint64_t xr = g < 2 ? (w0 & 0xFFFFu) : (w0 >> 16);
         const uint64_t y0 = w1 & 0xFFFFu, y1 = w1 >> 16, z0 = w2 & 0xFFFFu, z1 = w2 >> 16;
         const uint32_t chunk = g & 1u;
-        L[0] = reinterpret_cast<const float4 *>(vol + (z0 * P.sz + y0 * P.sy + xr) * 8)[chunk];
-        L[1] = reinterpret_cast<const float4 *>(vol + (z0 * P.sz + y1 * P.sy + xr) * 8)[chunk];
-        L[2] = reinterpret_cast<const float4 *>(vol + (z1 * P.sz + y0 * P.sy + xr) * 8)[chunk];
-        L[3] = reinterpret_cast<const float4 *>(vol + (z1 * P.sz + y1 * P.sy + xr) * 8)[chunk];
+        uint64_t r00, r10, r01, r11;
+        if constexpr (BR) {
+            const uint64_t bx = (xr >> 1) * 4u + (xr & 1u);
+            const uint64_t ry0 = (y0 >> 1) * P.sy + (y0 & 1u) * 2u + bx;
+            const uint64_t ry1 = (y1 >> 1) * P.sy + (y1 & 1u) * 2u + bx;
+            r00 = z0 * P.sz + ry0; r10 = z0 * P.sz + ry1;
+            r01 = z1 * P.sz + ry0; r11 = z1 * P.sz + ry1;
+        } else {
+            r00 = z0 * P.sz + y0 * P.sy + xr; r10 = z0 * P.sz + y1 * P.sy + xr;
+            r01 = z1 * P.sz + y0 * P.sy + xr; r11 = z1 * P.sz + y1 * P.sy + xr;
+        }
+        L[0] = reinterpret_cast<const float4 *>(vol + r00 * 8)[chunk];
+        L[1] = reinterpret_cast<const float4 *>(vol + r10 * 8)[chunk];
+        L[2] = reinterpret_cast<const float4 *>(vol + r01 * 8)[chunk];
+        L[3] = reinterpret_cast<const float4 *>(vol + r11 * 8)[chunk];
     }
     return live;
 }
@@ -1241,7 +1253,7 @@ __device__ __forceinline__ float qbcast(float v) {
     return qperm<K == 0 ? kQ0 : K == 1 ? kQ1 : K == 2 ? kQ2 : kQ3>(v);
 }
 
-template <int G>
+template <int G, bool BR>
 __device__ __forceinline__ float m7q_group(const float *__restrict__ vol, const Params &P,
                                            bool refresh_any, int refresh_bits, float xd, float yd,
                                            float zd, const CellPacked &fn, bool &ln, uint32_t g,
@@ -1250,7 +1262,7 @@ __device__ __forceinline__ float m7q_group(const float *__restrict__ vol, const 
     float r0[8], r1[8];
     pair_swap(L[0], L[1], odd, r0);  // corner (x = g>>1, y = g&1) at z0
     pair_swap(L[2], L[3], odd, r1);  //                              at z1
-    ln = qc_gather_cell<G>(vol, P, fn, g, L);
+    ln = qc_gather_cell<G, BR>(vol, P, fn, g, L);
     if (refresh_any && ((refresh_bits >> G) & 1)) {  // ray G left its cell: its new means
         mz[0] = raw_mean<8>(r0);
         mz[1] = raw_mean<8>(r1);
@@ -1271,6 +1283,7 @@ __device__ __forceinline__ float m7q_group(const float *__restrict__ vol, const 
     return (float)((double)m0 * (1.0 - (double)fzd) + (double)(m1 * fzd));
 }
 
+template <bool BR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAVES, 8))) void k_march_m7_quad(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
@@ -1299,10 +1312,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
     float mz0[2] = {0.f, 0.f}, mz1[2] = {0.f, 0.f}, mz2[2] = {0.f, 0.f}, mz3[2] = {0.f, 0.f};
     const CellPacked fc = pack_cell(P, cur, alive);
     bool lc[4];
-    lc[0] = qc_gather_cell<0>(vol, P, fc, g, L0);
-    lc[1] = qc_gather_cell<1>(vol, P, fc, g, L1);
-    lc[2] = qc_gather_cell<2>(vol, P, fc, g, L2);
-    lc[3] = qc_gather_cell<3>(vol, P, fc, g, L3);
+    lc[0] = qc_gather_cell<0, BR>(vol, P, fc, g, L0);
+    lc[1] = qc_gather_cell<1, BR>(vol, P, fc, g, L1);
+    lc[2] = qc_gather_cell<2, BR>(vol, P, fc, g, L2);
+    lc[3] = qc_gather_cell<3, BR>(vol, P, fc, g, L3);
     for (int i = 0; i < kMaxSteps; i++) {
         if (!wave_any(alive)) break;
         // the home ray at its current sample: refresh due? (its new cell's
@@ -1327,10 +1340,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
         const int rbits = qpermi<kQ0>(rb) | qpermi<kQ1>(rb) | qpermi<kQ2>(rb) | qpermi<kQ3>(rb);
         const bool rany = rbits != 0;
         bool ln[4];
-        const float b0 = m7q_group<0>(vol, P, rany, rbits, xd, yd, zd, fn, ln[0], g, L0, mz0);
-        const float b1 = m7q_group<1>(vol, P, rany, rbits, xd, yd, zd, fn, ln[1], g, L1, mz1);
-        const float b2 = m7q_group<2>(vol, P, rany, rbits, xd, yd, zd, fn, ln[2], g, L2, mz2);
-        const float b3 = m7q_group<3>(vol, P, rany, rbits, xd, yd, zd, fn, ln[3], g, L3, mz3);
+        const float b0 = m7q_group<0, BR>(vol, P, rany, rbits, xd, yd, zd, fn, ln[0], g, L0, mz0);
+        const float b1 = m7q_group<1, BR>(vol, P, rany, rbits, xd, yd, zd, fn, ln[1], g, L1, mz1);
+        const float b2 = m7q_group<2, BR>(vol, P, rany, rbits, xd, yd, zd, fn, ln[2], g, L2, mz2);
+        const float b3 = m7q_group<3, BR>(vol, P, rany, rbits, xd, yd, zd, fn, ln[3], g, L3, mz3);
         const float im = g == 0 ? b0 : (g == 1 ? b1 : (g == 2 ? b2 : b3));
         if (alive) {
             n = i + 1;
@@ -2124,17 +2137,20 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             P.path = 2;
         }
         if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {
-            note_kernel(P.brick ? "k_march_quad_brick" : "k_march_quad", B, method);
+            note_kernel(P.bvol ? "k_march_quad_brick" : "k_march_quad", B, method);
             // The quad march uses no LDS; an LDS request caps it at 2 workgroups
             // (2 waves per SIMD) per CU, which trims the oblique view's line
             // re-reads: 1024^3x8 C1 3.73 -> 3.52 ms (3 per CU by registers, 1 per
             // CU 3.91).  VR_WG_PER_CU overrides.
             const size_t qlds = cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2);
-            if (P.brick) {
+            if (P.bvol) {
+                Params Q = P;
+                Q.sy = P.bsy;
+                Q.sz = P.bsz;
                 switch (method) {
-                case 1: hipLaunchKernelGGL((k_march_quad<1, true>), grid, block, qlds, s, vol, P); break;
-                case 2: hipLaunchKernelGGL((k_march_quad<2, true>), grid, block, qlds, s, vol, P); break;
-                case 3: hipLaunchKernelGGL((k_march_quad<3, true>), grid, block, qlds, s, vol, P); break;
+                case 1: hipLaunchKernelGGL((k_march_quad<1, true>), grid, block, qlds, s, P.bvol, Q); break;
+                case 2: hipLaunchKernelGGL((k_march_quad<2, true>), grid, block, qlds, s, P.bvol, Q); break;
+                case 3: hipLaunchKernelGGL((k_march_quad<3, true>), grid, block, qlds, s, P.bvol, Q); break;
                 }
             } else {
                 switch (method) {
@@ -2253,9 +2269,17 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             const char *eq = std::getenv("VR_M7_QUAD");
             const bool quad = !(eq && std::atoi(eq) == 0);
             if (quad && P.oblique && P.m7x == P.nx && P.m7y == P.ny && P.m7z == P.nz) {
-                note_kernel("k_march_m7_quad", B, method);
-                hipLaunchKernelGGL(k_march_m7_quad, grid, block,
-                                   cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2), s, vol, P);
+                const size_t qlds = cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2);
+                if (P.bvol) {
+                    note_kernel("k_march_m7_quad_brick", B, method);
+                    Params Q = P;
+                    Q.sy = P.bsy;
+                    Q.sz = P.bsz;
+                    hipLaunchKernelGGL(k_march_m7_quad<true>, grid, block, qlds, s, P.bvol, Q);
+                } else {
+                    note_kernel("k_march_m7_quad", B, method);
+                    hipLaunchKernelGGL(k_march_m7_quad<false>, grid, block, qlds, s, vol, P);
+                }
                 break;
             }
         }
