@@ -403,9 +403,13 @@ def test_segmented_march_early_exit(pkg, orc, gpu, seg, nb, monkeypatch):
     assert torch.equal(frame, full)
 
 
-def test_padded_layout(pkg, orc, gpu, monkeypatch):
-    """pitched rows / slices (VR_PAD) change only addresses, never results"""
+@pytest.mark.parametrize("path", ["", "0"])
+def test_padded_layout(pkg, orc, gpu, path, monkeypatch):
+    """pitched rows / slices (VR_PAD) change only addresses, never results (path 0: the
+    quad march on the micro-brick copy made from the pitched records)"""
     import torch
+    if path:
+        monkeypatch.setenv("VR_PATH", path)
     vol = orc.synth_volume(20, 18, 16, 8)
     ref = orc.render(vol, orc.make_params(64, 48, pkg.camera.display_inv_view(), query_method=1))[:3]
     for pad in ("4,0", "3,77"):
@@ -415,6 +419,8 @@ def test_padded_layout(pkg, orc, gpu, monkeypatch):
         pkg.synthesize((20, 18, 16), 8)
         got = gpu_render(pkg, None, 64, 48, pkg.camera.display_inv_view(), 1, torch)
         assert_parity(got, ref, f"synth pad {pad}")
+        if path == "0":
+            assert pkg.last_kernel().startswith("k_march_quad_brick<")
 
 
 def test_fast_log_is_exact_for_every_float(pkg, gpu):

@@ -2142,7 +2142,13 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // (2 waves per SIMD) per CU, which trims the oblique view's line
             // re-reads: 1024^3x8 C1 3.73 -> 3.52 ms (3 per CU by registers, 1 per
             // CU 3.91).  VR_WG_PER_CU overrides.
-            const size_t qlds = cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2);
+            // A rank's tile list of <= 400 K rays (8 GPUs at 1080p) runs at 1 per
+            // CU: its tiles are scattered over the frame, and fewer rays in flight
+            // re-read fewer lines (cost-dealt C1 lists, max over 8 ranks: 0.71 ->
+            // 0.59 ms; 3 per CU 0.68; tools/rank_sim.py)
+            const int qcap = P.wg_per_cu > 0 ? P.wg_per_cu
+                             : (P.tile_list && (uint64_t)nslots * 256u <= 400000u) ? 1 : 2;
+            const size_t qlds = cap_lds(P, qcap);
             if (P.bvol) {
                 Params Q = P;
                 Q.sy = P.bsy;
