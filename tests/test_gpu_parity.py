@@ -146,13 +146,14 @@ def test_oblique_coarse_volume_takes_segmented_march(pkg, orc, gpu):
 def test_row_aligned_coarse_volume_takes_box_march(pkg, orc, gpu, monkeypatch):
     """row-aligned full frame, >= 4 pixels per voxel, more rays than the segmented
     threshold: methods 1/2 stage the wave's footprint box in LDS (path 1),
-    bit-identical; entropy keeps the wave-staged march"""
+    bit-identical; entropy keeps the wave-staged march; a frame below the threshold takes
+    the ray-segmented march"""
     import torch
     monkeypatch.setenv("VR_SEG_RAYS", "1000")
     vol = orc.synth_volume(20, 18, 16, 8)
     m = pkg.camera.display_inv_view((0.0, 0.0), translation=(0.05, -0.1, 0.0))
     for method, W, H, kern in ((1, 96, 64, "k_march<"), (2, 96, 64, "k_march<"),
-                               (3, 96, 64, "k_march_ws"), (1, 32, 24, "k_march_pipe")):
+                               (3, 96, 64, "k_march_ws"), (1, 32, 24, "k_march_segp4")):
         got = gpu_render(pkg, vol, W, H, m, method, torch)
         ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
         assert_parity(got, ref, f"coarse rows m{method} {W}x{H}")
@@ -292,6 +293,7 @@ def test_adaptive_frame_order_renders_identical_frames(pkg, orc, gpu, adapt, mon
     tile costs, the 2nd re-deals the tiles by them; every frame is the oracle's;
     a new view / new volume starts over"""
     import torch
+    monkeypatch.setenv("VR_SEG_RAYS", "0")  # keep this small frame on the recording march
     if not adapt:
         monkeypatch.setenv("VR_NO_ADAPT", "1")
     vol = orc.synth_volume(48, 40, 36, 8)
@@ -766,3 +768,24 @@ def test_quad_march_brick_layout(pkg, orc, gpu, dims, brick, monkeypatch):
     pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
     torch.cuda.synchronize()
     assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), full)
+
+
+@pytest.mark.parametrize("dims,nb,W,H,want", [
+    ((40, 36, 32), 1, 256, 256, "k_march_segp4<"), ((40, 36, 32), 4, 512, 320, None),
+    ((40, 36, 32), 8, 256, 200, "k_march_segp4<")])
+def test_small_frames_take_segmented_march(pkg, orc, gpu, dims, nb, W, H, want):
+    """small full frames run the pipelined ray-segmented march: 4 lanes per ray up to
+    128 K rays; oblique views (B < 8) 2 lanes up to 700 K, row-aligned ones one lane
+    above 128 K; bit-identical"""
+    import torch
+    vol = orc.synth_volume(*dims, nb)
+    pkg.init_distribution(vol)
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))):
+        for method in (1, 2):
+            got = gpu_render(pkg, None, W, H, cam, method, torch)
+            ref = orc.render(vol, orc.make_params(W, H, cam, query_method=method))[:3]
+            assert_parity(got, ref, f"{dims}x{nb} {W}x{H} m{method}")
+            rows = abs(float(cam[0])) >= 0.95
+            k = want or ("k_march_pipe<" if rows else "k_march_segp2<")
+            if nb < 8 or rows:
+                assert pkg.last_kernel().startswith(k), pkg.last_kernel()

@@ -551,6 +551,25 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         (uint64_t)d->width * d->height > seg_rays &&
         (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
         P.path = 1;
+    // Small full frames (BASELINE configs 1 and 2: 128^3 x 1 at 256^2, 256^3 x 4
+    // at 512^2) cannot fill the GPU with one ray per lane, so the per-ray step
+    // chain sets the time, as for a rank's tile list: the pipelined
+    // ray-segmented march, 4 lanes per ray up to 128 K rays, else 2.  Measured
+    // (profiles/r02/small_frames.log): 128^3 x 1 C0 0.136 -> 0.082 ms, C1
+    // 0.180 -> 0.093; 256^3 x 4 C1 0.224 -> 0.147, while its row-aligned view
+    // (262 K rays) stays on the one-lane march (0.136 vs 0.139).  Oblique views
+    // of 8-bin volumes keep the quad march (as for oblique rank lists).
+    int small_seg = 0;
+    {
+        const uint64_t rays = (uint64_t)d->width * d->height;
+        const bool nb_ok = g.nb == 1 || g.nb == 2 || g.nb == 4 || (g.nb == 8 && along_rows);
+        const uint64_t limit = along_rows ? std::min<uint64_t>(seg_rays, 131072) : seg_rays;
+        if (!d->d_tile_list && !codec && !flex && rays <= limit && nb_ok &&
+            (d->query_method == 1 || d->query_method == 2)) {
+            P.path = 7;
+            small_seg = rays <= 131072 ? -4 : -2;
+        }
+    }
     if (const char *e = std::getenv("VR_PATH")) {
         const int v = std::atoi(e);
         if (v >= 0 && v <= 9) P.path = v;
@@ -558,7 +577,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     P.wave_clock = g.wave_clock;
     P.tile_cost = record;
     P.hyb_tiles = 0;
-    P.seg_lanes = -2;  // VR_SEG=S: S lanes per ray, negative = pipelined windows
+    P.seg_lanes = small_seg ? small_seg : -2;  // VR_SEG=S: S lanes per ray, negative = pipelined windows
     if (const char *e = std::getenv("VR_SEG")) {
         const int v = std::atoi(e);
         if (v != 0 && v >= -8 && v <= 8 && (abs(v) & (abs(v) - 1)) == 0) P.seg_lanes = v;
