@@ -108,12 +108,14 @@ void dataProcessing(void);
 #define VR_ERR_UNSUPPORTED -4
 
 /* Baked statistics (basicDataProcessing).  vr_bake_stats bakes the planes of
- * the resident raw and codec volumes that are not baked yet: 4 planes of
- * slice_pitch * depth floats for the raw volume (mean, variance, entropy and
- * method 7's undivided corner mean at record index
- * z * slice_pitch + y * row_pitch + x, vr_volume_layout) and 3
- * planes of X * Y * Z floats for the codec volume (methods 4/5/6, dense voxel
- * order).  Re-uploading or releasing a volume drops its planes; a volume
+ * the resident raw and codec volumes that are not baked yet: 4 planes for the
+ * raw volume (mean, variance, entropy and method 7's undivided corner mean)
+ * and 3 for the codec volume (methods 4/5/6).  A plane is laid out in
+ * 16 x 2 x 1 bricks whose x runs overlap by one voxel: with
+ * sy = ((X - 1) / 15 + 1) * 32 and sz = ((Y + 1) / 2) * sy floats, voxel
+ * (x, y, z) sits at z * sz + (y / 2) * sy + (y % 2) * 16 + (x / 15) * 32 +
+ * x % 15 (and, for x = 15 k > 0, also at offset 15 of brick k - 1); a plane
+ * holds sz * Z floats.  Re-uploading or releasing a volume drops its planes; a volume
  * modified in place through vr_volume_info's pointer must be re-baked
  * (vr_release_stats, then vr_bake_stats).  vr_stats_info: device pointers
  * (nullptr = not baked) and plane lengths in floats. */

@@ -32,28 +32,45 @@ def _d2h(ptr, n):
     return out
 
 
+def plane_geometry(nx, ny):
+    """pitches of a baked plane (vr_device.h plane_pitches): 16 x 2 x 1 bricks, x runs
+    of 16 starting every 15 voxels (one apron voxel)"""
+    sy = ((nx - 1) // 15 + 1) * 32
+    return sy, ((ny + 1) // 2) * sy
+
+
+def plane_index(x, y, z, sy, sz):
+    """vr_device.h plane_index: voxel (x, y, z) at its home brick (x // 15)"""
+    kx = x // 15
+    return z * sz + (y >> 1) * sy + (y & 1) * 16 + kx * 32 + (x - 15 * kx)
+
+
+@pytest.mark.parametrize("nx,ny,nz", [(9, 7, 5), (31, 6, 3), (46, 3, 2)])
 @pytest.mark.parametrize("nb", [1, 3, 4, 8, 32])
-def test_planes_equal_oracle_stats(pkg, orc, gpu, baked, nb, monkeypatch):
-    """plane k < 3 at record index z*slice_pitch + y*row_pitch + x = statistic k+1 of that
-    record (orc_record_stats), plane 3 = method 7's corner mean (orc_corner_mean), bit for
-    bit, also with padded rows / slices"""
+def test_planes_equal_oracle_stats(pkg, orc, gpu, baked, nb, nx, ny, nz, monkeypatch):
+    """plane k < 3 at plane_index(x, y, z) = statistic k+1 of record (x, y, z)
+    (orc_record_stats), plane 3 = method 7's corner mean (orc_corner_mean), bit for bit;
+    x = 15 k also in the apron (offset 15) of brick k - 1; records with padded rows /
+    slices"""
     monkeypatch.setenv("VR_PAD", "3,5")
-    nx, ny, nz = 9, 7, 5
     vol = orc.synth_volume(nx, ny, nz, nb)
     pkg.init_distribution(vol)
     assert pkg.stats_info()[0][0] is None
     pkg.basicDataProcessing()
     (ptr, plane), _ = pkg.stats_info()
-    sy, sz = pkg.volume_layout()
-    assert ptr and plane == sz * nz and sy == nx + 3 and sz == sy * ny + 5
+    sy, sz = plane_geometry(nx, ny)
+    assert ptr and plane == sz * nz
     got = _d2h(ptr, 4 * plane).reshape(4, plane)
     for z in range(nz):
         for y in range(ny):
             for x in range(nx):
                 want = np.append(orc.record_stats(vol[z, y, x]),
                                  np.float32(orc.corner_mean(vol[z, y, x]))).astype(np.float32)
-                have = got[:, z * sz + y * sy + x]
-                assert np.array_equal(have.view(np.uint32), want.view(np.uint32)), (x, y, z)
+                i = plane_index(x, y, z, sy, sz)
+                assert np.array_equal(got[:, i].view(np.uint32), want.view(np.uint32)), (x, y, z)
+                if x > 0 and x % 15 == 0:
+                    assert np.array_equal(got[:, i - 32 + 15].view(np.uint32),
+                                          want.view(np.uint32)), ("apron", x, y, z)
 
 
 @pytest.mark.parametrize("nb", [1, 4, 5, 8, 32])
@@ -78,7 +95,8 @@ def test_baked_render_parity(pkg, orc, gpu, baked, nb):
     ("7", {"VR_SEG": "-8"}), ("2", {"VR_WG_PER_CU": "2"}), ("7", {"VR_SEG": "1"}),
 ])
 def test_baked_paths(pkg, orc, gpu, baked, path, env, monkeypatch):
-    """every kernel a baked frame can take (VR_PATH 1 / 2 / 7) is bit-identical"""
+    """every kernel a baked frame can take (VR_PATH 2 / 7; 1, the LDS-box march over x
+    rows, is ignored for the bricked planes) is bit-identical"""
     import torch
     monkeypatch.setenv("VR_PATH", path)
     for k, v in env.items():
@@ -127,11 +145,14 @@ def test_baked_codec(pkg, orc, gpu, baked, nb):
     pkg.init_codec(cb, t, e)
     pkg.basicDataProcessing()
     _, (ptr, plane) = pkg.stats_info()
-    assert ptr and plane == 22 * 18 * 14
+    sy, sz = plane_geometry(22, 18)
+    assert ptr and plane == sz * 14
     got = _d2h(ptr, 3 * plane).reshape(3, plane)
-    for v in range(0, plane, 7):
+    for v in range(0, 22 * 18 * 14, 7):
         want = orc.codec_stats(cb, t, e, v)
-        assert np.array_equal(got[:, v].view(np.uint32), want.view(np.uint32)), v
+        x, y, z = v % 22, (v // 22) % 18, v // (22 * 18)
+        i = plane_index(x, y, z, sy, sz)
+        assert np.array_equal(got[:, i].view(np.uint32), want.view(np.uint32)), v
     for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view()):
         for method in (4, 5, 6):
             got_f = codec_render(pkg, 72, 56, cam, method, torch)

@@ -70,6 +70,7 @@ struct State {
     // not baked, the march decodes the records at every step
     float *stats = nullptr, *cstats = nullptr;
     uint64_t stats_plane = 0, cstats_plane = 0;
+    uint64_t stats_sy = 0, stats_sz = 0, cstats_sy = 0, cstats_sz = 0;  // plane_pitches
     // 2x2 (x, y) micro-brick copy of an owned 8-bin volume for the quad march
     // of oblique views (ensure_brick, brick_index); nullptr = not made
     float *brick = nullptr;
@@ -419,8 +420,10 @@ void device_lds(int &per_cu, int &per_wg) {
 // gather8's 32-bit addressing of a baked plane: pitches and depth fit 24-bit
 // multiplies and the byte offset of every element fits 32 bits (a 1024^3 plane,
 // 2^30 floats, does: the last element sits at 2^32 - 4)
-int narrow_index(uint64_t sy, uint64_t sz, uint64_t nz) {
-    return sy < (1u << 24) && sz < (1u << 24) && nz < (1u << 24) && sz * nz <= (1ull << 30);
+// a baked plane's index fits the 32-bit form of gather8 (MODE 1: 24-bit
+// multiplies, 32-bit sums): pitches and depth < 2^24, plane < 2^32 floats
+int plane_narrow(uint64_t sy, uint64_t sz, uint64_t nz) {
+    return sy < (1u << 24) && sz < (1u << 24) && nz < (1u << 24) && sz * nz < (1ull << 32);
 }
 
 int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
@@ -608,7 +611,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
 // 1024^3 C0 0.375 ms); oblique views, whose lanes' loads touch many lines per
 // instruction, split each ray over 4 lanes (path 7, VR_SEG 4: 1024^3 C1 2.02
 // -> 1.32 ms, 1.11 at 4 workgroups per CU).  A deeper look-ahead ring (2-8 steps in flight per lane) was
-// slower everywhere but 512^3 C1 (within 3 %).  VR_PATH (1 / 2 / 7) overrides;
+// slower everywhere but 512^3 C1 (within 3 %).  VR_PATH (2 / 7) overrides;
 // P.seg_lanes keeps a VR_SEG setting.
 int baked_path(const vr_render_desc *d, vr::Params &P) {
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
@@ -632,9 +635,9 @@ int baked_path(const vr_render_desc *d, vr::Params &P) {
     if (!along_rows && !d->d_tile_list && P.wg_per_cu == 0 &&
         (uint64_t)d->width * d->height < 4ull * (uint64_t)P.nx * (uint64_t)P.ny)
         P.wg_per_cu = 4;
-    if (const char *e = std::getenv("VR_PATH")) {
+    if (const char *e = std::getenv("VR_PATH")) {  // the LDS-box march (1) reads x rows only
         const int v = std::atoi(e);
-        if (v == 1 || v == 2 || v == 7) path = v;
+        if (v == 2 || v == 7) path = v;
     }
     return path;
 }
@@ -651,11 +654,13 @@ int bake_stats() {
         P.sy = g.sy; P.sz = g.sz;
         P.nb = g.nb;
         P.enorm = entropy_norm(g.nb);
-        const uint64_t plane = g.sz * (uint64_t)g.nz;
-        float *buf = nullptr;  // + 4 floats: the pair loads of the march read x0 + 1
+        uint64_t psy = 0, psz = 0;
+        vr::plane_pitches((uint32_t)g.nx, (uint32_t)g.ny, psy, psz);
+        const uint64_t plane = psz * (uint64_t)g.nz;
+        float *buf = nullptr;
         VR_HIP(hipMalloc(&buf, (4 * plane + 4) * sizeof(float)));
         hipError_t e = hipMemsetAsync(buf, 0, (4 * plane + 4) * sizeof(float), g.stream);
-        if (e == hipSuccess) e = vr::launch_bake_raw(g.vol, P, buf, plane, g.stream);
+        if (e == hipSuccess) e = vr::launch_bake_raw(g.vol, P, buf, plane, psy, psz, g.stream);
         if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
         if (e != hipSuccess) {
             (void)hipFree(buf);
@@ -663,6 +668,8 @@ int bake_stats() {
         }
         g.stats = buf;
         g.stats_plane = plane;
+        g.stats_sy = psy;
+        g.stats_sz = psz;
     }
     if (g.cb && !g.cstats) {
         std::memset(&P, 0, sizeof P);
@@ -676,11 +683,13 @@ int bake_stats() {
         P.err = g.cerr;
         P.ntpl = g.ntpl;
         P.err_slots = g.err_slots;
-        const uint64_t plane = P.sz * (uint64_t)g.cnz;
-        float *buf = nullptr;  // + 4 floats as above
+        uint64_t psy = 0, psz = 0;
+        vr::plane_pitches((uint32_t)g.cnx, (uint32_t)g.cny, psy, psz);
+        const uint64_t plane = psz * (uint64_t)g.cnz;
+        float *buf = nullptr;
         VR_HIP(hipMalloc(&buf, (3 * plane + 4) * sizeof(float)));
         hipError_t e = hipMemsetAsync(buf, 0, (3 * plane + 4) * sizeof(float), g.stream);
-        if (e == hipSuccess) e = vr::launch_bake_codec(P, buf, plane, g.stream);
+        if (e == hipSuccess) e = vr::launch_bake_codec(P, buf, plane, psy, psz, g.stream);
         if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
         if (e != hipSuccess) {
             (void)hipFree(buf);
@@ -690,6 +699,8 @@ int bake_stats() {
         }
         g.cstats = buf;
         g.cstats_plane = plane;
+        g.cstats_sy = psy;
+        g.cstats_sz = psz;
     }
     return VR_OK;
 }
@@ -1243,12 +1254,17 @@ int vr_render(const vr_render_desc *desc) {
         // method 7 from the baked corner means (plane 3): the same corner cache
         // and double lerps (K:395-480), 4 bytes per corner refresh
         P.nb = 1;
+        P.sy = g.stats_sy;
+        P.sz = g.stats_sz;
         e = vr::launch_march(1, -7, g.stats + 3 * g.stats_plane, P, nslots, false, g.stream);
     } else if (baked) {
-        // one float per corner voxel, the same filter and composite (vr_stats.hip)
+        // one float per corner voxel, the same filter and composite (vr_stats.hip),
+        // addressed in the planes' bricks
         P.nb = 1;
+        P.sy = qm <= 3 ? g.stats_sy : g.cstats_sy;
+        P.sz = qm <= 3 ? g.stats_sz : g.cstats_sz;
         P.path = baked_path(desc, P);
-        const bool narrow = narrow_index(P.sy, P.sz, (uint64_t)P.nz);
+        const bool narrow = plane_narrow(P.sy, P.sz, (uint64_t)P.nz);
         e = vr::launch_march(1, narrow ? 0 : -1, baked, P, nslots, false, g.stream);
     } else if (is_flex_method(desc->query_method)) {
         e = vr::launch_march_flex(desc->query_method, P, nslots, g.stream);

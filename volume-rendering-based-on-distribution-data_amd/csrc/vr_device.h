@@ -91,6 +91,36 @@ __host__ __device__ __forceinline__ uint64_t brick_index(uint64_t x, uint64_t y,
     return z * bsz + (y >> 1) * bsy + (x >> 1) * 4u + (y & 1u) * 2u + (x & 1u);
 }
 
+// Baked statistics planes (basicDataProcessing, vr_stats.hip): 16 x 2 x 1
+// bricks -- one 128-B line holds 16 x-neighbours of two y rows -- whose x
+// runs overlap by one voxel (brick kx covers x = 15 kx .. 15 kx + 15), so the
+// x-pair of every footprint is one 8-byte load inside one line.  Row pitch
+// (floats per row of bricks, two y rows) and slice pitch: plane_pitches.  Fewer
+// distinct lines per frame than x rows at both the row-aligned and the oblique
+// bench views (simulated per 64x4 tile at 1024^3: C0 1.80 -> 1.57 GB, C1 4.47 ->
+// 3.79; tools/footprint_sim.c LAYOUT=10).
+constexpr uint32_t kPlaneStride = 15;  // x step between bricks (16 wide: one apron voxel)
+__host__ __device__ __forceinline__ void plane_pitches(uint32_t nx, uint32_t ny, uint64_t &sy,
+                                                       uint64_t &sz) {
+    const uint64_t nbx = nx > 0 ? (uint64_t)(nx - 1) / kPlaneStride + 1 : 0;
+    sy = nbx * 32u;
+    sz = (uint64_t)((ny + 1) / 2) * sy;
+}
+// x / 15 for x < 2^16, and the offset of x's pair (x, x + 1) in its brick row
+__host__ __device__ __forceinline__ uint32_t plane_bx(uint32_t x) {
+    const uint32_t kx = (x * 0x8889u) >> 19;
+    return kx * 32u + (x - kPlaneStride * kx);
+}
+// plane index of voxel (x, y, z) in the brick whose run starts at or below x
+// by at most 14 (its home); x = 15 k (k > 0) is also stored at offset 15 of
+// brick k - 1, where pairs starting at 15 k - 1 read it
+// (a slice, (Y + 1) / 2 * sy floats, is < 2^32: the in-slice part is 32-bit and
+// the index one 64-bit multiply-add)
+__host__ __device__ __forceinline__ uint64_t plane_index(uint32_t x, uint32_t y, uint32_t z,
+                                                         uint64_t sy, uint64_t sz) {
+    return (uint64_t)z * sz + (uint32_t)((y >> 1) * (uint32_t)sy + (y & 1u) * 16u + plane_bx(x));
+}
+
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)
 
 

@@ -80,11 +80,13 @@ hipError_t launch_march_gmm(int K, int method, const Params &P, uint32_t nblocks
                             hipStream_t s);
 hipError_t launch_synth_gmm(float *wm, float *sg, const SynthArgs &a, int K, int z_base, int nzs,
                             hipStream_t s);
-// ---- baked statistics (basicDataProcessing, vr_stats.hip): three planes of
-// `plane` floats each, statistic k+1 (raw) / C = k (codec) at the volume's record index
+// ---- baked statistics (basicDataProcessing, vr_stats.hip): planes of `plane`
+// floats each in 16 x 2 x 1 bricks of plane pitches psy / psz (plane_index),
+// statistic k+1 (raw) / C = k (codec)
 hipError_t launch_bake_raw(const float *vol, const Params &P, float *out, uint64_t plane,
-                           hipStream_t s);
-hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, hipStream_t s);
+                           uint64_t psy, uint64_t psz, hipStream_t s);
+hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, uint64_t psy,
+                             uint64_t psz, hipStream_t s);
 // 2x2 (x, y) micro-brick copy of an 8-bin volume (oblique views, vr_stats.hip):
 // pitches bsy (records per brick row) and bsz (records per slice), brick_index
 hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t bsy,

@@ -1391,7 +1391,9 @@ template <int B, bool BK = false>
 __device__ __forceinline__ float corner_mean(const float *__restrict__ vol, const Params &P,
                                              float ux, float uy, float uz) {
     const int ix = point_axis(ux, P.nx), iy = point_axis(uy, P.ny), iz = point_axis(uz, P.nz);
-    const uint64_t vidx = (uint64_t)iz * P.sz + (uint64_t)iy * P.sy + (uint64_t)ix;
+    // BK: the baked plane's 16 x 2 x 1 bricks (plane_index, P.sy / P.sz its pitches)
+    const uint64_t vidx = BK ? plane_index((uint32_t)ix, (uint32_t)iy, (uint32_t)iz, P.sy, P.sz)
+                             : (uint64_t)iz * P.sz + (uint64_t)iy * P.sy + (uint64_t)ix;
     if constexpr (B > 0) {
         float rec[B];
         load_rec<B>(vol, vidx, rec);
@@ -1429,7 +1431,7 @@ __device__ void m7_refresh(const float *__restrict__ vol, const Params &P, float
 // leaves, the refresh at that position computes exactly that cell
 // (floor/ceil of the same float position), so it decodes the gathered
 // records.  Bit-identical to k_march_m7.
-template <int B>
+template <int B, bool BK = false>
 __device__ __forceinline__ void m7_gather(const float *__restrict__ vol, const Params &P,
                                           const M7Cell &c, float (&rec)[8][B]) {
     const int x0 = point_axis(c.fx, P.nx), x1 = point_axis(c.cx, P.nx);
@@ -1437,9 +1439,12 @@ __device__ __forceinline__ void m7_gather(const float *__restrict__ vol, const P
     const int z0 = point_axis(c.fz, P.nz), z1 = point_axis(c.cz, P.nz);
     const int xs[2] = {x0, x1}, ys[2] = {y0, y1}, zs[2] = {z0, z1};
 #pragma unroll
-    for (int j = 0; j < 8; j++)
-        load_rec<B>(vol, (uint64_t)zs[j >> 2] * P.sz + (uint64_t)ys[(j >> 1) & 1] * P.sy +
-                             (uint64_t)xs[j & 1], rec[j]);
+    for (int j = 0; j < 8; j++) {
+        const uint32_t x = (uint32_t)xs[j & 1], y = (uint32_t)ys[(j >> 1) & 1],
+                       z = (uint32_t)zs[j >> 2];
+        load_rec<B>(vol, BK ? plane_index(x, y, z, P.sy, P.sz)
+                            : (uint64_t)z * P.sz + (uint64_t)y * P.sy + x, rec[j]);
+    }
 }
 
 #ifndef VR_M7_PIPE_MAXWAVES
@@ -1469,7 +1474,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PI
     M7Cell cur = m7_cell(P, px, py, pz), ca, cb;  // K:320-352 at the first sample
     float mean[8];
     float ra[8][B], rb[8][B];
-    m7_gather<B>(vol, P, cur, ra);
+    m7_gather<B, BK>(vol, P, cur, ra);
 #pragma unroll
     for (int j = 0; j < 8; j++) mean[j] = m7_rec_mean<B, BK>(ra[j]);
     ca = cur;
@@ -1490,7 +1495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PI
         const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);    // K:703, K:381
         const float nx = px + stx, ny = py + sty, nz = pz + stz;    // K:706
         cn = m7_cell(P, nx, ny, nz);
-        m7_gather<B>(vol, P, cn, rn);
+        m7_gather<B, BK>(vol, P, cn, rn);
         const float xd = (px * 0.5f + 0.5f - cur.fx) / (cur.cx - cur.fx);
         const float yd = (py * 0.5f + 0.5f - cur.fy) / (cur.cy - cur.fy);
         const float zd = (pz * 0.5f + 0.5f - cur.fz) / (cur.cz - cur.fz);
@@ -2206,8 +2211,8 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             return hipGetLastError();
         }
         if (B < 8 && P.path == 0) P.path = 2;  // per-ray pipelined for narrow records
-        if constexpr (B == 1) {  // baked statistics (vr_stats.hip): paths 1, 2, 7 only
-            if (method <= 0 && P.path != 1) P.path = 2;
+        if constexpr (B == 1) {  // baked statistics (vr_stats.hip, bricked planes): paths 2, 7 only
+            if (method <= 0) P.path = 2;
         }
         if (P.path == 2 && method >= -1 && method <= 3) {
             note_kernel("k_march_pipe", B, method);
@@ -2234,11 +2239,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     if (!COUNT) note_kernel(method == 7 ? "k_march_m7" : "k_march", B, method);
     switch (method) {
     case 0:
-    case -1:  // baked statistics: the box / direct march addresses in 64 bits either way
-        if constexpr (B == 1 && !COUNT) {
-            hipLaunchKernelGGL((k_march<1, -1, false>), grid, block, lds, s, vol, P);
-            break;
-        }
+    case -1:  // baked statistics: the pipelined / segmented marches only (bricked planes)
         return hipErrorInvalidValue;
     case 1: hipLaunchKernelGGL((k_march<B, 1, COUNT>), grid, block, lds, s, vol, P); break;
     case 2: hipLaunchKernelGGL((k_march<B, 2, COUNT>), grid, block, lds, s, vol, P); break;

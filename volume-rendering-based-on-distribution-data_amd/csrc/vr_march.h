@@ -149,58 +149,49 @@ __device__ __forceinline__ float blend8(const float (&s)[8], const Foot &f) {
     const float c1 = lerpq(c01, c11, f.ay);
     return lerpq(c0, c1, f.az);
 }
-// NARROW (the baked statistics planes, B = 1, method template 0): indices
-// from 24-bit multiplies and loads at a 32-bit byte offset from the uniform
-// base (global_load with an SGPR base) instead of 64-bit address arithmetic
-// per corner -- the march over a baked plane is VALU-heavy, its records are 4
-// bytes.  The caller guarantees pitches and depth < 2^24 and every byte offset
-// < 2^32 (vr_api.cpp narrow_index).
-__device__ __forceinline__ float load_at(const float *__restrict__ vol, uint32_t i) {
-    return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(vol) + (i << 2));
-}
-// statistics i and i+1 in one 8-byte load at 4-byte alignment (one address per
-// lane for both x corners; the plane is allocated one float long so i+1 exists)
+// a baked plane's x-pair in one 8-byte load at 4-byte alignment (one address
+// per lane for both x corners; bricks keep every pair inside one line)
 typedef float vr_f2a4 __attribute__((ext_vector_type(2), aligned(4)));
-__device__ __forceinline__ vr_f2a4 load_pair(const float *__restrict__ vol, uint32_t i) {
-    return *reinterpret_cast<const vr_f2a4 *>(reinterpret_cast<const char *>(vol) + (i << 2));
+__device__ __forceinline__ vr_f2a4 load_pair64(const float *__restrict__ vol, uint64_t i) {
+    return *reinterpret_cast<const vr_f2a4 *>(vol + i);
 }
-template <int B, bool NARROW = false>
+// MODE 0: records in x rows (P.sy / P.sz record pitches).  MODE 1 / 2: a baked
+// statistics plane (B = 1) in 16 x 2 x 1 bricks (plane_index; P.sy / P.sz the
+// plane pitches): each (y, z) row's x-pair is one 8-byte load; MODE 1 forms the
+// index with 24-bit multiplies in 32 bits (pitches < 2^24, plane < 2^32 floats:
+// vr_api.cpp plane_narrow), MODE 2 in 64 bits.
+template <int B, int MODE = 0>
 __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Params &P,
                                         const Foot &f, float (&rec)[8][B]) {
-    if constexpr (NARROW) {
-        static_assert(B == 1, "narrow addressing is for one-float records");
-        {
+    if constexpr (MODE != 0) {
+        static_assert(B == 1, "baked planes hold one float per voxel");
+        const uint32_t bx = plane_bx((uint32_t)f.x0);
+        const bool ox = f.x1 != f.x0;
+        uint64_t i00, i10, i01, i11;
+        if constexpr (MODE == 1) {
             const uint32_t sy = (uint32_t)P.sy, sz = (uint32_t)P.sz;
-            const uint32_t i0 = __umul24((uint32_t)f.z0, sz) + __umul24((uint32_t)f.y0, sy) +
-                                (uint32_t)f.x0;
-            const uint32_t ox = (uint32_t)(f.x1 - f.x0);
-            const uint32_t oy = __umul24((uint32_t)(f.y1 - f.y0), sy);
-            const uint32_t oz = __umul24((uint32_t)(f.z1 - f.z0), sz);
-#ifdef VR_BAKED_SINGLE  // A/B builds only: one 4-byte load per corner
-            rec[0][0] = load_at(vol, i0);
-            rec[1][0] = load_at(vol, i0 + ox);
-            rec[2][0] = load_at(vol, i0 + oy);
-            rec[3][0] = load_at(vol, i0 + oy + ox);
-            rec[4][0] = load_at(vol, i0 + oz);
-            rec[5][0] = load_at(vol, i0 + oz + ox);
-            rec[6][0] = load_at(vol, i0 + oz + oy);
-            rec[7][0] = load_at(vol, i0 + oz + oy + ox);
-#else
-            // x corners as one pair load per (y, z) row: half the gather
-            // instructions; x1 == x0 (clamped edge) takes the pair's first value
-            const vr_f2a4 a = load_pair(vol, i0), b = load_pair(vol, i0 + oy);
-            const vr_f2a4 c = load_pair(vol, i0 + oz), d = load_pair(vol, i0 + oz + oy);
-            rec[0][0] = a.x;
-            rec[1][0] = ox ? a.y : a.x;
-            rec[2][0] = b.x;
-            rec[3][0] = ox ? b.y : b.x;
-            rec[4][0] = c.x;
-            rec[5][0] = ox ? c.y : c.x;
-            rec[6][0] = d.x;
-            rec[7][0] = ox ? d.y : d.x;
-#endif
-            return;
+            const uint32_t z0 = __umul24((uint32_t)f.z0, sz), z1 = __umul24((uint32_t)f.z1, sz);
+            const uint32_t y0 = __umul24((uint32_t)f.y0 >> 1, sy) + ((uint32_t)f.y0 & 1u) * 16u + bx;
+            const uint32_t y1 = __umul24((uint32_t)f.y1 >> 1, sy) + ((uint32_t)f.y1 & 1u) * 16u + bx;
+            i00 = z0 + y0; i10 = z0 + y1; i01 = z1 + y0; i11 = z1 + y1;
+        } else {
+            const uint32_t sy = (uint32_t)P.sy;  // a slice is < 2^32 floats
+            const uint32_t y0 = ((uint32_t)f.y0 >> 1) * sy + ((uint32_t)f.y0 & 1u) * 16u + bx;
+            const uint32_t y1 = ((uint32_t)f.y1 >> 1) * sy + ((uint32_t)f.y1 & 1u) * 16u + bx;
+            i00 = (uint64_t)f.z0 * P.sz + y0; i10 = (uint64_t)f.z0 * P.sz + y1;
+            i01 = (uint64_t)f.z1 * P.sz + y0; i11 = (uint64_t)f.z1 * P.sz + y1;
         }
+        const vr_f2a4 a = load_pair64(vol, i00), b = load_pair64(vol, i10);
+        const vr_f2a4 c = load_pair64(vol, i01), d = load_pair64(vol, i11);
+        rec[0][0] = a.x;
+        rec[1][0] = ox ? a.y : a.x;
+        rec[2][0] = b.x;
+        rec[3][0] = ox ? b.y : b.x;
+        rec[4][0] = c.x;
+        rec[5][0] = ox ? c.y : c.x;
+        rec[6][0] = d.x;
+        rec[7][0] = ox ? d.y : d.x;
+        return;
     }
     const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
     const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
@@ -215,6 +206,10 @@ __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Par
     load_rec<B>(vol, r11 + f.x0, rec[6]);
     load_rec<B>(vol, r11 + f.x1, rec[7]);
 }
+
+// gather8's MODE for statistic template M (0 / -1: a baked plane)
+template <int M>
+constexpr int kGatherMode = M == 0 ? 1 : (M == -1 ? 2 : 0);
 
 template <int B, int M>
 __device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][B],
@@ -255,7 +250,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
     bool alive = true;
     Foot fa = footprint(P, px, py, pz), fb;
     float ra[8][B], rb[8][B];
-    gather8<B, M == 0>(vol, P, fa, ra);
+    gather8<B, kGatherMode<M>>(vol, P, fa, ra);
     // one step: decode (fc, rc) while the gathers of the next step go to (fn, rn)
     auto step = [&](int i, const Foot &fc, const float (&rc)[8][B], Foot &fn,
                     float (&rn)[8][B]) {
@@ -271,7 +266,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
         // footprint instead -- cache hits -- measured 2.4 ms against 1.36:
         // the select changed the schedule again.)
         fn = footprint(P, nx, ny, nz);
-        gather8<B, M == 0>(vol, P, fn, rn);
+        gather8<B, kGatherMode<M>>(vol, P, fn, rn);
         const float sample = decode8<B, M>(P, rc, fc);
         n = i + 1;
         if (composite(P, sample, sx, sy, sz, sw) || !cont) {

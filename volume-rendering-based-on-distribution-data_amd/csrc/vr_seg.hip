@@ -123,7 +123,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
             if (valid) {
                 const Foot f = footprint(P, px, py, pz);
                 float rec[8][B];
-                gather8<B, M == 0>(vol, P, f, rec);
+                gather8<B, kGatherMode<M>>(vol, P, f, rec);
                 smp = decode8<B, M>(P, rec, f);
             }
             const uint64_t vm = __ballot(valid);
@@ -138,7 +138,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
         bool va = geom((int)k, t), vb = false;
         if (va) {
             fa = footprint(P, px, py, pz);
-            gather8<B, M == 0>(vol, P, fa, ra);
+            gather8<B, kGatherMode<M>>(vol, P, fa, ra);
         }
         // one window: gather the next into (fn, rn, vn) while (fc, rc, vc) decodes
         auto window = [&](const Foot &fc, const float (&rc)[8][B], bool vc, Foot &fn,
@@ -148,7 +148,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
             vn = alive && geom(base + S + (int)k, tn);
             if (vn) {
                 fn = footprint(P, nx, ny, nz);
-                gather8<B, M == 0>(vol, P, fn, rn);
+                gather8<B, kGatherMode<M>>(vol, P, fn, rn);
             }
             float smp = 0.0f;
             if (vc && alive) smp = decode8<B, M>(P, rc, fc);

@@ -8,13 +8,23 @@
 // 8 corners with the same filter gives the same float for every sample, bit
 // for bit.  A baked frame reads 4 bytes per corner voxel instead of B * 4
 // (raw records) or a codebook entry + errors (codec), so the march is no
-// longer bound by the distribution bytes.  Planes use the volume's pitches:
-// plane k < 3 of the raw volume holds statistic k+1 at record index
-// z * slice_pitch + y * row_pitch + x, plane 3 method 7's corner mean (the
-// codec volume: 3 planes, dense voxel order).
+// longer bound by the distribution bytes.  Planes are laid out in 16 x 2 x 1
+// bricks with a one-voxel x apron (plane_index, vr_device.h): plane k < 3 of
+// the raw volume holds statistic k+1 of voxel (x, y, z), plane 3 method 7's
+// corner mean (the codec volume: 3 planes).
+
 #include "vr_internal.h"
 
 namespace vr {
+
+// a voxel's statistic at its home position and, for x = 15 k (k > 0), in the
+// apron (offset 15) of brick k - 1
+__device__ __forceinline__ void put_plane(float *__restrict__ out, uint32_t x, uint32_t y,
+                                          uint32_t z, uint64_t psy, uint64_t psz, float v) {
+    const uint64_t h = plane_index(x, y, z, psy, psz);
+    out[h] = v;
+    if (x > 0 && plane_bx(x) % 32u == 0) out[h - 32u + kPlaneStride] = v;
+}
 
 // One thread per voxel of an x-row (grid: x blocks of 256, y rows, z slices);
 // each record is read once, coalesced, and its statistics written to the four
@@ -24,7 +34,8 @@ namespace vr {
 // exact, vr_selftest_logf).
 template <int B>
 __global__ __launch_bounds__(256) void k_bake_raw(const float *__restrict__ vol, Params P,
-                                                  float *__restrict__ out, uint64_t plane) {
+                                                  float *__restrict__ out, uint64_t plane,
+                                                  uint64_t psy, uint64_t psz) {
     __shared__ LogEnt tab[65];
     copy_logtab(tab);
     __syncthreads();
@@ -46,24 +57,26 @@ __global__ __launch_bounds__(256) void k_bake_raw(const float *__restrict__ vol,
         e = record_stat_rt<3>(p, P.nb, P.enorm);
         c = raw_mean_rt(p, P.nb);
     }
-    out[off] = m;
-    out[plane + off] = v;
-    out[2 * plane + off] = e;
-    out[3 * plane + off] = c;  // method 7's corner mean (K:347-367), before the / 0.0217
+    const uint32_t y = blockIdx.y, z = blockIdx.z;
+    put_plane(out, x, y, z, psy, psz, m);
+    put_plane(out + plane, x, y, z, psy, psz, v);
+    put_plane(out + 2 * plane, x, y, z, psy, psz, e);
+    put_plane(out + 3 * plane, x, y, z, psy, psz, c);  // method 7's corner mean (K:347-367), before the / 0.0217
 }
 
 // codec voxels (methods 4/5/6, K:775-871): decode once, statistics C = 0, 1, 2
 template <int B>
 __global__ __launch_bounds__(256) void k_bake_codec(Params P, float *__restrict__ out,
-                                                    uint64_t plane) {
+                                                    uint64_t plane, uint64_t psy, uint64_t psz) {
     const uint32_t x = blockIdx.x * 256u + threadIdx.x;
     if (x >= (uint32_t)P.nx) return;
     const uint64_t off = (uint64_t)blockIdx.z * P.sz + (uint64_t)blockIdx.y * P.sy + x;
     float dec[B];
     codec_decode<B>(P, off, dec);
-    out[off] = codec_stat_of<B, 0>(dec, P.enorm);
-    out[plane + off] = codec_stat_of<B, 1>(dec, P.enorm);
-    out[2 * plane + off] = codec_stat_of<B, 2>(dec, P.enorm);
+    const uint32_t y = blockIdx.y, z = blockIdx.z;
+    put_plane(out, x, y, z, psy, psz, codec_stat_of<B, 0>(dec, P.enorm));
+    put_plane(out + plane, x, y, z, psy, psz, codec_stat_of<B, 1>(dec, P.enorm));
+    put_plane(out + 2 * plane, x, y, z, psy, psz, codec_stat_of<B, 2>(dec, P.enorm));
 }
 
 static bool bake_grid(const Params &P, dim3 &grid) {
@@ -73,33 +86,34 @@ static bool bake_grid(const Params &P, dim3 &grid) {
 }
 
 hipError_t launch_bake_raw(const float *vol, const Params &P, float *out, uint64_t plane,
-                           hipStream_t s) {
+                           uint64_t psy, uint64_t psz, hipStream_t s) {
     dim3 grid;
     if (!bake_grid(P, grid)) return hipErrorInvalidValue;
     const dim3 block(256);
     switch (P.nb) {
-    case 1: hipLaunchKernelGGL((k_bake_raw<1>), grid, block, 0, s, vol, P, out, plane); break;
-    case 2: hipLaunchKernelGGL((k_bake_raw<2>), grid, block, 0, s, vol, P, out, plane); break;
-    case 4: hipLaunchKernelGGL((k_bake_raw<4>), grid, block, 0, s, vol, P, out, plane); break;
-    case 8: hipLaunchKernelGGL((k_bake_raw<8>), grid, block, 0, s, vol, P, out, plane); break;
-    case 16: hipLaunchKernelGGL((k_bake_raw<16>), grid, block, 0, s, vol, P, out, plane); break;
-    case 32: hipLaunchKernelGGL((k_bake_raw<32>), grid, block, 0, s, vol, P, out, plane); break;
-    default: hipLaunchKernelGGL((k_bake_raw<0>), grid, block, 0, s, vol, P, out, plane); break;
+    case 1: hipLaunchKernelGGL((k_bake_raw<1>), grid, block, 0, s, vol, P, out, plane, psy, psz); break;
+    case 2: hipLaunchKernelGGL((k_bake_raw<2>), grid, block, 0, s, vol, P, out, plane, psy, psz); break;
+    case 4: hipLaunchKernelGGL((k_bake_raw<4>), grid, block, 0, s, vol, P, out, plane, psy, psz); break;
+    case 8: hipLaunchKernelGGL((k_bake_raw<8>), grid, block, 0, s, vol, P, out, plane, psy, psz); break;
+    case 16: hipLaunchKernelGGL((k_bake_raw<16>), grid, block, 0, s, vol, P, out, plane, psy, psz); break;
+    case 32: hipLaunchKernelGGL((k_bake_raw<32>), grid, block, 0, s, vol, P, out, plane, psy, psz); break;
+    default: hipLaunchKernelGGL((k_bake_raw<0>), grid, block, 0, s, vol, P, out, plane, psy, psz); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, hipStream_t s) {
+hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, uint64_t psy,
+                             uint64_t psz, hipStream_t s) {
     dim3 grid;
     if (!bake_grid(P, grid)) return hipErrorInvalidValue;
     const dim3 block(256);
     switch (P.nb) {
-    case 1: hipLaunchKernelGGL((k_bake_codec<1>), grid, block, 0, s, P, out, plane); break;
-    case 2: hipLaunchKernelGGL((k_bake_codec<2>), grid, block, 0, s, P, out, plane); break;
-    case 4: hipLaunchKernelGGL((k_bake_codec<4>), grid, block, 0, s, P, out, plane); break;
-    case 8: hipLaunchKernelGGL((k_bake_codec<8>), grid, block, 0, s, P, out, plane); break;
-    case 16: hipLaunchKernelGGL((k_bake_codec<16>), grid, block, 0, s, P, out, plane); break;
-    case 32: hipLaunchKernelGGL((k_bake_codec<32>), grid, block, 0, s, P, out, plane); break;
+    case 1: hipLaunchKernelGGL((k_bake_codec<1>), grid, block, 0, s, P, out, plane, psy, psz); break;
+    case 2: hipLaunchKernelGGL((k_bake_codec<2>), grid, block, 0, s, P, out, plane, psy, psz); break;
+    case 4: hipLaunchKernelGGL((k_bake_codec<4>), grid, block, 0, s, P, out, plane, psy, psz); break;
+    case 8: hipLaunchKernelGGL((k_bake_codec<8>), grid, block, 0, s, P, out, plane, psy, psz); break;
+    case 16: hipLaunchKernelGGL((k_bake_codec<16>), grid, block, 0, s, P, out, plane, psy, psz); break;
+    case 32: hipLaunchKernelGGL((k_bake_codec<32>), grid, block, 0, s, P, out, plane, psy, psz); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
