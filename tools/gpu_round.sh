@@ -31,6 +31,13 @@ for CTRS in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
   timeout -k 10 300 rocprofv3 --pmc $CTRS --output-format csv -d $O/pmc_C0_baked/p$i -o p$i -- python bench.py --baked --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc_C0_baked_p$i.log 2>&1; guard $? pmc-baked-$i
 done
 python tools/pmc_traffic.py $O/traffic.json "1024x8|C0|m1|baked" $O/pmc_C0_baked_p1.log $O/pmc_C0_baked/p1 $O/pmc_C0_baked/p2 $O/pmc_C0_baked/p3 || exit 1
+timeout -k 10 300 python -u bench.py --baked --camera C1 --no-cpu-baseline > $O/bench_1024x8_C1_baked.log 2>&1; guard $? bench-baked-C1
+i=0
+for CTRS in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $CTRS --output-format csv -d $O/pmc_C1_baked/p$i -o p$i -- python bench.py --baked --camera C1 --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc_C1_baked_p$i.log 2>&1; guard $? pmc-baked-C1-$i
+done
+python tools/pmc_traffic.py $O/traffic.json "1024x8|C1|m1|baked" $O/pmc_C1_baked_p1.log $O/pmc_C1_baked/p1 $O/pmc_C1_baked/p2 $O/pmc_C1_baked/p3 || exit 1
 for CAM in C0 C1; do
   timeout -k 10 300 python -u tools/rank_sim.py --camera $CAM > $O/rank_sim_$CAM.log 2>&1; guard $? rank-sim-$CAM
 done
