@@ -33,6 +33,10 @@ CONFIGS = {
     "256x4": (256, 4, 512, 512),
     "512x8": (512, 8, 1920, 1080),
     "1024x8": (1024, 8, 1920, 1080),
+    # the reference's own records are 32-bin histograms (C:86-87): wide-record frames
+    "512x32": (512, 32, 1920, 1080),
+    "1024x16": (1024, 16, 1920, 1080),
+    "1024x32": (1024, 32, 1920, 1080),
 }
 # GMM volumes: name -> (volume edge, components, W, H)
 GMM_CONFIGS = {

@@ -70,6 +70,52 @@ def test_bin_counts(pkg, orc, gpu, nb):
         assert_parity(got, ref, f"nb={nb} m{method}")
 
 
+@pytest.mark.parametrize("wide", ["", "1", "2"])
+@pytest.mark.parametrize("nb", [16, 32])
+@pytest.mark.parametrize("cam", ["C0", "C1"])
+def test_wide_records_take_batched_march(pkg, orc, gpu, nb, cam, wide, monkeypatch):
+    """16 / 32 bins (the reference's record width), mean and variance: the quad-
+    cooperative march (k_march_wq; the lane-per-record k_march_wide for row-aligned
+    16-bin views; VR_WIDE=1 / 2 force either), full
+    frames and packed tile lists bit-identical to the oracle; VR_PATH=1 keeps the
+    LDS-box march; entropy stays on k_march"""
+    import torch
+    monkeypatch.setenv("VR_WIDE", wide)
+    kind = wide or ("1" if nb == 16 and cam == "C0" else "2")
+    want = "k_march_wide<" if kind == "1" else "k_march_wq<"
+    vol = orc.synth_volume(21, 18, 15, nb)
+    m = pkg.camera.single_test_inv_view() if cam == "C0" else pkg.camera.display_inv_view()
+    W, H = 88, 60
+    pkg.init_distribution(vol)
+    for method in (1, 2):
+        got = gpu_render(pkg, None, W, H, m, method, torch)
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+        assert_parity(got, ref, f"{nb} bins {cam} m{method}")
+        assert pkg.last_kernel().startswith(want), pkg.last_kernel()
+    # a rank's packed tile list (multi-GPU path) through the same kernel
+    lists = pkg.tiles.tile_lists(W, H, 3, m)
+    n_slots = lists.shape[1]
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    packed = torch.full((3, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    for r in range(3):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+        assert pkg.last_kernel().startswith(want), pkg.last_kernel()
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, 3, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    ref8 = orc.render(vol, orc.make_params(W, H, m, query_method=1), want_float=False,
+                      want_steps=False)[0]
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref8)
+    got = gpu_render(pkg, None, W, H, m, 3, torch)
+    assert pkg.last_kernel().startswith("k_march<"), pkg.last_kernel()
+    monkeypatch.setenv("VR_PATH", "1")
+    got = gpu_render(pkg, None, W, H, m, 1, torch)
+    assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=1))[:3],
+                  f"{nb} bins {cam} m1 box")
+    assert pkg.last_kernel().startswith("k_march<"), pkg.last_kernel()
+
+
 def test_reference_isabel_shape_via_reference_api(pkg, orc, gpu):
     """The reference's own shape: 50x50x10 blocks x 32 bins, initCuda + render_kernel at
     512x512 with the runSingleTest camera (C:1016-1067)."""
@@ -158,6 +204,24 @@ def test_row_aligned_coarse_volume_takes_box_march(pkg, orc, gpu, monkeypatch):
         ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
         assert_parity(got, ref, f"coarse rows m{method} {W}x{H}")
         assert pkg.last_kernel().startswith(kern), pkg.last_kernel()
+
+
+@pytest.mark.parametrize("nb", [16, 32])
+def test_wide_coarse_rows_take_box_march(pkg, orc, gpu, nb, monkeypatch):
+    """16 / 32 bins, >= 4 pixels per voxel: row-aligned full frames above the
+    segmented threshold stage the wave's footprint box (k_march), oblique ones keep
+    the quad-cooperative march; bit-identical"""
+    import torch
+    monkeypatch.setenv("VR_SEG_RAYS", "1000")
+    vol = orc.synth_volume(20, 18, 16, nb)
+    pkg.init_distribution(vol)
+    rows = pkg.camera.display_inv_view((0.0, 0.0), translation=(0.05, -0.1, 0.0))
+    for m, kern in ((rows, "k_march<"), (pkg.camera.display_inv_view(), "k_march_wq<")):
+        for method in (1, 2):
+            got = gpu_render(pkg, None, 96, 64, m, method, torch)
+            ref = orc.render(vol, orc.make_params(96, 64, m, query_method=method))[:3]
+            assert_parity(got, ref, f"coarse {nb} bins m{method}")
+            assert pkg.last_kernel().startswith(kern), pkg.last_kernel()
 
 
 def test_edge_images(pkg, orc, gpu):

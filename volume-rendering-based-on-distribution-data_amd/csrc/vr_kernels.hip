@@ -864,6 +864,105 @@ __global__ __launch_bounds__(256) void k_march_pair(const float *__restrict__ vo
                 sw * P.brightness);
 }
 
+// ---- wide records (B = 16, 32: the reference's own 32-bin histograms) ----
+// One lane per ray, as k_march_pipe, but a step's 8 corner records (1 KiB per
+// lane at B = 32) cannot sit in registers twice.  The corners go in batches of
+// CG = 64 / B records (64 VGPRs): while batch k decodes, batch k + 1 -- after a
+// step's last batch, the first batch of the next step's footprint, gathered
+// unconditionally like k_march_pipe's next step -- is in flight, so every wave
+// keeps loads outstanding through the f64 decode chains (32 dependent bins per
+// record at B = 32).  A 32-bin record is exactly one 128-B line, so every byte
+// a gather fetches is used.  Arithmetic and blend order are those of k_march's
+// direct path (record_stat per corner, blend8).
+__device__ __forceinline__ uint64_t corner_index(const Params &P, const Foot &f, int j) {
+    const uint64_t z = (j & 4) ? (uint64_t)f.z1 : (uint64_t)f.z0;
+    const uint64_t y = (j & 2) ? (uint64_t)f.y1 : (uint64_t)f.y0;
+    const uint64_t x = (j & 1) ? (uint64_t)f.x1 : (uint64_t)f.x0;
+    return z * P.sz + y * P.sy + x;
+}
+
+// one batch: gather corners jn .. jn + CG - 1 of fl into nxt, then decode cur
+template <int B, int M>
+__device__ __forceinline__ void wide_batch(const float *__restrict__ vol, const Params &P,
+                                           const Foot &fl, int jn, float (&nxt)[64 / B][B],
+                                           const float (&cur)[64 / B][B], float *sv,
+                                           const LogEnt *lt) {
+    constexpr int CG = 64 / B;
+#pragma unroll
+    for (int j = 0; j < CG; j++) load_rec<B>(vol, corner_index(P, fl, jn + j), nxt[j]);
+#pragma unroll
+    for (int j = 0; j < CG; j++) sv[j] = record_stat_p<B, M>(cur[j], P.enorm, lt);
+}
+
+template <int B, int M>
+__device__ __forceinline__ int march_wide_tile(const float *__restrict__ vol, const Params &P,
+                                               uint32_t slot, uint32_t tile, uint32_t tid,
+                                               const LogEnt *lt) {
+    constexpr int CG = 64 / B, NB = 8 / CG;
+    static_assert(NB % 2 == 0, "batches alternate between two register sets");
+    uint32_t lx, ly;
+    tile_pixel(tid, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    if (x >= P.W || y >= P.H) return -1;  // no cross-lane work in this kernel
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    if (!make_ray(P, x, y, r)) {
+        write_miss(P, o);
+        return -1;
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    Foot fc = footprint(P, px, py, pz);
+    float ra[CG][B], rb[CG][B];
+#pragma unroll
+    for (int j = 0; j < CG; j++) load_rec<B>(vol, corner_index(P, fc, j), ra[j]);
+    for (int i = 0; i < kMaxSteps; i++) {
+        const float tn = t + kTStep;                               // K:701
+        const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, K:381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;   // K:706
+        const Foot fn = footprint(P, nx, ny, nz);
+        float sv[8];
+#pragma unroll
+        for (int k = 0; k < NB; k += 2) {
+            wide_batch<B, M>(vol, P, fc, (k + 1) * CG, rb, ra, sv + k * CG, lt);
+            const Foot &fl = k + 2 < NB ? fc : fn;
+            wide_batch<B, M>(vol, P, fl, ((k + 2) % NB) * CG, ra, rb, sv + (k + 1) * CG, lt);
+        }
+        const float sample = blend8(sv, fc);
+        n = i + 1;
+        if (composite(P, sample, sx, sy, sz, sw) || !cont) break;
+        t = tn;
+        px = nx;
+        py = ny;
+        pz = nz;
+        fc = fn;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+    return n;
+}
+
+// At most VR_WIDE_WAVES waves per SIMD: the register budget that keeps a batch
+// of loads in flight through the decode (as k_march_pipe's cap; without it the
+// scheduler sinks the loads below the decode to save registers).
+#ifndef VR_WIDE_WAVES
+#define VR_WIDE_WAVES 2
+#endif
+template <int B, int M>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_wide(const float *__restrict__ vol, Params P) {
+    static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    const int n = march_wide_tile<B, M>(vol, P, slot, tile, threadIdx.x, nullptr);
+    if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
+}
+
 // ---- half-step pipelined per-ray march (B <= 8) ----
 // k_march_pipe keeps a whole step of corner records in flight while the
 // previous step decodes (2 x 8 records per lane: 238 VGPRs at B = 8, two
@@ -996,6 +1095,197 @@ __device__ __forceinline__ FootPacked pack_foot(const Foot &f, bool live) {
            ((live ? 1 : 0) << 19);
     p.w2 = (int)(f.ax * 256.0f) | ((int)(f.ay * 256.0f) << 9) | ((int)(f.az * 256.0f) << 18);
     return p;
+}
+
+// ---- wide records, quad-cooperative gathers (B = 16, 32) ----
+// k_march_wide is bound by the texture-address path (PMC TA_BUSY 95-100 % at
+// 1024^3 x 32, C0): each 16-byte wave-instruction of a lane-owned 128-B record
+// touches 64 lines.  Here the 4 lanes of a quad (4 neighbouring rays) load
+// each other's records together: for corner j and quad ray R, lane g reads
+// chunk 4s + g of R's record (s = 0 .. B/16 - 1), so every 4-lane group of an
+// instruction is one contiguous 64-byte run, 16 runs per instruction.  A 4x4
+// transpose over (ray, lane) with quad_perm DPP (two butterfly stages, the
+// xor-2 and xor-1 exchanges) then leaves each lane with its own ray's whole
+// record, which it decodes exactly as k_march_wide does.  The loop is
+// wave-uniform (the quads exchange data every step); corner batches are
+// double-buffered as in k_march_wide.
+template <int D>
+__device__ __forceinline__ void quad_xchg(float4 &a, float4 &b, bool up) {
+    // butterfly over bit D of (register, lane): the lower lane keeps a and
+    // receives its partner's a into b; the upper lane keeps b, receives into a
+    // (selects on values, never on references: a select of two array
+    // addresses keeps the arrays out of registers)
+    constexpr int X = D == 1 ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+    const float a0 = a.x, a1 = a.y, a2 = a.z, a3 = a.w;
+    const float b0 = b.x, b1 = b.y, b2 = b.z, b3 = b.w;
+    const float u0 = qperm<X>(up ? a0 : b0), u1 = qperm<X>(up ? a1 : b1);
+    const float u2 = qperm<X>(up ? a2 : b2), u3 = qperm<X>(up ? a3 : b3);
+    a = make_float4(up ? u0 : a0, up ? u1 : a1, up ? u2 : a2, up ? u3 : a3);
+    b = make_float4(up ? b0 : u0, up ? b1 : u1, up ? b2 : u2, up ? b3 : u3);
+}
+// M[R] in lane g = chunk g of ray R's record  ->  M[c] in lane g = chunk c of ray g's record
+__device__ __forceinline__ void quad_transpose(float4 (&M)[4], uint32_t g) {
+    quad_xchg<2>(M[0], M[2], (g & 2u) != 0);
+    quad_xchg<2>(M[1], M[3], (g & 2u) != 0);
+    quad_xchg<1>(M[0], M[1], (g & 1u) != 0);
+    quad_xchg<1>(M[2], M[3], (g & 1u) != 0);
+}
+
+// the 4 rays' packed footprints of a quad (pack_foot: x0 | y0 << 16, z0 | dx << 16 |
+// dy << 17 | dz << 18 | live << 19)
+struct QuadFeet {
+    int w0[4], w1[4];
+};
+__device__ __forceinline__ QuadFeet quad_feet(const Foot &f, bool live) {
+    const FootPacked p = pack_foot(f, live);
+    QuadFeet q;
+    q.w0[0] = bcast_g<0>(p.w0); q.w1[0] = bcast_g<0>(p.w1);
+    q.w0[1] = bcast_g<1>(p.w0); q.w1[1] = bcast_g<1>(p.w1);
+    q.w0[2] = bcast_g<2>(p.w0); q.w1[2] = bcast_g<2>(p.w1);
+    q.w0[3] = bcast_g<3>(p.w0); q.w1[3] = bcast_g<3>(p.w1);
+    return q;
+}
+
+// Gather corner j of the quad's 4 rays (lane g: chunks 4s + g) into M[s][R];
+// rays not live skip their loads.
+template <int B>
+__device__ __forceinline__ void wq_gather(const float *__restrict__ vol, const Params &P,
+                                          const QuadFeet &q, int j, uint32_t g,
+                                          float4 (&M)[B / 16][4]) {
+#pragma unroll
+    for (int R = 0; R < 4; R++) {
+        const uint32_t w0 = (uint32_t)q.w0[R], w1 = (uint32_t)q.w1[R];
+        if ((w1 >> 19) & 1u) {
+            const uint64_t x = (w0 & 0xFFFFu) + ((j & 1) ? ((w1 >> 16) & 1u) : 0u);
+            const uint64_t y = (w0 >> 16) + ((j & 2) ? ((w1 >> 17) & 1u) : 0u);
+            const uint64_t z = (w1 & 0xFFFFu) + ((j & 4) ? ((w1 >> 18) & 1u) : 0u);
+            const float4 *rec =
+                reinterpret_cast<const float4 *>(vol + (z * P.sz + y * P.sy + x) * (uint64_t)B);
+#pragma unroll
+            for (int s = 0; s < B / 16; s++) M[s][R] = rec[4 * s + g];
+        }
+    }
+}
+
+// transpose a gathered corner and decode this lane's record
+template <int B, int M>
+__device__ __forceinline__ float wq_decode(float4 (&Mc)[B / 16][4], uint32_t g, bool alive,
+                                           float enorm) {
+#pragma unroll
+    for (int s = 0; s < B / 16; s++) quad_transpose(Mc[s], g);
+    float st = 0.0f;
+    if (alive) {
+        float p[B];
+#pragma unroll
+        for (int s = 0; s < B / 16; s++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                p[16 * s + 4 * c + 0] = Mc[s][c].x;
+                p[16 * s + 4 * c + 1] = Mc[s][c].y;
+                p[16 * s + 4 * c + 2] = Mc[s][c].z;
+                p[16 * s + 4 * c + 3] = Mc[s][c].w;
+            }
+        st = record_stat<B, M>(p, enorm);
+    }
+    return st;
+}
+
+// batches K (in A) and K + 1 (in Bf) of a step: batch K decodes while batch
+// K + 1 loads into Bf, then batch K + 1 decodes while the next batch -- of this
+// step or, after the step's last, the next step's first -- loads into A.
+// Compile-time K keeps every array index static (registers, no scratch).
+template <int B, int M, int K>
+__device__ __forceinline__ void wq_pair(const float *__restrict__ vol, const Params &P,
+                                        const QuadFeet &qc, const QuadFeet &qn, uint32_t g,
+                                        bool alive, float4 (&A)[64 / B][B / 16][4],
+                                        float4 (&Bf)[64 / B][B / 16][4], float (&sv)[8]) {
+    constexpr int CG = 64 / B, NB = 8 / CG;
+#pragma unroll
+    for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qc, (K + 1) * CG + c, g, Bf[c]);
+#pragma unroll
+    for (int c = 0; c < CG; c++) sv[K * CG + c] = wq_decode<B, M>(A[c], g, alive, P.enorm);
+    if constexpr (K + 2 < NB) {
+#pragma unroll
+        for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qc, (K + 2) * CG + c, g, A[c]);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qn, c, g, A[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < CG; c++) sv[(K + 1) * CG + c] = wq_decode<B, M>(Bf[c], g, alive, P.enorm);
+}
+
+template <int B, int M>
+__device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, const Params &P,
+                                             uint32_t slot, uint32_t tile, uint32_t tid) {
+    constexpr int S = B / 16;        // 16-byte chunks per lane per record
+    constexpr int CG = 64 / B;       // corners per batch (64 VGPRs)
+    constexpr int NB = 8 / CG;       // batches per step
+    static_assert(NB % 2 == 0, "batches alternate between two register sets");
+    uint32_t lx, ly;
+    tile_pixel(tid, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    const uint32_t g = tid & 3u;
+    // every lane stays to the end: the quads exchange records every step
+    Ray r = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    bool alive = valid && make_ray(P, x, y, r);
+    const bool hit = alive;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    Foot fc = footprint(P, px, py, pz);
+    QuadFeet qc = quad_feet(fc, alive);
+    float4 A[CG][S][4], Bf[CG][S][4];
+#pragma unroll
+    for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qc, c, g, A[c]);
+    for (int i = 0; i < kMaxSteps; i++) {
+        if (!wave_any(alive)) break;
+        const float tn = t + kTStep;                                        // K:701
+        const bool cont = alive && !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, K:381
+        const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
+        const Foot fn = footprint(P, nx, ny, nz);
+        const QuadFeet qn = quad_feet(fn, cont);
+        float sv[8];
+        wq_pair<B, M, 0>(vol, P, qc, qn, g, alive, A, Bf, sv);
+        if constexpr (NB == 4) wq_pair<B, M, 2>(vol, P, qc, qn, g, alive, A, Bf, sv);
+        if (alive) {
+            n = i + 1;
+            if (composite(P, blend8(sv, fc), sx, sy, sz, sw) || !cont) {
+                alive = false;
+            } else {
+                t = tn;
+                px = nx;
+                py = ny;
+                pz = nz;
+            }
+        }
+        fc = fn;
+        qc = qn;
+    }
+    if (!valid) return -1;
+    if (!hit) {
+        write_miss(P, o);
+        return -1;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+    return n;
+}
+
+template <int B, int M>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
+    static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    const int n = march_wq_tile<B, M>(vol, P, slot, tile, threadIdx.x);
+    if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
 }
 
 // Gather ray (G, q)'s four x-pairs: L[c] = chunk g of the pair at combo c =
@@ -2232,6 +2522,37 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             case 1: hipLaunchKernelGGL((k_march_pipe<B, 1>), grid, block, occupancy_lds(P), s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_pipe<B, 2>), grid, block, occupancy_lds(P), s, vol, P); break;
             case 3: hipLaunchKernelGGL((k_march_pipe<B, 3>), grid, block, occupancy_lds(P), s, vol, P); break;
+            }
+            return hipGetLastError();
+        }
+    }
+    if constexpr (!COUNT && (B == 16 || B == 32)) {
+        // wide records, mean / variance: the quad-cooperative march (k_march_wq),
+        // except row-aligned views of 16-bin records, whose lane-owned 64-B records
+        // already sit side by side (k_march_wide; 1024^3 x 16 C0 2.79 vs 3.90 ms;
+        // profiles/r02/wide_records.log).  VR_WIDE=1 / 2 forces one; VR_PATH=1 and
+        // coarse row-aligned full frames keep the LDS box (vr_api.cpp).  Entropy
+        // stays on k_march: unrolled over a batch its per-bin logarithms need more
+        // than 256 VGPRs (B = 16: 512 + spills).
+        if (P.path != 1 && (method == 1 || method == 2)) {
+            const size_t wl = occupancy_lds(P);
+            int kind = (B == 16 && !P.oblique) ? 1 : 2;
+            if (const char *ew = std::getenv("VR_WIDE")) {
+                const int v = std::atoi(ew);
+                if (v == 1 || v == 2) kind = v;
+            }
+            if (kind == 1) {
+                note_kernel("k_march_wide", B, method);
+                if (method == 1)
+                    hipLaunchKernelGGL((k_march_wide<B, 1>), grid, block, wl, s, vol, P);
+                else
+                    hipLaunchKernelGGL((k_march_wide<B, 2>), grid, block, wl, s, vol, P);
+            } else {
+                note_kernel("k_march_wq", B, method);
+                if (method == 1)
+                    hipLaunchKernelGGL((k_march_wq<B, 1>), grid, block, wl, s, vol, P);
+                else
+                    hipLaunchKernelGGL((k_march_wq<B, 2>), grid, block, wl, s, vol, P);
             }
             return hipGetLastError();
         }
