@@ -78,7 +78,7 @@ def test_wide_records_take_batched_march(pkg, orc, gpu, nb, cam, wide, monkeypat
     cooperative march (k_march_wq; the lane-per-record k_march_wide for row-aligned
     16-bin views; VR_WIDE=1 / 2 force either), full
     frames and packed tile lists bit-identical to the oracle; VR_PATH=1 keeps the
-    LDS-box march; entropy stays on k_march"""
+    LDS-box march; entropy always takes the quad march"""
     import torch
     monkeypatch.setenv("VR_WIDE", wide)
     kind = wide or ("1" if nb == 16 and cam == "C0" else "2")
@@ -108,7 +108,9 @@ def test_wide_records_take_batched_march(pkg, orc, gpu, nb, cam, wide, monkeypat
                       want_steps=False)[0]
     assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref8)
     got = gpu_render(pkg, None, W, H, m, 3, torch)
-    assert pkg.last_kernel().startswith("k_march<"), pkg.last_kernel()
+    assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=3))[:3],
+                  f"{nb} bins {cam} m3")
+    assert pkg.last_kernel().startswith("k_march_wq<"), pkg.last_kernel()
     monkeypatch.setenv("VR_PATH", "1")
     got = gpu_render(pkg, None, W, H, m, 1, torch)
     assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=1))[:3],

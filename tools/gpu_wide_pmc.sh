@@ -9,4 +9,4 @@ for CTRS in "TA_TA_BUSY_sum TA_BUSY_max GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD" \
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d gpurun_out/widepmc/p$i -o p$i -- python bench.py --config ${CFG:-1024x32} --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/widepmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/widepmc/p$i.log; exit 1; }
 done
-python tools/pmc_summary.py gpurun_out/widepmc k_march_wide 2>&1 | tail -30
+python tools/pmc_summary.py gpurun_out/widepmc ${KPAT:-k_march_w} 2>&1 | tail -30

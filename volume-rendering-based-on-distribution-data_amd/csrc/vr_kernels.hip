@@ -953,6 +953,7 @@ __device__ __forceinline__ int march_wide_tile(const float *__restrict__ vol, co
 #ifndef VR_WIDE_WAVES
 #define VR_WIDE_WAVES 2
 #endif
+constexpr bool WQ3 = true;  // entropy through the quad-cooperative wide march
 template <int B, int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_wide(const float *__restrict__ vol, Params P) {
     static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
@@ -1170,7 +1171,7 @@ __device__ __forceinline__ void wq_gather(const float *__restrict__ vol, const P
 // transpose a gathered corner and decode this lane's record
 template <int B, int M>
 __device__ __forceinline__ float wq_decode(float4 (&Mc)[B / 16][4], uint32_t g, bool alive,
-                                           float enorm) {
+                                           float enorm, const LogEnt *lt) {
 #pragma unroll
     for (int s = 0; s < B / 16; s++) quad_transpose(Mc[s], g);
     float st = 0.0f;
@@ -1185,7 +1186,7 @@ __device__ __forceinline__ float wq_decode(float4 (&Mc)[B / 16][4], uint32_t g, 
                 p[16 * s + 4 * c + 2] = Mc[s][c].z;
                 p[16 * s + 4 * c + 3] = Mc[s][c].w;
             }
-        st = record_stat<B, M>(p, enorm);
+        st = record_stat_p<B, M>(p, enorm, lt);
     }
     return st;
 }
@@ -1198,12 +1199,13 @@ template <int B, int M, int K>
 __device__ __forceinline__ void wq_pair(const float *__restrict__ vol, const Params &P,
                                         const QuadFeet &qc, const QuadFeet &qn, uint32_t g,
                                         bool alive, float4 (&A)[64 / B][B / 16][4],
-                                        float4 (&Bf)[64 / B][B / 16][4], float (&sv)[8]) {
+                                        float4 (&Bf)[64 / B][B / 16][4], float (&sv)[8],
+                                        const LogEnt *lt) {
     constexpr int CG = 64 / B, NB = 8 / CG;
 #pragma unroll
     for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qc, (K + 1) * CG + c, g, Bf[c]);
 #pragma unroll
-    for (int c = 0; c < CG; c++) sv[K * CG + c] = wq_decode<B, M>(A[c], g, alive, P.enorm);
+    for (int c = 0; c < CG; c++) sv[K * CG + c] = wq_decode<B, M>(A[c], g, alive, P.enorm, lt);
     if constexpr (K + 2 < NB) {
 #pragma unroll
         for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qc, (K + 2) * CG + c, g, A[c]);
@@ -1212,12 +1214,13 @@ __device__ __forceinline__ void wq_pair(const float *__restrict__ vol, const Par
         for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qn, c, g, A[c]);
     }
 #pragma unroll
-    for (int c = 0; c < CG; c++) sv[(K + 1) * CG + c] = wq_decode<B, M>(Bf[c], g, alive, P.enorm);
+    for (int c = 0; c < CG; c++) sv[(K + 1) * CG + c] = wq_decode<B, M>(Bf[c], g, alive, P.enorm, lt);
 }
 
 template <int B, int M>
 __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, const Params &P,
-                                             uint32_t slot, uint32_t tile, uint32_t tid) {
+                                             uint32_t slot, uint32_t tile, uint32_t tid,
+                                             const LogEnt *lt) {
     constexpr int S = B / 16;        // 16-byte chunks per lane per record
     constexpr int CG = 64 / B;       // corners per batch (64 VGPRs)
     constexpr int NB = 8 / CG;       // batches per step
@@ -1252,8 +1255,8 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
         const Foot fn = footprint(P, nx, ny, nz);
         const QuadFeet qn = quad_feet(fn, cont);
         float sv[8];
-        wq_pair<B, M, 0>(vol, P, qc, qn, g, alive, A, Bf, sv);
-        if constexpr (NB == 4) wq_pair<B, M, 2>(vol, P, qc, qn, g, alive, A, Bf, sv);
+        wq_pair<B, M, 0>(vol, P, qc, qn, g, alive, A, Bf, sv, lt);
+        if constexpr (NB == 4) wq_pair<B, M, 2>(vol, P, qc, qn, g, alive, A, Bf, sv, lt);
         if (alive) {
             n = i + 1;
             if (composite(P, blend8(sv, fc), sx, sy, sz, sw) || !cont) {
@@ -1280,11 +1283,15 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
 
 template <int B, int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
-    static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
+    __shared__ LogEnt s_lt[M == 3 ? 65 : 1];  // entropy: the exact-log table (copy_logtab)
+    if constexpr (M == 3) {
+        copy_logtab(s_lt);
+        __syncthreads();
+    }
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
-    const int n = march_wq_tile<B, M>(vol, P, slot, tile, threadIdx.x);
+    const int n = march_wq_tile<B, M>(vol, P, slot, tile, threadIdx.x, s_lt);
     if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
 }
 
@@ -2534,13 +2541,14 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         // coarse row-aligned full frames keep the LDS box (vr_api.cpp).  Entropy
         // stays on k_march: unrolled over a batch its per-bin logarithms need more
         // than 256 VGPRs (B = 16: 512 + spills).
-        if (P.path != 1 && (method == 1 || method == 2)) {
+        if (P.path != 1 && (method == 1 || method == 2 || (method == 3 && WQ3))) {
             const size_t wl = occupancy_lds(P);
-            int kind = (B == 16 && !P.oblique) ? 1 : 2;
+            int kind = (B == 16 && !P.oblique && method != 3) ? 1 : 2;
             if (const char *ew = std::getenv("VR_WIDE")) {
                 const int v = std::atoi(ew);
                 if (v == 1 || v == 2) kind = v;
             }
+            if (method == 3) kind = 2;  // k_march_wide: mean and variance only
             if (kind == 1) {
                 note_kernel("k_march_wide", B, method);
                 if (method == 1)
@@ -2551,8 +2559,10 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
                 note_kernel("k_march_wq", B, method);
                 if (method == 1)
                     hipLaunchKernelGGL((k_march_wq<B, 1>), grid, block, wl, s, vol, P);
-                else
+                else if (method == 2)
                     hipLaunchKernelGGL((k_march_wq<B, 2>), grid, block, wl, s, vol, P);
+                else if constexpr (WQ3)
+                    hipLaunchKernelGGL((k_march_wq<B, 3>), grid, block, wl, s, vol, P);
             }
             return hipGetLastError();
         }
