@@ -231,31 +231,50 @@ __device__ __forceinline__ float bin_width(int nb) {
 // (tests/test_oracle.py::test_bin_centres_fit_29_bits); the double product
 // (double)p * c_i of a 24-bit float is then exact, and
 // (double)mean + p * c_i rounded once is exactly fma(p, c_i, mean): one f64
-// op per bin fewer, bit-identical.  B = 32 centres reach 30 bits: mul + add.
+// op per bin fewer, bit-identical.  B = 32: 23 of the 32 centres fit 29 bits
+// and take the fused form, bins 23-31 (30 bits) keep mul + add; the choice is
+// made per bin at compile time (centre_bits evaluates the same float / double
+// expressions as the loop below).
+constexpr int centre_bits(int nb, int i) {
+    const float maxh = (float)0.0217;
+    const float bw = (maxh - 0.0f) / (float)nb;          // bin_width
+    double c = (double)(bw * (float)i) + (double)bw / 2.0;
+    while (c < 4503599627370496.0) c *= 2.0;            // scale into [2^52, 2^53): exact
+    while (c >= 9007199254740992.0) c *= 0.5;
+    unsigned long long m = (unsigned long long)c;
+    int b = 53;
+    while ((m & 1ull) == 0ull) {
+        m >>= 1;
+        b--;
+    }
+    return b;
+}
+
+template <int B, int I>
+__device__ __forceinline__ void mean_bins(const float (&p)[B], float bw, double half, float &mean) {
+    if constexpr (I < B) {
+        const double c = (double)(bw * (float)I) + half;
+#ifndef VR_NO_FMA_MEAN  // A/B builds only
+        constexpr bool fused = centre_bits(B, I) <= 29;
+#else
+        constexpr bool fused = false;
+#endif
+        if constexpr (fused) mean = (float)__builtin_fma((double)p[I], c, (double)mean);
+        else mean = (float)((double)mean + (double)p[I] * c);
+        mean_bins<B, I + 1>(p, bw, half, mean);
+    }
+}
+
 template <int B>
 __device__ __forceinline__ float raw_mean(const float (&p)[B]) {
     const float bw = bin_width(B);
     const double half = (double)bw / 2.0;
     float mean = 0.0f;
-#ifndef VR_NO_FMA_MEAN  // A/B builds only
-    if constexpr (B <= 16) {
-#else
-    if constexpr (false) {
-#endif
-#pragma unroll
-        for (int i = 0; i < B; i++) {
-            const double c = (double)(bw * (float)i) + half;
-            mean = (float)__builtin_fma((double)p[i], c, (double)mean);
-        }
-        return mean;
-    }
-#pragma unroll
-    for (int i = 0; i < B; i++) {
-        const double c = (double)(bw * (float)i) + half;
-        mean = (float)((double)mean + (double)p[i] * c);
-    }
+    mean_bins<B, 0>(p, bw, half, mean);
     return mean;
 }
+static_assert(centre_bits(16, 15) == 29 && centre_bits(32, 22) == 29 && centre_bits(32, 23) == 30,
+              "bin-centre widths (tests/test_oracle.py::test_bin_centres_fit_29_bits)");
 
 // K:749-755 (float arithmetic)
 template <int B>
