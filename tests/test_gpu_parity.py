@@ -111,6 +111,13 @@ def test_wide_records_take_batched_march(pkg, orc, gpu, nb, cam, wide, monkeypat
     assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=3))[:3],
                   f"{nb} bins {cam} m3")
     assert pkg.last_kernel().startswith("k_march_wq<"), pkg.last_kernel()
+    # method 7: quad-cooperative corner refreshes, method-7 grid = volume or not
+    for grid in ((21, 18, 15), (10, 12, 20)):
+        got = gpu_render(pkg, None, W, H, m, 7, torch, m7=grid)
+        assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=7,
+                                                           m7_dims=grid))[:3],
+                      f"{nb} bins {cam} m7 grid {grid}")
+        assert pkg.last_kernel().startswith("k_march_m7wq<"), pkg.last_kernel()
     monkeypatch.setenv("VR_PATH", "1")
     got = gpu_render(pkg, None, W, H, m, 1, torch)
     assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=1))[:3],

@@ -2281,6 +2281,176 @@ __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol,
                 sw * P.brightness);
 }
 
+// ---- method 7 for wide records (B = 16, 32), quad-cooperative refreshes ----
+// k_march_m7's refresh gathers 8 lane-owned records (texture-address-bound at
+// B = 32, as k_march_wide).  Here a refresh loads the 8 corner records of the
+// quad rays that need one with the quad gathers and DPP transpose of
+// k_march_wq (corner batches of 64 / B records double-buffered), then each
+// lane decodes its own corners' means (K:347-367).  The loop is wave-uniform;
+// cell test, lerps and composite are k_march_m7's.
+struct QuadCell {
+    int x[4], y[4], z[4], nd[4];  // per quad ray: floor | ceil << 16 per axis; refresh flag
+};
+
+template <int B>
+__device__ __forceinline__ void m7q_gather(const float *__restrict__ vol, const Params &P,
+                                           const QuadCell &q, int j, uint32_t g,
+                                           float4 (&M)[B / 16][4]) {
+#pragma unroll
+    for (int R = 0; R < 4; R++) {
+        if (q.nd[R]) {
+            const uint32_t ax = (uint32_t)q.x[R], ay = (uint32_t)q.y[R], az = (uint32_t)q.z[R];
+            const uint64_t x = (j & 1) ? (ax >> 16) : (ax & 0xFFFFu);
+            const uint64_t y = (j & 2) ? (ay >> 16) : (ay & 0xFFFFu);
+            const uint64_t z = (j & 4) ? (az >> 16) : (az & 0xFFFFu);
+            const float4 *rec =
+                reinterpret_cast<const float4 *>(vol + (z * P.sz + y * P.sy + x) * (uint64_t)B);
+#pragma unroll
+            for (int s = 0; s < B / 16; s++) M[s][R] = rec[4 * s + g];
+        }
+    }
+}
+
+// transpose a gathered corner and return this lane's record's undivided mean
+template <int B>
+__device__ __forceinline__ float m7q_decode(float4 (&Mc)[B / 16][4], uint32_t g, bool need) {
+#pragma unroll
+    for (int s = 0; s < B / 16; s++) quad_transpose(Mc[s], g);
+    float mean = 0.0f;
+    if (need) {
+        float p[B];
+#pragma unroll
+        for (int s = 0; s < B / 16; s++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                p[16 * s + 4 * c + 0] = Mc[s][c].x;
+                p[16 * s + 4 * c + 1] = Mc[s][c].y;
+                p[16 * s + 4 * c + 2] = Mc[s][c].z;
+                p[16 * s + 4 * c + 3] = Mc[s][c].w;
+            }
+        mean = raw_mean<B>(p);
+    }
+    return mean;
+}
+
+// corner batches K (in A) and K + 1 (in Bf) of one refresh; the batch after
+// K + 1 (if any) is gathered into A while K + 1 decodes
+template <int B, int K>
+__device__ __forceinline__ void m7q_pair(const float *__restrict__ vol, const Params &P,
+                                         const QuadCell &q, uint32_t g, bool need,
+                                         float4 (&A)[64 / B][B / 16][4],
+                                         float4 (&Bf)[64 / B][B / 16][4], float (&mn)[8]) {
+    constexpr int CG = 64 / B, NB = 8 / CG;
+#pragma unroll
+    for (int c = 0; c < CG; c++) m7q_gather<B>(vol, P, q, (K + 1) * CG + c, g, Bf[c]);
+#pragma unroll
+    for (int c = 0; c < CG; c++) {
+        const float v = m7q_decode<B>(A[c], g, need);
+        if (need) mn[K * CG + c] = v;
+    }
+    if constexpr (K + 2 < NB) {
+#pragma unroll
+        for (int c = 0; c < CG; c++) m7q_gather<B>(vol, P, q, (K + 2) * CG + c, g, A[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < CG; c++) {
+        const float v = m7q_decode<B>(Bf[c], g, need);
+        if (need) mn[(K + 1) * CG + c] = v;
+    }
+}
+
+template <int B>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_m7wq(const float *__restrict__ vol, Params P) {
+    constexpr int CG = 64 / B, NB = 8 / CG;
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    uint32_t lx, ly;
+    tile_pixel(threadIdx.x, lx, ly);
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.W && y < P.H;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    const uint32_t g = threadIdx.x & 3u;
+    // every lane stays to the end: the quads exchange records at every refresh
+    Ray r = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    bool alive = valid && make_ray(P, x, y, r);
+    const bool hit = alive;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    M7 m = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}};
+    int n = 0;
+    for (int i = 0; i < kMaxSteps; i++) {
+        if (!wave_any(alive)) break;
+        const float qx = px * 0.5f + 0.5f, qy = py * 0.5f + 0.5f, qz = pz * 0.5f + 0.5f;
+        // the first sample fills the cache (K:320-367), later ones refresh on
+        // leaving the cell (inInterpolation, K:253-270, 396)
+        const bool need = alive && (i == 0 || qx < m.fx || qy < m.fy || qz < m.fz ||
+                                    qx > m.cx || qy > m.cy || qz > m.cz);
+        if (wave_any(need)) {
+            if (need) {  // m7_refresh's cell bounds
+                m.fx = floorf(qx * (float)P.m7x) / (float)P.m7x;
+                m.cx = ceilf(qx * (float)P.m7x) / (float)P.m7x;
+                m.fy = floorf(qy * (float)P.m7y) / (float)P.m7y;
+                m.cy = ceilf(qy * (float)P.m7y) / (float)P.m7y;
+                m.fz = floorf(qz * (float)P.m7z) / (float)P.m7z;
+                m.cz = ceilf(qz * (float)P.m7z) / (float)P.m7z;
+            }
+            // corner voxels (corner_mean's point_axis), broadcast over the quad
+            const int cx = point_axis(m.fx, P.nx) | (point_axis(m.cx, P.nx) << 16);
+            const int cy = point_axis(m.fy, P.ny) | (point_axis(m.cy, P.ny) << 16);
+            const int cz = point_axis(m.fz, P.nz) | (point_axis(m.cz, P.nz) << 16);
+            const int nd = need ? 1 : 0;
+            QuadCell q;
+            q.x[0] = bcast_g<0>(cx); q.y[0] = bcast_g<0>(cy); q.z[0] = bcast_g<0>(cz); q.nd[0] = bcast_g<0>(nd);
+            q.x[1] = bcast_g<1>(cx); q.y[1] = bcast_g<1>(cy); q.z[1] = bcast_g<1>(cz); q.nd[1] = bcast_g<1>(nd);
+            q.x[2] = bcast_g<2>(cx); q.y[2] = bcast_g<2>(cy); q.z[2] = bcast_g<2>(cz); q.nd[2] = bcast_g<2>(nd);
+            q.x[3] = bcast_g<3>(cx); q.y[3] = bcast_g<3>(cy); q.z[3] = bcast_g<3>(cz); q.nd[3] = bcast_g<3>(nd);
+            float4 A[CG][B / 16][4], Bf[CG][B / 16][4];
+#pragma unroll
+            for (int c = 0; c < CG; c++) m7q_gather<B>(vol, P, q, c, g, A[c]);
+            m7q_pair<B, 0>(vol, P, q, g, need, A, Bf, m.mean);
+            if constexpr (NB == 4) m7q_pair<B, 2>(vol, P, q, g, need, A, Bf, m.mean);
+        }
+        if (alive) {
+            const float xd = (px * 0.5f + 0.5f - m.fx) / (m.cx - m.fx);
+            const float yd = (py * 0.5f + 0.5f - m.fy) / (m.cy - m.fy);
+            const float zd = (pz * 0.5f + 0.5f - m.fz) / (m.cz - m.fz);
+            const float *mn = m.mean;
+            const float m00 = (float)((double)mn[0] * (1.0 - (double)xd) + (double)(mn[1] * xd));
+            const float m10 = (float)((double)mn[2] * (1.0 - (double)xd) + (double)(mn[3] * xd));
+            const float m01 = (float)((double)mn[4] * (1.0 - (double)xd) + (double)(mn[5] * xd));
+            const float m11 = (float)((double)mn[6] * (1.0 - (double)xd) + (double)(mn[7] * xd));
+            const float m0 = (float)((double)m00 * (1.0 - (double)yd) + (double)(m10 * yd));
+            const float m1 = (float)((double)m01 * (1.0 - (double)yd) + (double)(m11 * yd));
+            const float im = (float)((double)m0 * (1.0 - (double)zd) + (double)(m1 * zd));
+            n = i + 1;
+            if (composite(P, im * 50.0f, sx, sy, sz, sw)) {  // K:479
+                alive = false;
+            } else {
+                t = t + kTStep;
+                if (t > r.tfar) {
+                    alive = false;
+                } else {
+                    px = px + stx;
+                    py = py + sty;
+                    pz = pz + stz;
+                }
+            }
+        }
+    }
+    if (!valid) return;
+    if (!hit) {
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 // ---- synthetic volume ----
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -2618,6 +2788,15 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
                     note_kernel("k_march_m7_quad", B, method);
                     hipLaunchKernelGGL(k_march_m7_quad<false>, grid, block, qlds, s, vol, P);
                 }
+                break;
+            }
+        }
+        if constexpr (B == 16 || B == 32) {
+            // wide records: quad-cooperative refreshes (VR_M7_WQ=0: k_march_m7)
+            const char *eq = std::getenv("VR_M7_WQ");
+            if (!(eq && std::atoi(eq) == 0)) {
+                note_kernel("k_march_m7wq", B, method);
+                hipLaunchKernelGGL((k_march_m7wq<B>), grid, block, occupancy_lds(P), s, vol, P);
                 break;
             }
         }
