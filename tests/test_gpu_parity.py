@@ -118,6 +118,12 @@ def test_wide_records_take_batched_march(pkg, orc, gpu, nb, cam, wide, monkeypat
                                                            m7_dims=grid))[:3],
                       f"{nb} bins {cam} m7 grid {grid}")
         assert pkg.last_kernel().startswith("k_march_m7wq<"), pkg.last_kernel()
+    monkeypatch.setenv("VR_M7_WQ", "0")
+    got = gpu_render(pkg, None, W, H, m, 7, torch, m7=(21, 18, 15))
+    assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=7,
+                                                       m7_dims=(21, 18, 15)))[:3],
+                  f"{nb} bins {cam} m7 lane-owned")
+    assert pkg.last_kernel().startswith("k_march_m7<"), pkg.last_kernel()
     monkeypatch.setenv("VR_PATH", "1")
     got = gpu_render(pkg, None, W, H, m, 1, torch)
     assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=1))[:3],
