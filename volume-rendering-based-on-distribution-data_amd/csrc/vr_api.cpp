@@ -549,10 +549,14 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // pipelined march (512^3 x 8 C0 1080p: m1 1.00 -> 0.88 ms, m2 1.00 -> 0.73;
     // it loses for entropy, oblique views, 1024^3 and launches of <= 262 K
     // rays: profiles/r02/paths_coarse_rows.log).
-    // The same holds for 16- and 32-bin records (512^3 x 32 C0 1080p: box 3.83 ms,
-    // quad-cooperative 6.04; profiles/r02/wide_records.log).
+    // The same holds for 16- and 32-bin records, whose box rows load through the
+    // quad-cooperative gathers (512^3 x 32 C0 1080p m1: box 2.97 ms, quad march
+    // 6.04; profiles/r02/wide_records.log), entropy included: decoding each record
+    // once per wave is what the log-heavy wide decode needs (VR_BOX3=0: quad march).
+    const bool wide3 = (g.nb == 16 || g.nb == 32) && d->query_method == 3 &&
+                       !(std::getenv("VR_BOX3") && std::atoi(std::getenv("VR_BOX3")) == 0);
     if (along_rows && !d->d_tile_list && (g.nb == 8 || g.nb == 16 || g.nb == 32) &&
-        (d->query_method == 1 || d->query_method == 2) &&
+        (d->query_method == 1 || d->query_method == 2 || wide3) &&
         (uint64_t)d->width * d->height > seg_rays &&
         (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
         P.path = 1;

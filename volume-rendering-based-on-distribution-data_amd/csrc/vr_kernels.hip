@@ -35,6 +35,51 @@ void note_kernel(const char *kind, int B, int method) {
 
 const char *last_march_kernel() { return g_last_kernel; }
 
+// quad_perm DPP: lane g of each quad reads lane sel[g] of its quad
+template <int CTRL>
+__device__ __forceinline__ float qperm(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int qpermi(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+constexpr int kQ0 = 0x00, kQ1 = 0x55, kQ2 = 0xAA, kQ3 = 0xFF;  // broadcast lane 0/1/2/3
+constexpr int kQx1 = 0xB1;   // [1,0,3,2]
+constexpr int kQ0101 = 0x44; // [0,1,0,1]
+constexpr int kQ2323 = 0xEE; // [2,3,2,3]
+
+template <int G>
+__device__ __forceinline__ int bcast_g(int v) {
+    if constexpr (G == 0) return qpermi<kQ0>(v);
+    else if constexpr (G == 1) return qpermi<kQ1>(v);
+    else if constexpr (G == 2) return qpermi<kQ2>(v);
+    else return qpermi<kQ3>(v);
+}
+
+template <int D>
+__device__ __forceinline__ void quad_xchg(float4 &a, float4 &b, bool up) {
+    // butterfly over bit D of (register, lane): the lower lane keeps a and
+    // receives its partner's a into b; the upper lane keeps b, receives into a
+    // (selects on values, never on references: a select of two array
+    // addresses keeps the arrays out of registers)
+    constexpr int X = D == 1 ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+    const float a0 = a.x, a1 = a.y, a2 = a.z, a3 = a.w;
+    const float b0 = b.x, b1 = b.y, b2 = b.z, b3 = b.w;
+    const float u0 = qperm<X>(up ? a0 : b0), u1 = qperm<X>(up ? a1 : b1);
+    const float u2 = qperm<X>(up ? a2 : b2), u3 = qperm<X>(up ? a3 : b3);
+    a = make_float4(up ? u0 : a0, up ? u1 : a1, up ? u2 : a2, up ? u3 : a3);
+    b = make_float4(up ? b0 : u0, up ? b1 : u1, up ? b2 : u2, up ? b3 : u3);
+}
+// M[R] in lane g = chunk g of ray R's record  ->  M[c] in lane g = chunk c of ray g's record
+__device__ __forceinline__ void quad_transpose(float4 (&M)[4], uint32_t g) {
+    quad_xchg<2>(M[0], M[2], (g & 2u) != 0);
+    quad_xchg<2>(M[1], M[3], (g & 2u) != 0);
+    quad_xchg<1>(M[0], M[1], (g & 1u) != 0);
+    quad_xchg<1>(M[2], M[3], (g & 1u) != 0);
+}
+
+
 
 
 // Compile-time tuning knobs (tools/build_variants.sh builds sweeps of them).
@@ -117,7 +162,39 @@ __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, cons
             const int y = (int)(((float)r + 0.5f) * rdx);
             const int x = r - y * dx;
             const uint64_t off = (uint64_t)(uint32_t)z * P.sz + (uint32_t)(y * sy + x);
-            load_rec<B>(vbase, off, rec[g]);
+            if constexpr (B == 16 || B == 32) {
+                // wide records: the quad loads its 4 lanes' records as contiguous
+                // 64-B runs (lane q reads chunk 4s + q of each) and a DPP transpose
+                // hands every lane its own (k_march_wq); lane-owned 64 / 128-B
+                // records made every 16-B wave load touch ~64 lines
+                const uint32_t q = lane & 3u;
+                const uint32_t lo = (uint32_t)off, hi = (uint32_t)(off >> 32);
+                float4 Mq[B / 16][4];
+#pragma unroll
+                for (int R = 0; R < 4; R++) {
+                    const uint32_t l = (uint32_t)(R == 0 ? bcast_g<0>((int)lo) : R == 1 ? bcast_g<1>((int)lo)
+                                                : R == 2 ? bcast_g<2>((int)lo) : bcast_g<3>((int)lo));
+                    const uint32_t h = (uint32_t)(R == 0 ? bcast_g<0>((int)hi) : R == 1 ? bcast_g<1>((int)hi)
+                                                : R == 2 ? bcast_g<2>((int)hi) : bcast_g<3>((int)hi));
+                    const float4 *src = reinterpret_cast<const float4 *>(
+                        vbase + (((uint64_t)h << 32) | l) * (uint64_t)B);
+#pragma unroll
+                    for (int c = 0; c < B / 16; c++) Mq[c][R] = src[4 * c + q];
+                }
+#pragma unroll
+                for (int c = 0; c < B / 16; c++) {
+                    quad_transpose(Mq[c], q);
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        rec[g][16 * c + 4 * k + 0] = Mq[c][k].x;
+                        rec[g][16 * c + 4 * k + 1] = Mq[c][k].y;
+                        rec[g][16 * c + 4 * k + 2] = Mq[c][k].z;
+                        rec[g][16 * c + 4 * k + 3] = Mq[c][k].w;
+                    }
+                }
+            } else {
+                load_rec<B>(vbase, off, rec[g]);
+            }
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -1060,28 +1137,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_HALF_WAV
 // are issued group by group into the registers the current group has just
 // released (rolling prefetch).
 
-// quad_perm DPP: lane g of each quad reads lane sel[g] of its quad
-template <int CTRL>
-__device__ __forceinline__ float qperm(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int CTRL>
-__device__ __forceinline__ int qpermi(int v) {
-    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
-}
-constexpr int kQ0 = 0x00, kQ1 = 0x55, kQ2 = 0xAA, kQ3 = 0xFF;  // broadcast lane 0/1/2/3
-constexpr int kQx1 = 0xB1;   // [1,0,3,2]
-constexpr int kQ0101 = 0x44; // [0,1,0,1]
-constexpr int kQ2323 = 0xEE; // [2,3,2,3]
-
-template <int G>
-__device__ __forceinline__ int bcast_g(int v) {
-    if constexpr (G == 0) return qpermi<kQ0>(v);
-    else if constexpr (G == 1) return qpermi<kQ1>(v);
-    else if constexpr (G == 2) return qpermi<kQ2>(v);
-    else return qpermi<kQ3>(v);
-}
-
 // footprint packed for the quad broadcast:
 //   w0 = x0 | y0 << 16,  w1 = z0 | dx << 16 | dy << 17 | dz << 18 | live << 19,
 //   w2 = filter weights in 9-bit fixed point (exact: q8 gives k/256, k <= 256)
@@ -1110,28 +1165,6 @@ __device__ __forceinline__ FootPacked pack_foot(const Foot &f, bool live) {
 // record, which it decodes exactly as k_march_wide does.  The loop is
 // wave-uniform (the quads exchange data every step); corner batches are
 // double-buffered as in k_march_wide.
-template <int D>
-__device__ __forceinline__ void quad_xchg(float4 &a, float4 &b, bool up) {
-    // butterfly over bit D of (register, lane): the lower lane keeps a and
-    // receives its partner's a into b; the upper lane keeps b, receives into a
-    // (selects on values, never on references: a select of two array
-    // addresses keeps the arrays out of registers)
-    constexpr int X = D == 1 ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
-    const float a0 = a.x, a1 = a.y, a2 = a.z, a3 = a.w;
-    const float b0 = b.x, b1 = b.y, b2 = b.z, b3 = b.w;
-    const float u0 = qperm<X>(up ? a0 : b0), u1 = qperm<X>(up ? a1 : b1);
-    const float u2 = qperm<X>(up ? a2 : b2), u3 = qperm<X>(up ? a3 : b3);
-    a = make_float4(up ? u0 : a0, up ? u1 : a1, up ? u2 : a2, up ? u3 : a3);
-    b = make_float4(up ? b0 : u0, up ? b1 : u1, up ? b2 : u2, up ? b3 : u3);
-}
-// M[R] in lane g = chunk g of ray R's record  ->  M[c] in lane g = chunk c of ray g's record
-__device__ __forceinline__ void quad_transpose(float4 (&M)[4], uint32_t g) {
-    quad_xchg<2>(M[0], M[2], (g & 2u) != 0);
-    quad_xchg<2>(M[1], M[3], (g & 2u) != 0);
-    quad_xchg<1>(M[0], M[1], (g & 1u) != 0);
-    quad_xchg<1>(M[2], M[3], (g & 1u) != 0);
-}
-
 // the 4 rays' packed footprints of a quad (pack_foot: x0 | y0 << 16, z0 | dx << 16 |
 // dy << 17 | dz << 18 | live << 19)
 struct QuadFeet {
