@@ -224,15 +224,16 @@ def test_row_aligned_coarse_volume_takes_box_march(pkg, orc, gpu, monkeypatch):
 @pytest.mark.parametrize("nb", [16, 32])
 def test_wide_coarse_rows_take_box_march(pkg, orc, gpu, nb, monkeypatch):
     """16 / 32 bins, >= 4 pixels per voxel: row-aligned full frames above the
-    segmented threshold stage the wave's footprint box (k_march), oblique ones keep
-    the quad-cooperative march; bit-identical"""
+    segmented threshold stage the wave's footprint box (k_march, entropy included;
+    box rows loaded by the quad gathers), oblique ones keep the quad-cooperative
+    march; bit-identical"""
     import torch
     monkeypatch.setenv("VR_SEG_RAYS", "1000")
     vol = orc.synth_volume(20, 18, 16, nb)
     pkg.init_distribution(vol)
     rows = pkg.camera.display_inv_view((0.0, 0.0), translation=(0.05, -0.1, 0.0))
     for m, kern in ((rows, "k_march<"), (pkg.camera.display_inv_view(), "k_march_wq<")):
-        for method in (1, 2):
+        for method in (1, 2, 3):
             got = gpu_render(pkg, None, 96, 64, m, method, torch)
             ref = orc.render(vol, orc.make_params(96, 64, m, query_method=method))[:3]
             assert_parity(got, ref, f"coarse {nb} bins m{method}")
