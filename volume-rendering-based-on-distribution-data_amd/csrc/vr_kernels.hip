@@ -1030,9 +1030,12 @@ __device__ __forceinline__ int march_wide_tile(const float *__restrict__ vol, co
 #ifndef VR_WIDE_WAVES
 #define VR_WIDE_WAVES 2
 #endif
+#ifndef VR_WIDE_MINW
+#define VR_WIDE_MINW 1      // waves per SIMD the register allocation must allow
+#endif
 constexpr bool WQ3 = true;  // entropy through the quad-cooperative wide march
 template <int B, int M>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_wide(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, VR_WIDE_WAVES))) void k_march_wide(const float *__restrict__ vol, Params P) {
     static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
@@ -1315,7 +1318,7 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
 }
 
 template <int B, int M>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
     __shared__ LogEnt s_lt[M == 3 ? 65 : 1];  // entropy: the exact-log table (copy_logtab)
     if constexpr (M == 3) {
         copy_logtab(s_lt);
@@ -2393,7 +2396,7 @@ __device__ __forceinline__ void m7q_pair(const float *__restrict__ vol, const Pa
 }
 
 template <int B>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_WIDE_WAVES))) void k_march_m7wq(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, VR_WIDE_WAVES))) void k_march_m7wq(const float *__restrict__ vol, Params P) {
     constexpr int CG = 64 / B, NB = 8 / CG;
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
