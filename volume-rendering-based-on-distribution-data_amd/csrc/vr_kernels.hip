@@ -1262,7 +1262,12 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
     constexpr int NB = 8 / CG;       // batches per step
     static_assert(NB % 2 == 0, "batches alternate between two register sets");
     uint32_t lx, ly;
-    tile_pixel(tid, lx, ly);
+    if (P.wq_map) {  // oblique views: a wave takes a 16x4 block, a quad one pixel column
+        lx = (tid >> 6) * 16u + ((tid & 63u) >> 2);
+        ly = tid & 3u;
+    } else {
+        tile_pixel(tid, lx, ly);
+    }
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.W && y < P.H;
@@ -2755,6 +2760,11 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
                 if (v == 1 || v == 2) kind = v;
             }
             if (method == 3) kind = 2;  // k_march_wide: mean and variance only
+            // k_march_wq pixels: 16x4 blocks per wave (a quad = a pixel column) beat a
+            // 64-pixel row per wave: 1024^3 x 32 C1 12.44 -> 11.77 ms, C0 6.64 -> 6.56,
+            // 1024^3 x 16 C1 6.78 -> 6.65 (profiles/r02/wide_records.log); VR_WQ_MAP=0: rows
+            P.wq_map = 1;
+            if (const char *em = std::getenv("VR_WQ_MAP")) P.wq_map = std::atoi(em) != 0;
             if (kind == 1) {
                 note_kernel("k_march_wide", B, method);
                 if (method == 1)
