@@ -1034,6 +1034,9 @@ __device__ __forceinline__ int march_wide_tile(const float *__restrict__ vol, co
 #define VR_WIDE_MINW 1      // waves per SIMD the register allocation must allow
 #endif
 constexpr bool WQ3 = true;  // entropy through the quad-cooperative wide march
+#ifndef M7_WQ_MAP
+#define M7_WQ_MAP 1         // k_march_m7wq pixel map default (P.wq_map)
+#endif
 template <int B, int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, VR_WIDE_WAVES))) void k_march_wide(const float *__restrict__ vol, Params P) {
     static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
@@ -2407,7 +2410,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MIN
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
     uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
+    if (P.wq_map) {  // a wave takes a 16x4 block, a quad one pixel column (k_march_wq)
+        lx = (threadIdx.x >> 6) * 16u + ((threadIdx.x & 63u) >> 2);
+        ly = threadIdx.x & 3u;
+    } else {
+        tile_pixel(threadIdx.x, lx, ly);
+    }
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.W && y < P.H;
@@ -2842,7 +2850,10 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             const char *eq = std::getenv("VR_M7_WQ");
             if (!(eq && std::atoi(eq) == 0)) {
                 note_kernel("k_march_m7wq", B, method);
-                hipLaunchKernelGGL((k_march_m7wq<B>), grid, block, occupancy_lds(P), s, vol, P);
+                Params Q = P;
+                Q.wq_map = M7_WQ_MAP;
+                if (const char *em = std::getenv("VR_WQ_MAP")) Q.wq_map = std::atoi(em) != 0;
+                hipLaunchKernelGGL((k_march_m7wq<B>), grid, block, occupancy_lds(P), s, vol, Q);
                 break;
             }
         }
