@@ -77,12 +77,55 @@ def parse():
     return ap.parse_args()
 
 
+def lib_sha16(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()[:16]
+
+
+def traffic_entry(args, kernel, world):
+    """(HBM bytes per launch, where they come from) of this workload from the
+    committed PMC passes (profiles/traffic.json, tools/pmc_traffic.py), or
+    (None, why not): only entries measured on this same libvr.so build (its
+    sha256) and kernel count -- a rebuilt library needs a new PMC pass"""
+    if world != 1 or not args.traffic_json or not os.path.exists(args.traffic_json):
+        return None, None
+    import __graft_entry__ as graft
+    key = f"{args.config}|{args.camera}|m{args.method}" + ("|baked" if args.baked else "")
+    with open(args.traffic_json) as f:
+        entry = json.load(f).get(key)
+    if not entry:
+        return None, f"no PMC entry for {key}"
+    sha = lib_sha16(graft.load_package().LIB_PATH)
+    if entry.get("kernel") != kernel or entry.get("lib_sha16") != sha:
+        return None, (f"PMC entry {key} was measured on {entry.get('kernel')} of libvr.so "
+                      f"{entry.get('lib_sha16')}, this run is {kernel} of {sha}")
+    return entry.get("hbm_bytes_per_launch"), (
+        f"{os.path.relpath(args.traffic_json, ROOT)}[{key}]: FETCH_SIZE x 2 + WRITE_SIZE per "
+        f"launch, rocprofv3 --pmc on this libvr.so build ({sha}), {entry.get('measured', '')}")
+
+
+def host_threads():
+    """CPU threads for the baseline and what the host grants: the OpenMP team is
+    OMP_NUM_THREADS when set (the GPU box sets it to the job's CPU share, 16 per
+    GPU), else every CPU in this process's affinity mask."""
+    affinity = len(os.sched_getaffinity(0))
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (env or affinity), {"nproc": os.cpu_count(), "affinity": affinity,
+                               "omp_num_threads_env": env or None}
+
+
 def cpu_baseline(pkg, cfg_name, m, method, row_stride):
-    """The CPU oracle (C, OpenMP) ray-casting the same scene on this host's cores."""
+    """The CPU oracle (C, OpenMP) ray-casting the same scene on this host's cores.
+    Also returns the oracle's frame (packed RGBA8, float RGBA, samples per pixel)
+    of a first, untimed pass for the parity check of the GPU frame."""
     import __graft_entry__ as graft
     orc = graft.load_oracle()
     n, nb, W, H = CONFIGS[cfg_name]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads, host = host_threads()
     if row_stride <= 0:
         row_stride = 1  # the whole frame
     codec = method in (4, 5, 6)
@@ -91,27 +134,52 @@ def cpu_baseline(pkg, cfg_name, m, method, row_stride):
     else:
         vol = orc.synth_volume(n, n, n, nb, SEED, threads)
     p = orc.make_params(W, H, m, query_method=method, m7_dims=(n, n, n))
+
+    def frame(want):
+        if codec:
+            return orc.render_codec(cb, tp, er, p, row_start=0, row_stride=row_stride,
+                                    nthreads=threads)
+        return orc.render(vol, p, row_start=0, row_stride=row_stride, nthreads=threads,
+                          want_float=want, want_steps=want)
+    ref = frame(True)[:3]  # untimed: the parity frame
     # repeat the frame until ~24 core-seconds of work have been timed
     frames, samples, dt = 0, 0, 0.0
     while frames == 0 or dt * threads < 24.0 and frames < 16:
         t0 = time.perf_counter()
-        if codec:
-            _, _, _, s = orc.render_codec(cb, tp, er, p, row_start=0, row_stride=row_stride,
-                                          nthreads=threads)
-        else:
-            _, _, _, s = orc.render(vol, p, row_start=0, row_stride=row_stride,
-                                    nthreads=threads, want_float=False, want_steps=False)
+        _, _, _, smp = frame(False)
         dt += time.perf_counter() - t0
-        samples += s
+        samples += smp
         frames += 1
     rows = len(range(0, H, row_stride))
     rays = rows * W * frames
+    omp = orc.max_threads()
     return {
         "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+        "nproc": host["nproc"], "affinity_cpus": host["affinity"], "omp_max_threads": omp,
         "sample": (f"oracle/vr_oracle.c (-O3, OpenMP) on every {row_stride}th row of the "
                    f"{W}x{H} frame, {frames} frame(s) ({rays} rays, {samples} samples, "
-                   f"{dt:.2f} s on {threads} threads), "
-                   f"full {n}^3x{nb} {'codec ' if codec else ''}volume in host RAM"),
+                   f"{dt:.2f} s on {threads} threads = OMP_NUM_THREADS, the host's CPU share "
+                   f"for this GPU; nproc {host['nproc']}, affinity {host['affinity']} CPUs, "
+                   f"omp_get_max_threads {omp}), full {n}^3x{nb} "
+                   f"{'codec ' if codec else ''}volume in host RAM"),
+    }, (ref, row_stride)
+
+
+def frame_parity(got8, got_f, got_n, ref, row_stride, kernel):
+    """GPU frame vs the oracle's frame (rows 0, s, 2s, ... of the CPU baseline):
+    the reference's own check compares its whole benchmark frame (C:1073-1077)"""
+    r8, rf, rn = ref
+    rows = slice(0, None, row_stride)
+    g8, gf, gn, r8, rf, rn = got8[rows], got_f[rows], got_n[rows], r8[rows], rf[rows], rn[rows]
+    hit = rn >= 0
+    return {
+        "against": "oracle frame of the cpu_baseline (same volume, camera, method)",
+        "rows": int(g8.shape[0]), "pixels": int(g8.size), "hit_pixels": int(hit.sum()),
+        "rgba8_mismatch": int(np.sum(g8 != r8)),
+        "max_abs": float(np.max(np.abs(gf - rf))) if gf.size else 0.0,
+        "tol": 1e-4,
+        "steps_mismatch": int(np.sum(gn[hit] != rn[hit]) + np.sum(gn[~hit] != -1)),
+        "kernel": kernel,
     }
 
 
@@ -147,7 +215,7 @@ def gmm_cpu_baseline(m, method, W, H, K):
     import __graft_entry__ as graft
     orc = graft.load_oracle()
     n = GMM_CPU_EDGE
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads, host = host_threads()
     wm, sg = orc.synth_gmm(n, n, n, K, SEED, nthreads=threads)
     rows = (H // 2 - 24, H // 2 + 24)  # the centre band: the longest rays
     p = orc.make_params(W, H, m, query_method=method)
@@ -160,6 +228,8 @@ def gmm_cpu_baseline(m, method, W, H, K):
         frames += 1
     return {
         "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+        "nproc": host["nproc"], "affinity_cpus": host["affinity"],
+        "omp_max_threads": orc.max_threads(),
         "sample": (f"oracle/vr_oracle.c GMM march (-O3, OpenMP) on the {rows[1] - rows[0]} centre rows of the "
                    f"{W}x{H} frame, {frames} pass(es) ({rays} rays, {dt:.2f} s on {threads} "
                    f"threads), {n}^3 x {K} GMM volume in host RAM (the GPU workload's "
@@ -331,6 +401,7 @@ def main_gmm(args):
         last = frames[(nframe[0] - 1) % R]
         np.save(args.dump_frame, last.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
+    traffic, traffic_src = traffic_entry(args, kernel, world)
     alg_bytes = u * rec_bytes + W * H * 4 if u is not None else None
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
     ms_per_step = elapsed / args.steps * 1e3
@@ -371,7 +442,8 @@ def main_gmm(args):
                 "bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": kernel,
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
@@ -533,23 +605,41 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
 
     # HBM bytes per launch from the committed PMC passes of this same workload
-    # (tools/pmc_traffic.py; FETCH_SIZE x 2 + WRITE_SIZE), only if measured on
-    # the kernel variant that ran here
-    traffic = None
-    if world == 1 and args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            entry = json.load(f).get(f"{args.config}|{args.camera}|m{args.method}"
-                                     + ("|baked" if args.baked else ""))
-        if entry and entry.get("kernel") == kernel:
-            traffic = entry.get("hbm_bytes_per_launch")
+    # (tools/pmc_traffic.py; FETCH_SIZE x 2 + WRITE_SIZE), only if they were
+    # measured on this very libvr.so build (sha256 of the file) and kernel
+    traffic, traffic_src = traffic_entry(args, kernel, world)
+
+    # parity of the timed frame's view (untimed; full frames at N = 1 are checked
+    # against the oracle frame of the CPU baseline below, N > 1 assembled frames
+    # against rank 0's own whole-frame render)
+    check = None
+    if rank == 0:
+        with torch.cuda.stream(stream):
+            g8 = torch.zeros(W * H, dtype=torch.int32, device=dev)
+            gf = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+            gn = torch.full((W * H,), -2, dtype=torch.int32, device=dev)
+            pkg.render(pkg.make_desc(g8, W, H, m, query_method=args.method, d_output_f=gf,
+                                     d_steps=gn))
+        torch.cuda.synchronize()
+        check = (g8.cpu().numpy().view(np.uint32).reshape(H, W),
+                 gf.cpu().numpy().reshape(H, W, 4), gn.cpu().numpy().reshape(H, W),
+                 pkg.last_kernel())
 
     ms_per_step = elapsed / args.steps * 1e3
     value = W * H / (elapsed / args.steps) / 1e6
     out = None
     if rank == 0:
-        cpu = None
+        cpu, parity = None, None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(pkg, args.config, m, args.method, args.cpu_row_stride)
+            cpu, (ref, stride) = cpu_baseline(pkg, args.config, m, args.method,
+                                              args.cpu_row_stride)
+            parity = frame_parity(*check, ref=ref, row_stride=stride)
+            parity["timed_kernel"] = kernel
+        elif world > 1:
+            got = frame.cpu().numpy().view(np.uint32).reshape(H, W)
+            parity = {"against": "rank 0's whole-frame render of the same view",
+                      "pixels": W * H, "rgba8_mismatch": int(np.sum(got != check[0])),
+                      "kernel": check[3]}
         out = {
             "metric": f"Mrays/s + fps at {n}^3 x {nb}-bin volume, {W}x{H}; % HBM roofline",
             "value": round(value, 3),
@@ -584,11 +674,13 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": kernel,
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
                 "U_records": int(u) if u is not None else None,
             },
+            "parity": parity,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -39,8 +39,12 @@ typedef struct { float x, y; } vr_float2;                     /* == float2     *
 /* Replaces render_kernel, K:2387-2401.  Launches the per-ray march into the
  * caller-owned device buffer d_output (imageW*imageH packed RGBA8, row-major,
  * A<<24|B<<16|G<<8|R).  Miss pixels are not written (caller zeroes, C:208).
- * gridSize/blockSize are accepted for ABI compatibility; the library picks its
- * own gfx950 launch geometry (64x4-pixel tiles, one 64-pixel row per wave).
+ * gridSize/blockSize keep their meaning -- pixels with x < gridSize.x*blockSize.x
+ * and y < gridSize.y*blockSize.y are rendered (K:282-286), the rest of the
+ * image is left untouched; an empty grid/block or more than 1024 threads per
+ * block is an invalid launch (VR_ERR_ARG, nothing rendered) -- but not their
+ * geometry: the library picks its own gfx950 launch (64x4-pixel tiles, one
+ * 64-pixel row per wave).
  * volumeSize is used exactly where the reference uses it: the method-7 corner
  * grid (K:322-352).  queryMethod: 1 mean, 2 variance, 3 entropy,
  * 7 software-interpolated mean, 4/5/6 fractal-codec mean / variance / entropy
@@ -118,7 +122,12 @@ void dataProcessing(void);
  * holds sz * Z floats.  Re-uploading or releasing a volume drops its planes; a volume
  * modified in place through vr_volume_info's pointer must be re-baked
  * (vr_release_stats, then vr_bake_stats).  vr_stats_info: device pointers
- * (nullptr = not baked) and plane lengths in floats. */
+ * (nullptr = not baked) and plane lengths in floats.
+ * Layout copy: the first oblique-view frame of a library-owned 8-bin volume
+ * makes a second, 2x2 (x, y) micro-brick copy of its records (DESIGN.md 4.6;
+ * as many bytes as the volume, made synchronously, only while HBM keeps
+ * max(4 GiB, 5 %) free after it).  vr_release_stats drops it with the planes,
+ * so after an in-place modification the next oblique frame rebuilds it. */
 int vr_bake_stats(void);
 int vr_release_stats(void);
 int vr_stats_info(const float **d_raw, uint64_t *raw_plane, const float **d_codec,
@@ -213,6 +222,17 @@ int vr_volume_layout(size_t *row_pitch, size_t *slice_pitch);
 
 /* Stream for all subsequent launches (hipStream_t; NULL = null stream). */
 int vr_set_stream(void *stream);
+
+/* Tuning knobs (tests and tools): kernel-path overrides ("VR_PATH" 0 quad,
+ * 1 LDS-box, 2 per-ray pipelined, 4 wave-staged, 7 ray-segmented; "VR_SEG"
+ * lanes per ray 2/4, pipelined -2/-4), occupancy caps ("VR_WG_PER_CU"),
+ * layout experiments ("VR_PAD", "VR_BRICK", ...).
+ * value NULL removes a knob; vr_clear_tuning removes all.  Every knob only
+ * changes which kernel computes a frame, never its pixels.  The library reads
+ * no environment variables (a build with -DVR_TUNING also takes unset knobs
+ * from the environment, for tooling). */
+int vr_set_tuning(const char *key, const char *value);
+void vr_clear_tuning(void);
 
 /* Explicit-parameter render.  With d_tile_list == NULL the whole frame is
  * rendered into d_output[y*width + x].  Otherwise the n_tiles 64x4-pixel

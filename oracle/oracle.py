@@ -67,6 +67,8 @@ def lib():
                                                            ctypes.c_void_p, ctypes.c_void_p]
         L.orc_splitmix64.argtypes = [ctypes.c_uint64]
         L.orc_splitmix64.restype = ctypes.c_uint64
+        L.orc_max_threads.argtypes = []
+        L.orc_max_threads.restype = ctypes.c_int
         L.orc_synth_fill.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_uint64, fp, ctypes.c_int]
         L.orc_flex_corner.argtypes = [ctypes.POINTER(Flex), ctypes.c_int, ctypes.c_int,
@@ -187,6 +189,11 @@ def synth_codec(nx, ny, nz, nbins, ntemplates=24, slots=None, seed=20261015):
 
 def _fp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def max_threads() -> int:
+    """omp_get_max_threads() of the oracle library in this process"""
+    return int(lib().orc_max_threads())
 
 
 def make_params(width, height, inv_view, density=0.05, brightness=1.0, transfer_offset=0.0,

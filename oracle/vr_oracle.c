@@ -529,6 +529,10 @@ int64_t orc_count_footprint(const float *vol, int nx, int ny, int nz, int nbins,
 /* synthetic distribution volume                       */
 /* ------------------------------------------------------------------------ */
 
+/* omp_get_max_threads() of this process (bench.py reports it beside the
+ * threads the CPU baseline uses) */
+int orc_max_threads(void) { return omp_get_max_threads(); }
+
 uint64_t orc_splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

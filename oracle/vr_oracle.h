@@ -131,6 +131,7 @@ int64_t orc_count_footprint(const float *vol, int nx, int ny, int nz, int nbins,
 void orc_synth_codec(int nx, int ny, int nz, int nbins, int ntpl, int slots, uint64_t seed,
                      int32_t *codebook, float *templates, float *errors);
 uint64_t orc_splitmix64(uint64_t x);
+int orc_max_threads(void);
 void orc_synth_fill(int nx, int ny, int nz, int nbins, uint64_t seed, float *vol,
                     int nthreads);
 

@@ -36,3 +36,22 @@ def gpu(pkg):
     torch.cuda.set_device(0)
     pkg._lib.load()
     return torch.device("cuda", 0)
+
+
+class _Tuning:
+    """vr_set_tuning knobs for one test (kernel-path overrides, occupancy caps,
+    layouts); the library reads no environment, so tests set them explicitly"""
+
+    def __init__(self, pkg):
+        self.pkg = pkg
+
+    def set(self, key, value):
+        self.pkg.set_tuning(key, value)
+
+
+@pytest.fixture
+def tune(pkg):
+    """Tuning knobs, all cleared when the test ends."""
+    pkg.clear_tuning()
+    yield _Tuning(pkg)
+    pkg.clear_tuning()

@@ -91,3 +91,37 @@ def test_flex_table_validation_without_gpu(pkg, orc):
     u["simple_count"][2] = 17
     with pytest.raises(pkg.VRError, match="simple entry 2"):
         pkg.init_flex(u)
+
+
+def test_render_kernel_launch_configuration_without_gpu(pkg):
+    """render_kernel validates gridSize / blockSize like a CUDA launch would
+    (K:2397): an empty grid or block, or > 1024 threads per block, is an
+    invalid configuration, recorded before any device call"""
+    L = pkg._lib.load()
+    for grid, block in (((0, 1, 1), (16, 16, 1)), ((4, 0, 1), (16, 16, 1)),
+                        ((4, 4, 1), (16, 16, 0)), ((4, 4, 1), (64, 32, 1))):
+        with pytest.raises(pkg.VRError) as e:
+            pkg.render_kernel(grid, block, 0x1000, 64, 64, 0.05, 1.0, 0.0, 1.0, 1, (4, 4, 4))
+        assert e.value.status == pkg._lib.VR_ERR_ARG
+        assert "launch configuration" in str(e.value)
+    L.vr_clear_error()
+
+
+def test_tuning_knobs_are_explicit(pkg):
+    """knobs go through vr_set_tuning only (no environment reads in the default
+    build); an empty key is rejected, None removes a knob"""
+    pkg.set_tuning("VR_PATH", "2")
+    pkg.set_tuning("VR_PATH", None)
+    pkg.clear_tuning()
+    with pytest.raises(pkg.VRError) as e:
+        pkg.set_tuning("", "1")
+    assert e.value.status == pkg._lib.VR_ERR_ARG
+    src = open(os.path.join(ROOT, "volume-rendering-based-on-distribution-data_amd", "csrc",
+                            "vr_api.cpp")).read()
+    # the only getenv sits behind the tooling build flag
+    assert src.count("getenv(") == 1
+    i = src.index("getenv(")
+    assert src.rfind("#ifdef VR_TUNING", 0, i) > src.rfind("#endif", 0, i)
+    for f in ("vr_kernels.hip", "vr_seg.hip", "vr_gmm.hip", "vr_stats.hip", "vr_flex.hip"):
+        assert "getenv(" not in open(os.path.join(ROOT, "volume-rendering-based-on-"
+                                                  "distribution-data_amd", "csrc", f)).read()

@@ -47,12 +47,12 @@ def plane_index(x, y, z, sy, sz):
 
 @pytest.mark.parametrize("nx,ny,nz", [(9, 7, 5), (31, 6, 3), (46, 3, 2)])
 @pytest.mark.parametrize("nb", [1, 3, 4, 8, 32])
-def test_planes_equal_oracle_stats(pkg, orc, gpu, baked, nb, nx, ny, nz, monkeypatch):
+def test_planes_equal_oracle_stats(pkg, orc, gpu, baked, nb, nx, ny, nz, tune):
     """plane k < 3 at plane_index(x, y, z) = statistic k+1 of record (x, y, z)
     (orc_record_stats), plane 3 = method 7's corner mean (orc_corner_mean), bit for bit;
     x = 15 k also in the apron (offset 15) of brick k - 1; records with padded rows /
     slices"""
-    monkeypatch.setenv("VR_PAD", "3,5")
+    tune.set("VR_PAD", "3,5")
     vol = orc.synth_volume(nx, ny, nz, nb)
     pkg.init_distribution(vol)
     assert pkg.stats_info()[0][0] is None
@@ -92,15 +92,15 @@ def test_baked_render_parity(pkg, orc, gpu, baked, nb):
 
 @pytest.mark.parametrize("path,env", [
     ("1", {}), ("1", {"VR_BOX_MAX": "64"}), ("7", {"VR_SEG": "-2"}), ("7", {"VR_SEG": "4"}),
-    ("7", {"VR_SEG": "-8"}), ("2", {"VR_WG_PER_CU": "2"}), ("7", {"VR_SEG": "1"}),
+    ("7", {"VR_SEG": "-4"}), ("2", {"VR_WG_PER_CU": "2"}), ("7", {"VR_SEG": "2"}),
 ])
-def test_baked_paths(pkg, orc, gpu, baked, path, env, monkeypatch):
+def test_baked_paths(pkg, orc, gpu, baked, path, env, tune):
     """every kernel a baked frame can take (VR_PATH 2 / 7; 1, the LDS-box march over x
     rows, is ignored for the bricked planes) is bit-identical"""
     import torch
-    monkeypatch.setenv("VR_PATH", path)
+    tune.set("VR_PATH", path)
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        tune.set(k, v)
     vol = orc.synth_volume(20, 18, 16, 8)
     pkg.init_distribution(vol)
     pkg.bake_stats()
@@ -193,11 +193,11 @@ def test_release_reupload_and_errors(pkg, orc, gpu, baked):
 
 @pytest.mark.parametrize("nb", [1, 4, 8, 32])
 @pytest.mark.parametrize("pipe", ["1", "0"])
-def test_baked_method7(pkg, orc, gpu, baked, nb, pipe, monkeypatch):
+def test_baked_method7(pkg, orc, gpu, baked, nb, pipe, tune):
     """method 7 from the baked corner means (plane 3): the corner cache and double lerps of
     K:395-480 over 4-byte corners, both m7 kernels, grid = volume and grid != volume"""
     import torch
-    monkeypatch.setenv("VR_M7_PIPE", pipe)
+    tune.set("VR_M7_PIPE", pipe)
     vol = orc.synth_volume(18, 16, 14, nb)
     pkg.init_distribution(vol)
     pkg.bake_stats()

@@ -14,8 +14,8 @@ pytestmark = pytest.mark.gpu
 
 # kernel-path overrides a case may take (vr_api.cpp fill_params / baked_path)
 PATHS = [{}, {}, {"VR_PATH": "0"}, {"VR_PATH": "1"}, {"VR_PATH": "1", "VR_BOX_MAX": "64"},
-         {"VR_PATH": "2"}, {"VR_PATH": "4"}, {"VR_PATH": "3"}, {"VR_PATH": "7", "VR_SEG": "-2"},
-         {"VR_PATH": "7", "VR_SEG": "4"}, {"VR_PATH": "5"}, {"VR_WG_PER_CU": "2"}]
+         {"VR_PATH": "2"}, {"VR_PATH": "4"}, {"VR_PATH": "7", "VR_SEG": "-4"},
+         {"VR_PATH": "7", "VR_SEG": "-2"}, {"VR_PATH": "7", "VR_SEG": "4"}, {"VR_WG_PER_CU": "2"}]
 
 
 def draw_camera(pkg, rng):
@@ -43,7 +43,7 @@ def draw_params(rng):
 
 
 @pytest.mark.parametrize("seed", range(200))
-def test_random_histogram_case(pkg, orc, gpu, seed, monkeypatch):
+def test_random_histogram_case(pkg, orc, gpu, seed, tune):
     import torch
     rng = np.random.default_rng(1000 + seed)
     dims = tuple(int(v) for v in rng.integers(2, 41, 3))
@@ -56,7 +56,7 @@ def test_random_histogram_case(pkg, orc, gpu, seed, monkeypatch):
     baked = bool(rng.integers(0, 3) == 0)
     m7 = tuple(int(v) for v in rng.integers(2, 41, 3)) if rng.integers(0, 2) else dims
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        tune.set(k, v)
     vol = orc.synth_volume(*dims, nb, seed=seed)
     pkg.init_distribution(vol)
     if baked:

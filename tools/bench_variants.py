@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--pads", nargs="*", default=[""],
                     help="VR_PAD layouts to synthesize in turn, e.g. '' '4,0' '4,64'")
     ap.add_argument("--env", nargs="*", default=[""],
-                    help="env settings to sweep, e.g. 'VR_BOX_MAX=0' 'VR_WG_PER_CU=4,VR_BOX_MAX=0'")
+                    help="tuning knobs (vr_set_tuning) to sweep, e.g. 'VR_BOX_MAX=0' 'VR_WG_PER_CU=4,VR_BOX_MAX=0'")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
@@ -58,6 +58,7 @@ def main():
                                      ctypes.POINTER(ctypes.c_int),
                                      ctypes.POINTER(ctypes.c_void_p)]
         L.vr_last_error.restype = ctypes.c_char_p
+        L.vr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         libs[name] = L
     torch.cuda.set_device(0)
     for pad in args.pads:
@@ -67,11 +68,9 @@ def main():
 def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
     first = next(iter(libs.values()))
     ext = pkg._lib.Extent(n, n, n)
-    if pad:
-        os.environ["VR_PAD"] = pad
-    else:
-        os.environ.pop("VR_PAD", None)
+    first.vr_set_tuning(b"VR_PAD", pad.encode() if pad else None)
     assert first.vr_synthesize(ext, nb, bench.SEED) == 0
+    first.vr_set_tuning(b"VR_PAD", None)
     ptr = ctypes.c_void_p()
     first.vr_volume_info(None, None, ctypes.byref(ptr))
     for L in list(libs.values())[1:]:  # other variants adopt the same (dense) volume
@@ -93,13 +92,12 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
         envs.append(d)
     configs = list(itertools.product(libs.keys(), envs, descs.keys()))
     times = {i: [] for i in range(len(configs))}
-    base_env = dict(os.environ)
     for rnd in range(args.rounds):
         for i, (name, env, cam) in enumerate(configs):
-            os.environ.clear()
-            os.environ.update(base_env)
-            os.environ.update(env)
             L = libs[name]
+            L.vr_clear_tuning()
+            for k, v in env.items():  # knobs (vr_set_tuning): the library reads no environment
+                L.vr_set_tuning(k.encode(), v.encode())
             d = descs[cam]
             # two untimed frames: a changed env re-keys the frame order, whose first
             # frame records tile costs and whose second re-deals by them (host sync)
@@ -119,8 +117,8 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / args.reps)
         print(f"round {rnd} done", file=sys.stderr, flush=True)
-    os.environ.clear()
-    os.environ.update(base_env)
+    for L in libs.values():
+        L.vr_clear_tuning()
     print(f"config {args.config} method {args.method} pad '{pad}'"
           + (" baked" if args.baked else ""))
     for i, (name, env, cam) in enumerate(configs):

@@ -33,8 +33,9 @@ def per_dispatch(dirs):
             rows = collections.defaultdict(dict)
             for r in csv.DictReader(open(f)):
                 k = r["Kernel_Name"]
-                if "vr::k_march" not in k or ("vr::k_march<" in k and ", true>" in k):
-                    continue  # the march only (not the footprint-counting variant)
+                if "vr::k_march" not in k or ", true>" in k and ("vr::k_march<" in k or
+                                                                  "vr::k_march_gmm<" in k):
+                    continue  # the march only (not the footprint-counting variants)
                 rows[(k, r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
             for (k, _), cs in rows.items():
                 names[k] = names.get(k, 0) + 1
@@ -70,6 +71,14 @@ def main():
     }
     if entry["read_bytes"] is not None and entry["write_bytes"] is not None:
         entry["hbm_bytes_per_launch"] = int(entry["read_bytes"] + entry["write_bytes"])
+    # the build the passes ran on: bench.py reports this traffic only for it
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench as _bench
+    lib = os.environ.get("VRDD_LIB") or os.path.join(
+        root, "volume-rendering-based-on-distribution-data_amd", "csrc", "build", "libvr.so")
+    entry["lib_sha16"] = _bench.lib_sha16(lib)
+    entry["measured"] = os.environ.get("PMC_TAG", "")
     db = {}
     if os.path.exists(out_path):
         db = json.load(open(out_path))

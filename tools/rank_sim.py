@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--no-lpt", action="store_true", help="tile lists without longest-first order")
     ap.add_argument("--baked", action="store_true", help="bake the statistics planes first")
-    ap.add_argument("--env", default="", help="NAME=VALUE[,NAME=VALUE] set for the renders")
+    ap.add_argument("--env", default="", help="tuning knobs NAME=VALUE[,NAME=VALUE] (vr_set_tuning) for the renders")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
@@ -37,7 +37,7 @@ def main():
         pkg.bake_stats()
     for kv in filter(None, args.env.split(",")):
         k, v = kv.split("=")
-        os.environ[k] = v
+        pkg.set_tuning(k, v)  # tuning knobs: the library reads no environment
     m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
          else pkg.camera.display_inv_view((30.0, 45.0)))
 

@@ -5,7 +5,7 @@ rendered alone, as tools/rank_sim.py does) with vr_debug_wave_clock on, and
 prints for each launch: span, live waves over time (per XCD), when the live
 count falls below 90 / 50 / 10 % of its peak, and wave-duration statistics.
 
-  VR_PATH=2 python tools/wave_timeline.py [--camera C0] [--world 8] [--ranks 0,1]
+  python tools/wave_timeline.py [--camera C0] [--world 8] [--ranks 0,1] [--env VR_PATH=2]
 """
 import argparse
 import os
@@ -58,11 +58,16 @@ def main():
     ap.add_argument("--camera", default="C0")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--ranks", default="0")
+    ap.add_argument("--env", default="VR_PATH=2",
+                    help="tuning knobs NAME=VALUE[,NAME=VALUE] (vr_set_tuning)")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
     import bench
     pkg = g.load_package()
+    for kv in filter(None, args.env.split(",")):
+        k, v = kv.split("=")
+        pkg.set_tuning(k, v)
     n, nb, W, H = bench.CONFIGS[args.config]
     pkg.synthesize((n, n, n), nb, bench.SEED)
     m = (pkg.camera.single_test_inv_view() if args.camera == "C0"

@@ -98,6 +98,7 @@ EXPORTS = [
     "vr_load_flex_files", "vr_debug_wave_clock",
     "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_render_gmm",
     "vr_gmm_count_footprint", "vr_bake_stats", "vr_release_stats", "vr_stats_info",
+    "vr_set_tuning", "vr_clear_tuning",
 ]
 
 _lib = None
@@ -212,6 +213,10 @@ def load() -> ctypes.CDLL:
     L.vr_release_stats.restype = i32
     L.vr_stats_info.argtypes = [vp] * 4
     L.vr_stats_info.restype = i32
+    L.vr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    L.vr_set_tuning.restype = i32
+    L.vr_clear_tuning.argtypes = []
+    L.vr_clear_tuning.restype = None
     _lib = L
     return L
 

@@ -332,6 +332,20 @@ def set_stream(stream) -> None:
     check(_lib.load().vr_set_stream(raw))
 
 
+def set_tuning(key: str, value=None) -> None:
+    """Set (value not None) or remove a tuning knob (include/vr.h vr_set_tuning):
+    kernel-path overrides and occupancy caps for tests and tools.  Knobs change
+    which kernel computes a frame, never its pixels; the library reads no
+    environment variables."""
+    L = _lib.load()
+    check(L.vr_set_tuning(str(key).encode(), None if value is None else str(value).encode()))
+
+
+def clear_tuning() -> None:
+    """Remove every tuning knob (back to the default dispatch)."""
+    _lib.load().vr_clear_tuning()
+
+
 def make_desc(d_output, width: int, height: int, inv_view, density=0.05, brightness=1.0,
               transfer_offset=0.0, transfer_scale=1.0, query_method=1, volume_size=None,
               d_output_f=None, d_steps=None, d_tile_list=None, n_tiles=0) -> RenderDesc:
@@ -403,14 +417,25 @@ def init_gmm(wm, sigma, dims=None, z_base: int = 0, adopt: bool = False) -> None
     nzs, ny, nx, K = (int(v) for v in wm.shape[:4])
     if dims is None:
         dims = (nx, ny, nzs)
+    if len(wm.shape) != 5 or int(wm.shape[4]) != 2:
+        raise ValueError(f"wm must have shape (nzs, ny, nx, K, 2), got {tuple(wm.shape)}")
+    if tuple(int(v) for v in sigma.shape) != (nzs, ny, nx, K):
+        raise ValueError(f"sigma must have shape wm.shape[:4] = {(nzs, ny, nx, K)}, "
+                         f"got {tuple(sigma.shape)}")
     if hasattr(wm, "data_ptr") and getattr(wm, "is_cuda", False):
+        import torch
+        for name, t in (("wm", wm), ("sigma", sigma)):
+            if not getattr(t, "is_cuda", False):
+                raise ValueError(f"{name} must be a CUDA tensor like wm")
+            if t.dtype != torch.float32:
+                raise ValueError(f"{name} must be float32, got {t.dtype}")
+            if not t.is_contiguous():
+                raise ValueError(f"{name} must be contiguous (the march reads dense planes)")
         check(L.vr_init_gmm(_ptr(wm), _ptr(sigma), _extent(dims), K, int(z_base), nzs,
                             2 if adopt else 1))
         return
     a = np.ascontiguousarray(np.asarray(wm, dtype=np.float32))
     b = np.ascontiguousarray(np.asarray(sigma, dtype=np.float32))
-    if b.shape != a.shape[:4]:
-        raise ValueError("sigma must have shape wm.shape[:4]")
     check(L.vr_init_gmm(a.ctypes.data, b.ctypes.data, _extent(dims), K, int(z_base), nzs, 0))
 
 
@@ -469,7 +494,7 @@ __all__ = [
     "flex_process", "flex_info", "load_flex_files", "parse_flex_files", "synthesize", "synthesize_codec", "codec_info",
     "volume_info",
     "volume_layout",
-    "set_stream", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "version",
+    "set_stream", "set_tuning", "clear_tuning", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "version",
     "init_gmm", "synthesize_gmm", "gmm_info", "free_gmm", "gmm_slab", "render_gmm",
     "gmm_count_footprint", "bake_stats", "release_stats", "stats_info",
     "VRError", "PAD",

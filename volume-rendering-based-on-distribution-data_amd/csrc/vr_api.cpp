@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -83,6 +84,13 @@ struct State {
 
 State g;
 
+// Tuning knobs: kernel-path overrides, occupancy caps and layout experiments
+// (tests force every kernel path through them; tools sweep them).  Set only
+// through vr_set_tuning; the default build never reads the environment, so a
+// variable left set in a shell cannot change which kernel runs.  A build with
+// -DVR_TUNING also takes unset knobs from the environment (tooling).
+std::map<std::string, std::string> g_tuning;
+
 int fail(int status, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -137,7 +145,7 @@ void release_volume() {
 // px records to every row and pz records to every slice (layout experiments).
 void choose_pitch(int nx, int ny, uint64_t &sy, uint64_t &sz) {
     long px = 0, pz = 0;
-    if (const char *e = std::getenv("VR_PAD")) {
+    if (const char *e = vr::tuning("VR_PAD")) {
         char *end = nullptr;
         px = std::strtol(e, &end, 10);
         if (end && *end == ',') pz = std::strtol(end + 1, nullptr, 10);
@@ -303,7 +311,7 @@ void lists_from_costs(const std::vector<uint32_t> &cost, uint32_t tx, uint32_t t
 int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_t *&perm,
                 uint32_t **record) {
     uint32_t bx = 1, by = 4;
-    if (const char *e = std::getenv("VR_XBLOCK")) {
+    if (const char *e = vr::tuning("VR_XBLOCK")) {
         char *end = nullptr;
         const long a = std::strtol(e, &end, 10);
         long b = a;
@@ -315,7 +323,7 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
     // everything that changes the samples each ray takes keys the order
     uint32_t key[22] = {d->width, d->height, bx, by};
     std::memcpy(key + 4, d->inv_view, sizeof d->inv_view);
-    key[16] = std::getenv("VR_NO_LPT") ? 1u : 0u;
+    key[16] = vr::tuning("VR_NO_LPT") ? 1u : 0u;
     key[17] = (uint32_t)d->query_method;
     std::memcpy(key + 18, &d->density, sizeof(float));
     std::memcpy(key + 19, &d->transfer_offset, sizeof(float));
@@ -379,7 +387,7 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
     if (rc != VR_OK) return rc;
     std::memcpy(g.perm_key, key, sizeof key);
     perm = g.perm;
-    g.order_state = (key[16] || std::getenv("VR_NO_ADAPT")) ? 2 : 1;
+    g.order_state = (key[16] || vr::tuning("VR_NO_ADAPT")) ? 2 : 1;
     g.cost_recorded = false;
     if (g.order_state == 1) {
         if (ntile > g.tile_cost_cap) {
@@ -447,6 +455,8 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     std::memcpy(P.m, d->inv_view, sizeof P.m);
     P.W = d->width;
     P.H = d->height;
+    P.CW = d->width;
+    P.CH = d->height;
     P.density = d->density;
     P.brightness = d->brightness;
     P.toff = d->transfer_offset;
@@ -463,7 +473,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         P.err_slots = g.err_slots;
         // template tables up to 32 KiB are staged in LDS (VR_CODEC_LDS=0 disables)
         const size_t tb = (size_t)g.ntpl * g.cnb * sizeof(float);
-        const char *el = std::getenv("VR_CODEC_LDS");
+        const char *el = vr::tuning("VR_CODEC_LDS");
         P.tpl_lds = (tb <= 32768 && !(el && std::atoi(el) == 0)) ? (int)tb : 0;
     } else {
         P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
@@ -494,13 +504,13 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     P.mark = nullptr;
     // VR_BOX_MAX: per-wave LDS box capacity (tuning / ablation knob; 0 disables staging)
     P.box_max = vr::kBoxMax;
-    if (const char *e = std::getenv("VR_BOX_MAX")) {
+    if (const char *e = vr::tuning("VR_BOX_MAX")) {
         const int v = std::atoi(e);
         if (v >= 0 && v <= 2048) P.box_max = v;
     }
     // VR_WG_PER_CU: cap resident workgroups per CU through the LDS request (tuning knob)
     P.wg_per_cu = 0;
-    if (const char *e = std::getenv("VR_WG_PER_CU")) {
+    if (const char *e = vr::tuning("VR_WG_PER_CU")) {
         const int v = std::atoi(e);
         if (v >= 1 && v <= 32) P.wg_per_cu = v;
     }
@@ -512,10 +522,9 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // decodes every record once per wave-step instead of once per touching
     // ray.  Oblique views use the quad-cooperative gathers (path 0, B == 8),
     // which keep every 4-lane group on one contiguous 64-byte run.
-    // VR_PATH overrides: 0 quad, 1 k_march (LDS-staged box / per-ray),
-    // 2 per-ray pipelined, 3 workgroup-staged rows, 4 wave-staged rows,
-    // 5 per-ray half-step pipelined, 6 per-ray with neighbour-shared x1 records,
-    // 7 ray-segmented (VR_SEG lanes per ray).
+    // VR_PATH overrides (vr_set_tuning): 0 quad, 1 k_march (LDS-staged box /
+    // per-ray), 2 per-ray pipelined, 4 wave-staged rows, 7 ray-segmented
+    // (VR_SEG lanes per ray).
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
     P.oblique = along_rows ? 0 : 1;
@@ -530,7 +539,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // 0.81 ms) (tools/rank_sim.py, tools/gpu_seg4.sh).
     // VR_SEG_RAYS overrides the ray-count threshold.
     uint64_t seg_rays = 700000;
-    if (const char *e = std::getenv("VR_SEG_RAYS")) seg_rays = std::strtoull(e, nullptr, 10);
+    if (const char *e = vr::tuning("VR_SEG_RAYS")) seg_rays = std::strtoull(e, nullptr, 10);
     if (along_rows && d->d_tile_list && (d->query_method == 1 || d->query_method == 2) &&
         (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= seg_rays)
         P.path = 7;
@@ -554,7 +563,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // 6.04; profiles/r02/wide_records.log), entropy included: decoding each record
     // once per wave is what the log-heavy wide decode needs (VR_BOX3=0: quad march).
     const bool wide3 = (g.nb == 16 || g.nb == 32) && d->query_method == 3 &&
-                       !(std::getenv("VR_BOX3") && std::atoi(std::getenv("VR_BOX3")) == 0);
+                       !(vr::tuning("VR_BOX3") && std::atoi(vr::tuning("VR_BOX3")) == 0);
     if (along_rows && !d->d_tile_list && (g.nb == 8 || g.nb == 16 || g.nb == 32) &&
         (d->query_method == 1 || d->query_method == 2 || wide3) &&
         (uint64_t)d->width * d->height > seg_rays &&
@@ -579,17 +588,16 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
             small_seg = rays <= 131072 ? -4 : -2;
         }
     }
-    if (const char *e = std::getenv("VR_PATH")) {
+    if (const char *e = vr::tuning("VR_PATH")) {
         const int v = std::atoi(e);
-        if (v >= 0 && v <= 9) P.path = v;
+        if (v == 0 || v == 1 || v == 2 || v == 4 || v == 7) P.path = v;
     }
     P.wave_clock = g.wave_clock;
     P.tile_cost = record;
-    P.hyb_tiles = 0;
     P.seg_lanes = small_seg ? small_seg : -2;  // VR_SEG=S: S lanes per ray, negative = pipelined windows
-    if (const char *e = std::getenv("VR_SEG")) {
+    if (const char *e = vr::tuning("VR_SEG")) {
         const int v = std::atoi(e);
-        if (v != 0 && v >= -8 && v <= 8 && (abs(v) & (abs(v) - 1)) == 0) P.seg_lanes = v;
+        if (v == 2 || v == 4 || v == -2 || v == -4) P.seg_lanes = v;
     }
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {
@@ -599,14 +607,6 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         nslots = (uint32_t)all;
     }
     P.n_tiles = nslots;
-    // VR_HYB=K: hybrid march (path 9), the first K slots ray-segmented
-    if (const char *e = std::getenv("VR_HYB")) {
-        const long k = std::atol(e);
-        if (k > 0) {
-            P.path = 9;
-            P.hyb_tiles = (int)std::min<uint64_t>((uint64_t)k & ~7ull, nslots & ~7u);
-        }
-    }
     return VR_OK;
 }
 
@@ -633,7 +633,7 @@ int baked_path(const vr_render_desc *d, vr::Params &P) {
         if (rays <= 400000) path = 7;
         else if (rays <= 700000) path = 7, seg = -2;
     }
-    if (path == 7 && !std::getenv("VR_SEG")) P.seg_lanes = seg;
+    if (path == 7 && !vr::tuning("VR_SEG")) P.seg_lanes = seg;
     // oblique full frames of a fine volume (< 4 pixels per voxel of the x-y
     // face): 4 workgroups per CU, fewer rays' lines in flight per L2 (1024^3
     // C1 1.28 -> 1.11 ms; 2-3 per CU 1.25, 6 1.19); coarse volumes (512^3:
@@ -641,7 +641,7 @@ int baked_path(const vr_render_desc *d, vr::Params &P) {
     if (!along_rows && !d->d_tile_list && P.wg_per_cu == 0 &&
         (uint64_t)d->width * d->height < 4ull * (uint64_t)P.nx * (uint64_t)P.ny)
         P.wg_per_cu = 4;
-    if (const char *e = std::getenv("VR_PATH")) {  // the LDS-box march (1) reads x rows only
+    if (const char *e = vr::tuning("VR_PATH")) {  // the LDS-box march (1) reads x rows only
         const int v = std::atoi(e);
         if (v == 2 || v == 7) path = v;
     }
@@ -733,18 +733,20 @@ void blob_axis(int n, double c, double s, float *out) {
 // one 128-B line when x0 and y0 are even, so a wave step touches fewer lines
 // than in x rows.  Made on the first such frame of an owned
 // volume (a caller-owned buffer adopted by vr_init_distribution may change
-// behind the library's back), only if HBM keeps 1 GiB free after it; without
-// it the quad march reads the x rows.  VR_BRICK=0 disables it.
+// behind the library's back), only if HBM keeps max(4 GiB, 5 %) free after it; without
+// it the quad march reads the x rows.  VR_BRICK=0 (vr_set_tuning) disables it.
 bool ensure_brick() {
-    if (const char *e = std::getenv("VR_BRICK"))
+    if (const char *e = vr::tuning("VR_BRICK"))
         if (std::atoi(e) == 0) return false;
     if (g.brick) return true;
     if (!g.vol || !g.owned || g.nb != 8) return false;
     const uint64_t nxp = (uint64_t)g.nx + (g.nx & 1), nyp = (uint64_t)g.ny + (g.ny & 1);
     const uint64_t bsy = 2 * nxp, bsz = nxp * nyp;
     const uint64_t bytes = bsz * (uint64_t)g.nz * 8 * sizeof(float);
+    // the copy must leave max(4 GiB, 5 % of the device) free for the caller
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (1ull << 30)) {
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
+        free_b < bytes + std::max<uint64_t>(4ull << 30, total_b / 20)) {
         (void)hipGetLastError();
         return false;
     }
@@ -757,7 +759,10 @@ bool ensure_brick() {
     std::memset(&P, 0, sizeof P);
     P.nx = g.nx; P.ny = g.ny; P.nz = g.nz;
     P.sy = g.sy; P.sz = g.sz;
-    if (vr::launch_brick8(g.vol, P, buf, bsy, bsz, g.stream) != hipSuccess) {
+    // synchronous, like the statistics bake: a later frame may run on another
+    // stream (vr_set_stream) and must never see a partly written copy
+    if (vr::launch_brick8(g.vol, P, buf, bsy, bsz, g.stream) != hipSuccess ||
+        hipStreamSynchronize(g.stream) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFree(buf);
         return false;
@@ -772,6 +777,15 @@ bool ensure_brick() {
 
 namespace vr {
 int record_error(int status, const char *msg) { return fail(status, "%s", msg); }
+const char *tuning(const char *key) {
+    auto it = g_tuning.find(key);
+    if (it != g_tuning.end()) return it->second.c_str();
+#ifdef VR_TUNING
+    return std::getenv(key);
+#else
+    return nullptr;
+#endif
+}
 // Span index: sorted keys and, per key, the entry the reference's linear scan
 // (K:1352-1372) returns -- its `break` leaves only the x loop, so among equal
 // spans the last 64-entry row holding one wins, and its first entry.  Entries
@@ -833,12 +847,6 @@ int vr_selftest_logf(uint64_t *counts) {
     return VR_OK;
 }
 
-#ifdef VR_WG_PROF
-// tooling build only (tools/wg_prof.py): read and reset the phase counters
-int vr_wg_prof_read(unsigned long long *host16) {
-    return vr::wg_prof_read(host16) == hipSuccess ? VR_OK : VR_ERR_HIP;
-}
-#endif
 const char *vr_last_error(void) { return g.err.c_str(); }
 int vr_last_status(void) { return g.status; }
 void vr_clear_error(void) {
@@ -848,6 +856,19 @@ void vr_clear_error(void) {
 
 uint32_t vr_tiles_x(uint32_t width) { return tiles_x(width); }
 uint32_t vr_tiles_y(uint32_t height) { return tiles_y(height); }
+
+int vr_set_tuning(const char *key, const char *value) {
+    if (!key || !*key) return fail(VR_ERR_ARG, "vr_set_tuning: empty key");
+    if (value) g_tuning[key] = value;
+    else g_tuning.erase(key);
+    g.perm_key[0] = 0;  // knobs such as VR_XBLOCK / VR_NO_LPT shape the frame order
+    return VR_OK;
+}
+
+void vr_clear_tuning(void) {
+    g_tuning.clear();
+    g.perm_key[0] = 0;
+}
 
 int vr_set_stream(void *stream) {
     g.stream = (hipStream_t)stream;
@@ -1246,11 +1267,28 @@ int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins) {
     return VR_OK;
 }
 
-int vr_render(const vr_render_desc *desc) {
+}  // extern "C"
+
+namespace {
+
+// One frame of vr_render / render_kernel; clip_w x clip_h is the top-left
+// rectangle of pixels the launch covers (render_kernel's gridSize x blockSize,
+// K:2397 + K:282-286; the whole image otherwise).
+int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
     vr::Params P;
     uint32_t nslots = 0;
     int rc = fill_params(desc, P, nslots, true);
     if (rc != VR_OK) return rc;
+    P.CW = std::min(clip_w, P.W);
+    P.CH = std::min(clip_h, P.H);
+    if (P.CW < P.W || P.CH < P.H) {
+        // the launch keeps the whole frame's tiles and order; pixels outside
+        // the rectangle leave at once (miss-free: nothing written), and the
+        // frame records no tile costs for the adaptive order
+        if (desc->d_tile_list) return fail(VR_ERR_ARG, "a clipped render takes the whole frame");
+        if (P.CW == 0 || P.CH == 0) return VR_OK;
+        P.tile_cost = nullptr;
+    }
     hipError_t e;
     const int qm = desc->query_method;
     const float *baked = (qm >= 1 && qm <= 3 && g.stats)   ? g.stats + (uint64_t)(qm - 1) * g.stats_plane
@@ -1282,7 +1320,7 @@ int vr_render(const vr_render_desc *desc) {
     } else {
         // the quad marches of oblique views (methods 1/2/3 on path 0; method 7
         // when its grid is the volume's) read the micro-brick copy
-        const char *eq = std::getenv("VR_M7_QUAD");
+        const char *eq = vr::tuning("VR_M7_QUAD");
         const bool m7_quad = qm == 7 && P.oblique && P.m7x == P.nx && P.m7y == P.ny &&
                              P.m7z == P.nz && !(eq && std::atoi(eq) == 0);
         if (g.nb == 8 && ((P.path == 0 && qm >= 1 && qm <= 3) || m7_quad) && ensure_brick()) {
@@ -1296,6 +1334,12 @@ int vr_render(const vr_render_desc *desc) {
     if (P.tile_cost) g.cost_recorded = true;
     return VR_OK;
 }
+
+}  // namespace
+
+extern "C" {
+
+int vr_render(const vr_render_desc *desc) { return render_frame(desc, UINT32_MAX, UINT32_MAX); }
 
 int vr_debug_wave_clock(uint64_t *d_buf) {
     g.wave_clock = reinterpret_cast<unsigned long long *>(d_buf);
@@ -1414,6 +1458,8 @@ int fill_gmm_params(const vr_render_desc *d, const vr_gmm_slab *slab, vr::Params
     std::memcpy(P.m, d->inv_view, sizeof P.m);
     P.W = d->width;
     P.H = d->height;
+    P.CW = d->width;
+    P.CH = d->height;
     P.density = d->density;
     P.brightness = d->brightness;
     P.toff = d->transfer_offset;
@@ -1429,7 +1475,7 @@ int fill_gmm_params(const vr_render_desc *d, const vr_gmm_slab *slab, vr::Params
     P.out_f = d->d_output_f;
     P.out_n = d->d_steps;
     device_lds(P.lds_cu, P.lds_wg);
-    if (const char *e = std::getenv("VR_WG_PER_CU")) {
+    if (const char *e = vr::tuning("VR_WG_PER_CU")) {
         const int v = std::atoi(e);
         if (v >= 1 && v <= 32) P.wg_per_cu = v;
     }
@@ -1437,7 +1483,7 @@ int fill_gmm_params(const vr_render_desc *d, const vr_gmm_slab *slab, vr::Params
     // same step, so their corner loads share lines (1024^3 x 16, 1080p: C0
     // 4.89 -> 4.20 ms, C1 7.88 -> 7.38); VR_GMM_LOCKSTEP=0 refills groups one by one
     P.path = 1;
-    if (const char *e = std::getenv("VR_GMM_LOCKSTEP")) P.path = std::atoi(e) ? 1 : 0;
+    if (const char *e = vr::tuning("VR_GMM_LOCKSTEP")) P.path = std::atoi(e) ? 1 : 0;
     const int zr_hi = g.gmm.z_base + g.gmm.nzs;  // resident slices end (exclusive)
     if (!slab) {
         if (g.gmm.z_base != 0 || g.gmm.nzs != g.gmm.nz)
@@ -1629,8 +1675,18 @@ int64_t vr_gmm_count_footprint(const vr_render_desc *desc) {
 void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output, uint32_t imageW,
                    uint32_t imageH, float density, float brightness, float transferOffset,
                    float transferScale, int queryMethod, vr_extent volumeSize) {
-    (void)gridSize;
-    (void)blockSize;
+    // d_render covers x = blockIdx.x * blockDim.x + threadIdx.x < imageW (and
+    // the same in y, K:282-286): a grid smaller than the image leaves the
+    // pixels beyond gridSize x blockSize untouched, a larger one is cut at the
+    // image.  An empty or over-sized launch fails like the reference's launch
+    // would (cudaErrorInvalidConfiguration, reported by getLastCudaError, C:214).
+    const uint64_t threads = (uint64_t)blockSize.x * blockSize.y * blockSize.z;
+    if (gridSize.x == 0 || gridSize.y == 0 || gridSize.z == 0 || threads == 0 || threads > 1024) {
+        fail(VR_ERR_ARG, "render_kernel: invalid launch configuration grid (%u,%u,%u) block (%u,%u,%u)",
+             gridSize.x, gridSize.y, gridSize.z, blockSize.x, blockSize.y, blockSize.z);
+        return;
+    }
+    const uint64_t cw = (uint64_t)gridSize.x * blockSize.x, ch = (uint64_t)gridSize.y * blockSize.y;
     vr_render_desc d;
     std::memset(&d, 0, sizeof d);
     d.d_output = d_output;
@@ -1643,7 +1699,8 @@ void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output, uint
     d.transfer_scale = transferScale;
     d.query_method = queryMethod;
     d.volume_size = volumeSize;
-    (void)vr_render(&d);
+    (void)render_frame(&d, (uint32_t)std::min<uint64_t>(cw, UINT32_MAX),
+                       (uint32_t)std::min<uint64_t>(ch, UINT32_MAX));
 }
 
 void copyInvViewMatrix(float *invViewMatrix, size_t sizeofMatrix) {
@@ -1737,6 +1794,7 @@ int vr_bake_stats(void) { return bake_stats(); }
 int vr_release_stats(void) {
     release_stats();
     release_cstats();
+    release_brick();  // the micro-brick copy is derived from the records too
     return VR_OK;
 }
 

@@ -27,6 +27,8 @@ constexpr uint32_t kPad = 0xFFFFFFFFu;     // tile-list padding
 struct Params {
     float m[12];                 // c_invViewMatrix (K:116), row-major 3x4
     uint32_t W, H;
+    uint32_t CW, CH;             // pixels rendered: x < CW, y < CH (render_kernel's grid
+                                 // coverage, C:122 / K:2397; W, H otherwise)
     float density, brightness, toff, tscale;
     int nx, ny, nz;              // resident volume dims
     uint64_t sy, sz;             // record pitch of a voxel row / slice in HBM
@@ -59,7 +61,6 @@ struct Params {
     int ntpl, err_slots;
     int tpl_lds;                 // codec march: template table copied to LDS (bytes, 0 = no)
     int seg_lanes;               // ray-segmented march (path 7): lanes per ray
-    int hyb_tiles;               // hybrid march (path 9): leading slots ray-segmented
     // flexible blocks (methods 8/9/0): per-block (mean, variance, entropy, 0)
     const float4 *flex;
     int nflex;                   // blocks per axis

@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void k_march_flex(Params P) {
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;
+    if (x >= P.CW || y >= P.CH) return;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;

@@ -125,7 +125,7 @@ __device__ __forceinline__ bool gmm_begin(const Params &P, uint32_t wave_base, u
     } else {
         x = row_x0 + e;
         y = row_y;
-        if (x >= P.W || y >= P.H) return false;
+        if (x >= P.CW || y >= P.CH) return false;
         s.pix = y * P.W + x;
     }
     if (!make_ray(P, x, y, s.r)) {

@@ -34,12 +34,9 @@ void note_kernel(const char *kind, int B, int method);
 // specialisation
 bool launch_march_seg(int nb, int method, int S, const float *vol, const Params &P,
                       uint32_t nslots, hipStream_t s, hipError_t &err);
-// hybrid: the first P.hyb_tiles slots ray-segmented (S lanes), the rest pipelined
-bool launch_march_hyb(int nb, int method, int S, const float *vol, const Params &P,
-                      uint32_t nslots, hipStream_t s, hipError_t &err);
-#ifdef VR_WG_PROF
-hipError_t wg_prof_read(unsigned long long *host);   // tooling build only
-#endif
+// tuning knob `key` set through vr_set_tuning (nullptr if unset); a -DVR_TUNING
+// build falls back to the environment.  The default build never reads it.
+const char *tuning(const char *key);
 hipError_t launch_march_codec(int nb, int method, const Params &P, uint32_t nslots, bool count,
                               hipStream_t s);
 hipError_t launch_codec_bytes(const unsigned long long *bits, uint64_t nvox, const int4 *cb,

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
+    const bool valid = x < P.CW && y < P.CH;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     // every lane stays to the end: the staged decode needs all 64 lanes
@@ -304,29 +304,6 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
                 sw * P.brightness);
 }
 
-// ---- workgroup-staged march (B <= 8) ----
-// The 256 rays of a tile march in lockstep.  Each step the workgroup builds the
-// exact set of voxel records its live rays' trilinear footprints touch, as
-// x-spans of (y,z) voxel rows: every lane min/max-es its x0/x1 into a row
-// table in LDS (4 rows per lane), the non-empty rows are compacted with a
-// workgroup scan, then 8-lane groups stream the rows from HBM (consecutive
-// lanes on consecutive records), decode each record's statistic ONCE and park
-// it in LDS.  Finally every lane blends its 8 corners from LDS.  Compared with
-// per-lane gathers this loads each record once per tile-step instead of once
-// per touching ray, and keeps the texture-address unit on a few lines per
-// instruction.  A step whose row table or record set does not fit falls back to
-// per-lane gathers (workgroup-uniform).
-constexpr int kWgTbl = 1024;   // (y,z) row-table entries (Y*Z <= kWgTbl)
-#ifdef VR_WG_PROF   // tooling build: per-phase cycle totals of thread 0 (tools/wg_prof.py)
-__device__ unsigned long long g_wg_prof[16];
-#define WG_PROF_T(k) if (tid == 0) { const uint64_t now_ = clock64(); prof_[k] += now_ - tlast_; tlast_ = now_; }
-#define WG_PROF_C(k, v) if (tid == 0) prof_[k] += (uint64_t)(v);
-#else
-#define WG_PROF_T(k)
-#define WG_PROF_C(k, v)
-#endif
-constexpr int kWgRec = 4096;   // staged record statistics per step (< 2^12)
-
 __device__ __forceinline__ int wave_incl_scan(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
@@ -337,232 +314,10 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
-template <int B, int M>
-__global__ __launch_bounds__(256) void k_march_wg(const float *__restrict__ vol, Params P) {
-    __shared__ int s_xmn[kWgTbl], s_xmx[kWgTbl], s_toff[kWgTbl];
-    __shared__ uint2 s_rows[kWgTbl];   // x: ry | rz << 10 | loff << 20,  y: xmin | len << 16
-    __shared__ float s_stat[kWgRec];
-    __shared__ int s_red[4][6];
-    const uint32_t slot = launch_slot(P);
-    const uint32_t tile = tile_of(P, slot);
-    if (tile == kPad) return;  // whole workgroup uniform
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    for (uint32_t e = tid; e < (uint32_t)kWgTbl; e += 256) {
-        s_xmn[e] = 0x7FFFFFFF;
-        s_xmx[e] = -1;
-    }
-    uint32_t lx, ly;
-    tile_pixel(tid, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
-                                   : (uint64_t)y * P.W + x;
-    Ray r;
-    bool alive = valid && make_ray(P, x, y, r);
-    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
-    float t = r.tnear;
-    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
-    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
-    int n = 0;
-    const uint32_t grp = tid >> 3, gl = tid & 7u;
-#ifdef VR_WG_PROF
-    uint64_t prof_[16] = {0};
-    uint64_t tlast_ = clock64();
-#endif
-    for (int i = 0; i < kMaxSteps; i++) {
-        Foot f = {0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0.0f};
-        if (alive) f = footprint(P, px, py, pz);
-        {   // workgroup extent of the live footprints in y and z
-            const int a = wave_min(alive ? f.y0 : 0x7FFFFFFF);
-            const int b = wave_max(alive ? f.y1 : -1);
-            const int c = wave_min(alive ? f.z0 : 0x7FFFFFFF);
-            const int d = wave_max(alive ? f.z1 : -1);
-            if (lane == 0) {
-                s_red[wave][0] = a; s_red[wave][1] = b; s_red[wave][2] = c; s_red[wave][3] = d;
-            }
-        }
-        WG_PROF_T(0)
-        __syncthreads();
-        WG_PROF_T(1)
-        int ymn = s_red[0][0], ymx = s_red[0][1], zmn = s_red[0][2], zmx = s_red[0][3];
-#pragma unroll
-        for (int w = 1; w < 4; w++) {
-            ymn = min(ymn, s_red[w][0]); ymx = max(ymx, s_red[w][1]);
-            zmn = min(zmn, s_red[w][2]); zmx = max(zmx, s_red[w][3]);
-        }
-        if (ymx < 0) break;  // no live ray in the tile
-        const int Y = ymx - ymn + 1, E = Y * (zmx - zmn + 1);
-        bool staged = E <= kWgTbl;
-        float sample = 0.0f;
-        WG_PROF_C(11, 1)
-        if (staged) {
-            const int e00 = (f.y0 - ymn) + Y * (f.z0 - zmn);
-            const int e10 = e00 + (f.y1 - f.y0), e01 = e00 + Y * (f.z1 - f.z0);
-            const int e11 = e01 + (f.y1 - f.y0);
-            if (alive) {
-                atomicMin(&s_xmn[e00], f.x0); atomicMax(&s_xmx[e00], f.x1);
-                atomicMin(&s_xmn[e10], f.x0); atomicMax(&s_xmx[e10], f.x1);
-                atomicMin(&s_xmn[e01], f.x0); atomicMax(&s_xmx[e01], f.x1);
-                atomicMin(&s_xmn[e11], f.x0); atomicMax(&s_xmx[e11], f.x1);
-            }
-            WG_PROF_T(2)
-            __syncthreads();
-            WG_PROF_T(3)
-            // compaction: thread t owns table entries 4t .. 4t+3
-            int mn[4], ln[4], cnt = 0, rec = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int e = 4 * (int)tid + j;
-                ln[j] = 0;
-                mn[j] = 0;
-                if (e < E) {
-                    const int a = s_xmn[e], b = s_xmx[e];
-                    if (b >= a) { mn[j] = a; ln[j] = b - a + 1; cnt++; rec += ln[j]; }
-                    s_xmn[e] = 0x7FFFFFFF;
-                    s_xmx[e] = -1;
-                }
-            }
-            const int icnt = wave_incl_scan(cnt), irec = wave_incl_scan(rec);
-            if (lane == 63) { s_red[wave][4] = icnt; s_red[wave][5] = irec; }
-            WG_PROF_T(4)
-            __syncthreads();
-            WG_PROF_T(5)
-            int rows = 0, recs = 0, rbase = icnt - cnt, obase = irec - rec;
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const int c = s_red[w][4], d = s_red[w][5];
-                if (w < (int)wave) { rbase += c; obase += d; }
-                rows += c;
-                recs += d;
-            }
-            staged = recs <= kWgRec;
-            if (staged) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    if (ln[j] > 0) {
-                        const int e = 4 * (int)tid + j;
-                        const int rz = e / Y, ry = e - rz * Y;
-                        s_rows[rbase] = make_uint2((uint32_t)ry | ((uint32_t)rz << 10) |
-                                                       ((uint32_t)obase << 20),
-                                                   (uint32_t)mn[j] | ((uint32_t)ln[j] << 16));
-                        s_toff[e] = obase - mn[j];
-                        rbase++;
-                        obase += ln[j];
-                    }
-                }
-                WG_PROF_C(12, 1)
-                WG_PROF_C(13, rows)
-                WG_PROF_C(14, recs)
-            }
-            WG_PROF_T(6)
-            __syncthreads();
-            WG_PROF_T(7)
-            if (staged) {
-                // 8-lane group grp streams rows grp, grp+32, ...; lane gl takes
-                // records gl, gl+8, ... of each row.  4 records in flight per lane.
-                int k = (int)grp, nn = (int)gl;
-                uint64_t gb = 0;
-                int lo = 0, len = 0;
-                if (k < rows) {
-                    const uint2 rw = s_rows[k];
-                    gb = (uint64_t)(zmn + (int)((rw.x >> 10) & 1023u)) * P.sz +
-                         (uint64_t)(ymn + (int)(rw.x & 1023u)) * P.sy + (rw.y & 0xFFFFu);
-                    lo = (int)(rw.x >> 20);
-                    len = (int)(rw.y >> 16);
-                }
-                while (k < rows) {
-                    uint64_t ga[4];
-                    int li[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        while (k < rows && nn >= len) {
-                            k += 32;
-                            nn = (int)gl;
-                            if (k < rows) {
-                                const uint2 rw = s_rows[k];
-                                gb = (uint64_t)(zmn + (int)((rw.x >> 10) & 1023u)) * P.sz +
-                                     (uint64_t)(ymn + (int)(rw.x & 1023u)) * P.sy +
-                                     (rw.y & 0xFFFFu);
-                                lo = (int)(rw.x >> 20);
-                                len = (int)(rw.y >> 16);
-                            }
-                        }
-                        if (k < rows) {
-                            ga[u] = gb + (uint64_t)nn;
-                            li[u] = lo + nn;
-                            nn += 8;
-                        } else {
-                            ga[u] = 0;
-                            li[u] = -1;
-                        }
-                    }
-                    float rr[4][B];
-                    WG_PROF_C(15, 1)
-#pragma unroll
-                    for (int u = 0; u < 4; u++) load_rec<B>(vol, ga[u], rr[u]);
-#pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (li[u] >= 0) s_stat[li[u]] = record_stat<B, M>(rr[u], P.enorm);
-                }
-            }
-            WG_PROF_T(8)
-            __syncthreads();
-            WG_PROF_T(9)
-            if (staged && alive) {
-                const int t00 = s_toff[e00], t10 = s_toff[e10];
-                const int t01 = s_toff[e01], t11 = s_toff[e11];
-                float sv[8];
-                sv[0] = s_stat[t00 + f.x0]; sv[1] = s_stat[t00 + f.x1];
-                sv[2] = s_stat[t10 + f.x0]; sv[3] = s_stat[t10 + f.x1];
-                sv[4] = s_stat[t01 + f.x0]; sv[5] = s_stat[t01 + f.x1];
-                sv[6] = s_stat[t11 + f.x0]; sv[7] = s_stat[t11 + f.x1];
-                sample = blend8(sv, f);
-            }
-        }
-        if (alive) {
-            if (!staged) sample = sample_direct<B, M>(vol, P, f);
-            n = i + 1;
-            if (composite(P, sample, sx, sy, sz, sw)) {
-                alive = false;
-            } else {
-                t = t + kTStep;
-                if (t > r.tfar) {
-                    alive = false;
-                } else {
-                    px = px + stx;
-                    py = py + sty;
-                    pz = pz + stz;
-                }
-            }
-        }
-        WG_PROF_T(10)
-    }
-#ifdef VR_WG_PROF
-    if (tid == 0)
-        for (int k = 0; k < 16; k++) atomicAdd(&g_wg_prof[k], prof_[k]);
-#endif
-    if (!valid) return;
-    if (n == 0) {  // miss (K:302-303): nothing written
-        write_miss(P, o);
-        return;
-    }
-    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
-                sw * P.brightness);
-}
-
-#ifdef VR_WG_PROF
-hipError_t wg_prof_read(unsigned long long *host) {
-    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_prof), sizeof(g_wg_prof));
-    if (e != hipSuccess) return e;
-    static const unsigned long long zero[16] = {0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_wg_prof), zero, sizeof(zero));
-}
-#endif
-
 // ---- wave-staged march (B <= 8) ----
-// The same exact-footprint staging as k_march_wg, but per wave (8x8 rays) and
-// wave-synchronous: no workgroup barriers, so the 16-20 resident waves of a CU
+// Exact-footprint staging per wave (8x8 rays), wave-synchronous: no workgroup
+// barriers (a workgroup-wide version with 5 barriers per step was latency-bound,
+// DESIGN.md 4.3), so the 16-20 resident waves of a CU
 // hide each other's HBM latency.  Per step: (y,z) row table by LDS atomics,
 // compaction by DPP scans, row-start marks + a max-scan give every lane its
 // (row, x) for consecutive records, so consecutive lanes load consecutive
@@ -623,7 +378,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
     tile_pixel(tid, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
+    const bool valid = x < P.CW && y < P.CH;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -633,10 +388,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
     float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
     const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
     int n = 0;
-#ifdef VR_WG_PROF
-    uint64_t prof_[16] = {0};
-    uint64_t tlast_ = clock64();
-#endif
     for (int i = 0; i < kMaxSteps; i++) {
         if (!wave_any(alive)) break;
         Foot f = {0, 0, 0, 0, 0, 0, 0.0f, 0.0f, 0.0f};
@@ -648,9 +399,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
         const int Y = ymx - ymn + 1, E = Y * (zmx - zmn + 1);
         bool staged = E <= kWsTbl;
         float sample = 0.0f;
-        WG_PROF_C(11, 1)
-        WG_PROF_C(6, E > kWsTbl)
-        WG_PROF_T(0)
         if (staged) {
             const int e00 = (f.y0 - ymn) + Y * (f.z0 - zmn);
             const int e10 = e00 + (f.y1 - f.y0), e01 = e00 + Y * (f.z1 - f.z0);
@@ -662,7 +410,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                 atomicMin(&xmn[e11], f.x0); atomicMax(&xmx[e11], f.x1);
             }
             wave_sync();
-            WG_PROF_T(2)
             // compaction: lane owns table entries 4*lane .. 4*lane+3 (and resets them)
             int mn[4], ln[4], cnt = 0, rec = 0;
 #pragma unroll
@@ -681,13 +428,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
             const int rows = __builtin_amdgcn_readlane(icnt, 63);
             const int R = __builtin_amdgcn_readlane(irec, 63);
             staged = rows <= kWsRows && R <= kWsRec;
-            WG_PROF_C(7, rows > kWsRows)
-            WG_PROF_C(8, R > kWsRec)
-            WG_PROF_T(4)
             if (staged) {
-                WG_PROF_C(12, 1)
-                WG_PROF_C(13, rows)
-                WG_PROF_C(14, R)
                 // row-start marks carry the step as a tag: stale marks never match
                 const float rY = 1.0f / (float)Y;
                 int rb = icnt - cnt, ob = irec - rec;
@@ -706,7 +447,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                     }
                 }
                 wave_sync();
-                WG_PROF_T(5)
                 // consecutive lanes on consecutive records; U x 64 records in flight
                 // (fewer for the register-hungry entropy decode)
                 constexpr int U = M == 3 ? VR_WS_U3 : 4;
@@ -714,7 +454,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                 for (int q0 = 0; q0 < R; q0 += 64 * U) {
                     float rr[U][B];
                     int li[U];
-                    WG_PROF_C(15, 1)
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         const int q = q0 + 64 * u + (int)lane;
@@ -744,7 +483,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                         if (li[u] >= 0) stat[li[u]] = record_stat_p<B, M>(rr[u], P.enorm, s_lt);
                 }
                 wave_sync();
-                WG_PROF_T(9)
                 if (alive) {
                     const int t00 = toff[e00], t10 = toff[e10];
                     const int t01 = toff[e01], t11 = toff[e11];
@@ -774,12 +512,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                 }
             }
         }
-        WG_PROF_T(10)
     }
-#ifdef VR_WG_PROF
-    if (tid == 0)
-        for (int k = 0; k < 16; k++) atomicAdd(&g_wg_prof[k], prof_[k]);
-#endif
     if (!valid) return;
     if (n == 0) {  // miss (K:302-303): nothing written
         write_miss(P, o);
@@ -815,130 +548,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_PIPE_WAV
         w[1] = wall_clock64();
         w[2] = __smid();  // XCC id in the high bits on gfx94x/gfx950
     }
-}
-
-// ---- neighbour-shared per-ray march (B % 4 == 0, row-aligned views) ----
-// A wave is one 64-pixel row.  When the screen x axis runs along the voxel
-// rows, a lane's x1 corner is usually its right neighbour's x0 corner, so each
-// lane gathers only its 4 x0 records and takes the 4 x1 records from lane + 1
-// with a DPP wave shift; lanes whose neighbour is not adjacent in HBM (gaps,
-// other rows, lane 63) gather their x1 record themselves, in instructions that
-// touch only a few lines.  Half the full-width gathers of k_march_pipe, same
-// registers, same two-step pipeline; the loop is wave-uniform so the DPP
-// always reads live lanes.
-__device__ __forceinline__ uint32_t wave_shl1(uint32_t v, uint32_t edge) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x130, 0xF, 0xF, false);
-}
-
-template <int B>
-struct PairStep {
-    float lo[4][B];   // x0 record of each (y, z) corner row
-    float hi[4][B];   // x1 record where gathered (fix lanes)
-    uint32_t fix;     // bit c: x1 of row c gathered by this lane
-    uint32_t same;    // bit c: x1 == x0 (clamped edge)
-};
-
-template <int B>
-__device__ __forceinline__ void gather_pair(const float *__restrict__ vol, const Params &P,
-                                            const Foot &f, bool act, PairStep<B> &st) {
-    const uint64_t rows[4] = {(uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy,
-                              (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy,
-                              (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy,
-                              (uint64_t)f.z1 * P.sz + (uint64_t)f.y1 * P.sy};
-    st.fix = 0;
-    st.same = f.x1 == f.x0 ? 0xFu : 0u;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        const uint64_t i0 = rows[c] + (uint64_t)f.x0, i1 = rows[c] + (uint64_t)f.x1;
-        if (act) load_rec<B>(vol, i0, st.lo[c]);
-        // the right neighbour's x0 index (lane 63 and dead lanes: no match)
-        const uint64_t mine = act ? i0 : ~0ull;
-        const uint32_t nlo = wave_shl1((uint32_t)mine, 0xFFFFFFFFu);
-        const uint32_t nhi = wave_shl1((uint32_t)(mine >> 32), 0xFFFFFFFFu);
-        const bool need = act && f.x1 != f.x0 && (nlo != (uint32_t)i1 || nhi != (uint32_t)(i1 >> 32));
-        if (need) {
-            load_rec<B>(vol, i1, st.hi[c]);
-            st.fix |= 1u << c;
-        }
-    }
-}
-
-template <int B, int M>
-__device__ __forceinline__ float decode_pair(const Params &P, const PairStep<B> &st,
-                                             const Foot &f) {
-    float s[8];
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        float x1[B];
-#pragma unroll
-        for (int k = 0; k < B; k++) {  // all lanes execute the shift
-            const float nb = __uint_as_float(wave_shl1(__float_as_uint(st.lo[c][k]), 0u));
-            x1[k] = (st.same >> c) & 1u ? st.lo[c][k] : ((st.fix >> c) & 1u ? st.hi[c][k] : nb);
-        }
-        s[2 * c] = record_stat<B, M>(st.lo[c], P.enorm);
-        s[2 * c + 1] = record_stat<B, M>(x1, P.enorm);
-    }
-    return blend8(s, f);
-}
-
-template <int B, int M>
-__global__ __launch_bounds__(256) void k_march_pair(const float *__restrict__ vol, Params P) {
-    const uint32_t slot = launch_slot(P);
-    const uint32_t tile = tile_of(P, slot);
-    if (tile == kPad) return;
-    uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
-                                   : (uint64_t)y * P.W + x;
-    Ray r;
-    bool alive = valid && make_ray(P, x, y, r);
-    if (!alive) {
-        r.ox = r.oy = r.oz = r.dx = r.dy = r.dz = 0.0f;
-        r.tnear = r.tfar = 0.0f;
-    }
-    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
-    float t = r.tnear;
-    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
-    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
-    int n = 0;
-    Foot fa = footprint(P, px, py, pz), fb = fa;
-    PairStep<B> a, b;
-    gather_pair<B>(vol, P, fa, alive, a);
-    auto step = [&](int i, const Foot &fc, const PairStep<B> &sc, Foot &fn, PairStep<B> &sn) {
-        const float tn = t + kTStep;                                        // K:701
-        const bool cont = alive && !(tn > r.tfar) && (i + 1 < kMaxSteps);   // K:703, K:381
-        const float nx = px + stx, ny = py + sty, nz = pz + stz;            // K:706
-        fn = footprint(P, nx, ny, nz);
-        gather_pair<B>(vol, P, fn, cont, sn);
-        const float sample = decode_pair<B, M>(P, sc, fc);  // wave-wide (DPP)
-        if (alive) {
-            n = i + 1;
-            if (composite(P, sample, sx, sy, sz, sw) || !cont) {
-                alive = false;
-            } else {
-                t = tn;
-                px = nx;
-                py = ny;
-                pz = nz;
-            }
-        }
-    };
-    for (int i = 0; i < kMaxSteps; i += 2) {
-        if (!wave_any(alive)) break;
-        step(i, fa, a, fb, b);
-        if (!wave_any(alive)) break;
-        step(i + 1, fb, b, fa, a);
-    }
-    if (!valid) return;
-    if (n == 0) {
-        write_miss(P, o);
-        return;
-    }
-    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
-                sw * P.brightness);
 }
 
 // ---- wide records (B = 16, 32: the reference's own 32-bin histograms) ----
@@ -981,7 +590,7 @@ __device__ __forceinline__ int march_wide_tile(const float *__restrict__ vol, co
     tile_pixel(tid, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return -1;  // no cross-lane work in this kernel
+    if (x >= P.CW || y >= P.CH) return -1;  // no cross-lane work in this kernel
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -1045,81 +654,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MIN
     if (tile == kPad) return;
     const int n = march_wide_tile<B, M>(vol, P, slot, tile, threadIdx.x, nullptr);
     if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
-}
-
-// ---- half-step pipelined per-ray march (B <= 8) ----
-// k_march_pipe keeps a whole step of corner records in flight while the
-// previous step decodes (2 x 8 records per lane: 238 VGPRs at B = 8, two
-// waves per SIMD).  Here the next step's gathers are issued one half at a
-// time, each half into the registers whose records were just decoded, so at
-// most 8 records per lane are live: half the registers, twice the waves per
-// CU, and a ray's dependent step chain still overlaps half a step of loads.
-template <int B>
-__device__ __forceinline__ void gather4(const float *__restrict__ vol, const Params &P,
-                                        const Foot &f, int zsel, float (&rec)[4][B]) {
-    const uint64_t z = zsel ? (uint64_t)f.z1 : (uint64_t)f.z0;
-    const uint64_t r0 = z * P.sz + (uint64_t)f.y0 * P.sy;
-    const uint64_t r1 = z * P.sz + (uint64_t)f.y1 * P.sy;
-    load_rec<B>(vol, r0 + f.x0, rec[0]);
-    load_rec<B>(vol, r0 + f.x1, rec[1]);
-    load_rec<B>(vol, r1 + f.x0, rec[2]);
-    load_rec<B>(vol, r1 + f.x1, rec[3]);
-}
-
-#ifndef VR_HALF_WAVES
-#define VR_HALF_WAVES 4     // waves per SIMD the half-step march is register-capped for
-#endif
-
-template <int B, int M>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_HALF_WAVES, 8))) void k_march_half(const float *__restrict__ vol, Params P) {
-    const uint32_t slot = launch_slot(P);
-    const uint32_t tile = tile_of(P, slot);
-    if (tile == kPad) return;
-    uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
-    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
-    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;  // no cross-lane work in this kernel
-    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
-                                   : (uint64_t)y * P.W + x;
-    Ray r;
-    if (!make_ray(P, x, y, r)) {
-        write_miss(P, o);
-        return;
-    }
-    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
-    float t = r.tnear;
-    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
-    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
-    int n = 0;
-    Foot fc = footprint(P, px, py, pz);
-    float lo[4][B], hi[4][B];  // z0 and z1 corner records of the current step
-    gather4<B>(vol, P, fc, 0, lo);
-    gather4<B>(vol, P, fc, 1, hi);
-    for (int i = 0; i < kMaxSteps; i++) {
-        const float tn = t + kTStep;                               // K:701
-        const bool cont = !(tn > r.tfar) && (i + 1 < kMaxSteps);  // K:703, K:381
-        const float nx = px + stx, ny = py + sty, nz = pz + stz;   // K:706
-        Foot fn = fc;
-        if (cont) fn = footprint(P, nx, ny, nz);
-        float sv[8];
-#pragma unroll
-        for (int j = 0; j < 4; j++) sv[j] = record_stat<B, M>(lo[j], P.enorm);
-        if (cont) gather4<B>(vol, P, fn, 0, lo);
-#pragma unroll
-        for (int j = 0; j < 4; j++) sv[4 + j] = record_stat<B, M>(hi[j], P.enorm);
-        if (cont) gather4<B>(vol, P, fn, 1, hi);
-        const float sample = blend8(sv, fc);
-        n = i + 1;
-        if (composite(P, sample, sx, sy, sz, sw) || !cont) break;
-        t = tn;
-        px = nx;
-        py = ny;
-        pz = nz;
-        fc = fn;
-    }
-    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
-                sw * P.brightness);
 }
 
 #ifndef VR_QUAD_MAP
@@ -1273,7 +807,7 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
     }
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
+    const bool valid = x < P.CW && y < P.CH;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     const uint32_t g = tid & 3u;
@@ -1455,7 +989,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
 #endif
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
+    const bool valid = x < P.CW && y < P.CH;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     // every lane stays to the end: quads cooperate on each other's rays
@@ -1634,7 +1168,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
     const uint32_t lx = wave * 16u + q, ly = g;  // 16x4 block per wave, quad = a column
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
+    const bool valid = x < P.CW && y < P.CH;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -1800,7 +1334,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PI
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;
+    if (x >= P.CW || y >= P.CH) return;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -1949,7 +1483,7 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;
+    if (x >= P.CW || y >= P.CH) return;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -2113,7 +1647,7 @@ __global__ __launch_bounds__(256) void k_march_codec_quad(const float *__restric
     const uint32_t lx = wave * 16u + q, ly = g;  // 16x4 block per wave, quad = a column
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
+    const bool valid = x < P.CW && y < P.CH;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     // every lane stays to the end: quads cooperate on each other's rays
@@ -2182,7 +1716,7 @@ static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream
     const bool tl = P.tpl_lds != 0;
     if constexpr (B == 8 && !COUNT) {
         // oblique views: the quad-cooperative codec march (VR_CODEC_QUAD=0 disables)
-        const char *eq = std::getenv("VR_CODEC_QUAD");
+        const char *eq = tuning("VR_CODEC_QUAD");
         if (P.oblique && !(eq && std::atoi(eq) == 0)) {
             note_kernel("k_march_codec_quad", B, method);
             switch (method * 2 + (tl ? 1 : 0)) {
@@ -2282,7 +1816,7 @@ __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol,
     tile_pixel(threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;
+    if (x >= P.CW || y >= P.CH) return;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -2418,7 +1952,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MIN
     }
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    const bool valid = x < P.W && y < P.H;
+    const bool valid = x < P.CW && y < P.CH;
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     const uint32_t g = threadIdx.x & 3u;
@@ -2652,11 +2186,6 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             if (launch_march_seg(B, method, P.seg_lanes, vol, P, nslots, s, err)) return err;
             P.path = 2;
         }
-        if (P.path == 9) {
-            hipError_t err = hipSuccess;
-            if (launch_march_hyb(B, method, P.seg_lanes, vol, P, nslots, s, err)) return err;
-            P.path = 2;
-        }
         if (B == 8 && P.path == 0 && method >= 1 && method <= 3) {
             note_kernel(P.bvol ? "k_march_quad_brick" : "k_march_quad", B, method);
             // The quad march uses no LDS; an LDS request caps it at 2 workgroups
@@ -2685,35 +2214,6 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
                 case 2: hipLaunchKernelGGL((k_march_quad<2, false>), grid, block, qlds, s, vol, P); break;
                 case 3: hipLaunchKernelGGL((k_march_quad<3, false>), grid, block, qlds, s, vol, P); break;
                 }
-            }
-            return hipGetLastError();
-        }
-        if (P.path == 3 && method >= 1 && method <= 3) {
-            note_kernel("k_march_wg", B, method);
-            switch (method) {
-            case 1: hipLaunchKernelGGL((k_march_wg<B, 1>), grid, block, 0, s, vol, P); break;
-            case 2: hipLaunchKernelGGL((k_march_wg<B, 2>), grid, block, 0, s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_wg<B, 3>), grid, block, 0, s, vol, P); break;
-            }
-            return hipGetLastError();
-        }
-        if constexpr (B % 4 == 0) {
-            if (P.path == 6 && method >= 1 && method <= 3) {
-                note_kernel("k_march_pair", B, method);
-                switch (method) {
-                case 1: hipLaunchKernelGGL((k_march_pair<B, 1>), grid, block, 0, s, vol, P); break;
-                case 2: hipLaunchKernelGGL((k_march_pair<B, 2>), grid, block, 0, s, vol, P); break;
-                case 3: hipLaunchKernelGGL((k_march_pair<B, 3>), grid, block, 0, s, vol, P); break;
-                }
-                return hipGetLastError();
-            }
-        }
-        if (P.path == 5 && method >= 1 && method <= 3) {
-            note_kernel("k_march_half", B, method);
-            switch (method) {
-            case 1: hipLaunchKernelGGL((k_march_half<B, 1>), grid, block, 0, s, vol, P); break;
-            case 2: hipLaunchKernelGGL((k_march_half<B, 2>), grid, block, 0, s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_half<B, 3>), grid, block, 0, s, vol, P); break;
             }
             return hipGetLastError();
         }
@@ -2763,7 +2263,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         if (P.path != 1 && (method == 1 || method == 2 || (method == 3 && WQ3))) {
             const size_t wl = occupancy_lds(P);
             int kind = (B == 16 && !P.oblique && method != 3) ? 1 : 2;
-            if (const char *ew = std::getenv("VR_WIDE")) {
+            if (const char *ew = tuning("VR_WIDE")) {
                 const int v = std::atoi(ew);
                 if (v == 1 || v == 2) kind = v;
             }
@@ -2772,7 +2272,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // 64-pixel row per wave: 1024^3 x 32 C1 12.44 -> 11.77 ms, C0 6.64 -> 6.56,
             // 1024^3 x 16 C1 6.78 -> 6.65 (profiles/r02/wide_records.log); VR_WQ_MAP=0: rows
             P.wq_map = 1;
-            if (const char *em = std::getenv("VR_WQ_MAP")) P.wq_map = std::atoi(em) != 0;
+            if (const char *em = tuning("VR_WQ_MAP")) P.wq_map = std::atoi(em) != 0;
             if (kind == 1) {
                 note_kernel("k_march_wide", B, method);
                 if (method == 1)
@@ -2805,7 +2305,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // k_march_m7_pipe, VR_M7_PIPE=1, only adds loads), 4 workgroups per CU
             // on row-aligned views, 2 on oblique ones (1024^3 C0 0.68 -> 0.64 ms,
             // C1 2.03 -> 1.67; profiles/r02/baked_m7.log)
-            const char *ep = std::getenv("VR_M7_PIPE");
+            const char *ep = tuning("VR_M7_PIPE");
             const size_t lds =
                 cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : (P.oblique ? 2 : 4));
             if (ep && std::atoi(ep) != 0) {
@@ -2828,7 +2328,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         if constexpr (B == 8) {
             // oblique views with the method-7 grid equal to the volume: the
             // quad-cooperative march (VR_M7_QUAD=0 disables), 2 workgroups per CU
-            const char *eq = std::getenv("VR_M7_QUAD");
+            const char *eq = tuning("VR_M7_QUAD");
             const bool quad = !(eq && std::atoi(eq) == 0);
             if (quad && P.oblique && P.m7x == P.nx && P.m7y == P.ny && P.m7z == P.nz) {
                 const size_t qlds = cap_lds(P, P.wg_per_cu > 0 ? P.wg_per_cu : 2);
@@ -2847,19 +2347,19 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         }
         if constexpr (B == 16 || B == 32) {
             // wide records: quad-cooperative refreshes (VR_M7_WQ=0: k_march_m7)
-            const char *eq = std::getenv("VR_M7_WQ");
+            const char *eq = tuning("VR_M7_WQ");
             if (!(eq && std::atoi(eq) == 0)) {
                 note_kernel("k_march_m7wq", B, method);
                 Params Q = P;
                 Q.wq_map = M7_WQ_MAP;
-                if (const char *em = std::getenv("VR_WQ_MAP")) Q.wq_map = std::atoi(em) != 0;
+                if (const char *em = tuning("VR_WQ_MAP")) Q.wq_map = std::atoi(em) != 0;
                 hipLaunchKernelGGL((k_march_m7wq<B>), grid, block, occupancy_lds(P), s, vol, Q);
                 break;
             }
         }
         if constexpr (B > 0 && B <= 8) {
             // pipelined corner gathers (VR_M7_PIPE=0: the plain march)
-            const char *ep = std::getenv("VR_M7_PIPE");
+            const char *ep = tuning("VR_M7_PIPE");
             const bool pipe = !(ep && std::atoi(ep) == 0);
             if (pipe) {
                 // oblique views at 2 workgroups per CU (1024^3x8 C1: 8.53 -> 7.45 ms;

@@ -234,7 +234,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
     tile_pixel(tid, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return -1;  // no cross-lane work in this kernel
+    if (x >= P.CW || y >= P.CH) return -1;  // no cross-lane work in this kernel
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;

@@ -82,7 +82,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
     const uint32_t lx = p % kTileW, ly = p / kTileW;
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
-    if (x >= P.W || y >= P.H) return;  // the whole group leaves
+    if (x >= P.CW || y >= P.CH) return;  // the whole group leaves
     const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
                                    : (uint64_t)y * P.W + x;
     Ray r;
@@ -178,82 +178,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVE
     march_seg_part<B, M, S, PIPE>(vol, P, (b & 7u) + 8u * (b / (8u * S)), (b >> 3) % S);
 }
 
-// Hybrid launch for tile lists ordered longest-first (multi-GPU ranks): the
-// first P.hyb_tiles slots (a multiple of 8) are ray-segmented (S lanes per
-// ray, workgroups 0 .. hyb_tiles*S-1, mapped as in k_march_seg), the rest run
-// the one-lane pipelined march (workgroup hyb_tiles*S + i -> slot hyb_tiles + i,
-// same XCD as slot % 8).  At a rank's share of a frame the longest rays'
-// step chains, slowed by the whole launch's memory traffic, set the frame
-// time (tools/wave_timeline.py); splitting only those rays over S lanes
-// shortens the critical chains without paying the segmented march's overhead
-// on every ray.
-template <int B, int M, int S>
-__global__ __launch_bounds__(256) void k_march_hyb(const float *__restrict__ vol, Params P) {
-    const uint32_t b = blockIdx.x;
-    const uint32_t nseg = (uint32_t)P.hyb_tiles * S;
-    if (b < nseg) {
-        march_seg_part<B, M, S, false>(vol, P, (b & 7u) + 8u * (b / (8u * S)), (b >> 3) % S);
-        return;
-    }
-    const uint32_t slot = (uint32_t)P.hyb_tiles + (b - nseg);
-    const uint32_t tile = tile_of(P, slot);
-    if (tile == kPad) return;
-    unsigned long long t0 = 0;
-    if (P.wave_clock) t0 = wall_clock64();
-    const int n = march_pipe_tile<B, M>(vol, P, slot, tile, threadIdx.x);
-    if (P.tile_cost) record_tile_cost(P, tile, n);
-    if (P.wave_clock && (threadIdx.x & 63) == 0) {
-        unsigned long long *w = P.wave_clock + ((uint64_t)slot * 4u + threadIdx.x / 64u) * 3u;
-        w[0] = t0;
-        w[1] = wall_clock64();
-        w[2] = __smid();
-    }
-}
-
-template <int B, int S>
-static hipError_t hyb_launch(int method, const float *vol, const Params &P, uint32_t nslots,
-                             hipStream_t s) {
-    const dim3 grid((uint32_t)P.hyb_tiles * S + (nslots - (uint32_t)P.hyb_tiles)), block(256);
-    switch (method) {
-    case 1: hipLaunchKernelGGL((k_march_hyb<B, 1, S>), grid, block, 0, s, vol, P); break;
-    case 2: hipLaunchKernelGGL((k_march_hyb<B, 2, S>), grid, block, 0, s, vol, P); break;
-    case 3: hipLaunchKernelGGL((k_march_hyb<B, 3, S>), grid, block, 0, s, vol, P); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template <int B>
-static bool hyb_b(int method, int S, const float *vol, const Params &P, uint32_t nslots,
-                  hipStream_t s, hipError_t &err) {
-    switch (S) {
-    case 2: err = hyb_launch<B, 2>(method, vol, P, nslots, s); return true;
-    case 4: err = hyb_launch<B, 4>(method, vol, P, nslots, s); return true;
-    case 8: err = hyb_launch<B, 8>(method, vol, P, nslots, s); return true;
-    default: return false;
-    }
-}
-
-bool launch_march_hyb(int nb, int method, int S, const float *vol, const Params &P,
-                      uint32_t nslots, hipStream_t s, hipError_t &err) {
-    if (method < 1 || method > 3 || P.hyb_tiles % 8 != 0 || (uint32_t)P.hyb_tiles > nslots)
-        return false;
-    bool ok = false;
-    switch (nb) {
-    case 1: ok = hyb_b<1>(method, S, vol, P, nslots, s, err); break;
-    case 2: ok = hyb_b<2>(method, S, vol, P, nslots, s, err); break;
-    case 4: ok = hyb_b<4>(method, S, vol, P, nslots, s, err); break;
-    case 8: ok = hyb_b<8>(method, S, vol, P, nslots, s, err); break;
-    default: return false;
-    }
-    if (ok) {
-        char kind[32];
-        snprintf(kind, sizeof kind, "k_march_hyb%d", S);
-        note_kernel(kind, nb, method);
-    }
-    return ok;
-}
-
 template <int B, int S, bool PIPE>
 static hipError_t seg_launch(int method, const float *vol, const Params &P, uint32_t nslots,
                              hipStream_t s) {
@@ -282,16 +206,13 @@ static hipError_t seg_launch(int method, const float *vol, const Params &P, uint
 template <int B>
 static bool seg_b(int method, int S, const float *vol, const Params &P, uint32_t nslots,
                   hipStream_t s, hipError_t &err) {
-    // S > 0: plain windows; S < 0: pipelined windows of |S| lanes
+    // S > 0: plain windows; S < 0: pipelined windows of |S| lanes (the
+    // dispatch uses 4, -2 and -4; 2 is kept as the plain counterpart of -2)
     switch (S) {
-    case 1: err = seg_launch<B, 1, false>(method, vol, P, nslots, s); return true;
     case 2: err = seg_launch<B, 2, false>(method, vol, P, nslots, s); return true;
     case 4: err = seg_launch<B, 4, false>(method, vol, P, nslots, s); return true;
-    case 8: err = seg_launch<B, 8, false>(method, vol, P, nslots, s); return true;
-    case -1: err = seg_launch<B, 1, true>(method, vol, P, nslots, s); return true;
     case -2: err = seg_launch<B, 2, true>(method, vol, P, nslots, s); return true;
     case -4: err = seg_launch<B, 4, true>(method, vol, P, nslots, s); return true;
-    case -8: err = seg_launch<B, 8, true>(method, vol, P, nslots, s); return true;
     default: return false;
     }
 }

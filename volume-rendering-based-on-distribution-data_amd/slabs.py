@@ -67,6 +67,8 @@ def bounds_by_cost(nz: int, n: int, direction: int, bounds, costs,
     march order covering [0, nz)."""
     if direction == 0:
         raise ValueError("rays of this view cross z-slabs in both directions")
+    if n < 1 or n > nz:
+        raise ValueError(f"{n} slabs cannot partition {nz} slices (1 <= n <= nz)")
     # per-slice cost in march order (slice index 0 = first crossed)
     dens = np.zeros(nz, dtype=np.float64)
     for (lo, hi), c in zip(bounds, costs):
@@ -103,6 +105,8 @@ def bounds_by_cost(nz: int, n: int, direction: int, bounds, costs,
         i = max(range(len(cuts) - 1), key=lambda j: cuts[j + 1] - cuts[j])
         cuts.insert(i + 1, (cuts[i] + cuts[i + 1]) // 2)
     march = [(cuts[i], cuts[i + 1]) for i in range(n)]  # in march-order slice indices
+    # n <= nz and every halving splits a slab of >= 2 slices, so no slab is empty
+    assert len(cuts) == n + 1 and all(b > a for a, b in march), march
     if direction > 0:
         return march
     return [(nz - b, nz - a) for a, b in march]
