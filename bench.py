@@ -165,7 +165,7 @@ def cpu_baseline(pkg, cfg_name, m, method, row_stride):
     }, (ref, row_stride)
 
 
-def frame_parity(got8, got_f, got_n, ref, row_stride, kernel):
+def frame_parity(got8, got_f, got_n, kernel, ref, row_stride):
     """GPU frame vs the oracle's frame (rows 0, s, 2s, ... of the CPU baseline):
     the reference's own check compares its whole benchmark frame (C:1073-1077)"""
     r8, rf, rn = ref
