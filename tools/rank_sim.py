@@ -41,8 +41,8 @@ def main():
     m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
          else pkg.camera.display_inv_view((30.0, 45.0)))
 
-    def timed(fn):
-        for _ in range(3):  # a full frame's 2nd render re-deals its tiles (adaptive order)
+    def timed(fn, warm=3):
+        for _ in range(warm):  # a full frame's 2nd render re-deals its tiles (adaptive order)
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -54,8 +54,11 @@ def main():
 
     full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     dfull = pkg.make_desc(full, W, H, m, query_method=args.method)
-    t1 = timed(lambda: pkg.render(dfull))
-    print(f"{args.config} {args.camera} m{args.method}: full frame {t1:.3f} ms "
+    # steady state: the clocks and address translation need ~15-20 frames of a
+    # running frame loop (profiles/r02/loop_timing.log); the speedups below are
+    # against this steady full frame, measured again after the rank lists
+    t1 = timed(lambda: pkg.render(dfull), warm=30)
+    print(f"{args.config} {args.camera} m{args.method}: steady full frame {t1:.3f} ms "
           f"({pkg.last_kernel()})")
     # latency floor: k centre-most tiles alone on the GPU
     lists1 = pkg.tiles.tile_lists(W, H, 1, m)[0]
@@ -83,7 +86,7 @@ def main():
         # two passes over the ranks, the second reported (the first pass's rank 0
         # ran right after a different launch shape)
         for _ in range(2):
-            per = [timed(lambda d=d: pkg.render(d)) for d in descs]
+            per = [timed(lambda d=d: pkg.render(d), warm=10) for d in descs]
         frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
         tu = timed(lambda: pkg.unscatter_tiles(packed, dl, world, slots, frame, W, H))
         torch.cuda.synchronize()
@@ -91,6 +94,8 @@ def main():
         print(f"  {mode:4s} N={world}: per-rank ms {' '.join(f'{x:.3f}' for x in per)}  max {max(per):.3f}"
               f"  unscatter {tu:.3f}  -> est. speedup {t1 / (max(per) + tu):.2f}x"
               f"  frame {'identical' if ok else 'DIFFERS'}")
+    t2 = timed(lambda: pkg.render(dfull), warm=30)
+    print(f"steady full frame again: {t2:.3f} ms (speedups above use {t1:.3f})")
 
 
 if __name__ == "__main__":

@@ -137,70 +137,89 @@ __device__ __forceinline__ void mark_foot(const Params &P, const Foot &f) {
     }
 }
 
+// NG groups of 64 box voxels from position p0: all NG loads issue before the
+// first decode waits on them
+template <int B, int M, int NG>
+__device__ __forceinline__ void box_chunk(const float *__restrict__ vbase, const Params &P,
+                                          float *box, int dx, int dxy, int V, uint32_t lane,
+                                          int p0, float rdx, float rdxy) {
+    const uint32_t sy = (uint32_t)P.sy;
+    float rec[NG][B];
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        const int p = min(p0 + g * 64 + (int)lane, V - 1);
+        const int z = (int)(((float)p + 0.5f) * rdxy);
+        const int r = p - z * dxy;
+        const int y = (int)(((float)r + 0.5f) * rdx);
+        const int x = r - y * dx;
+        const uint64_t off = (uint64_t)(uint32_t)z * P.sz + (uint32_t)(y * sy + x);
+        if constexpr (B == 16 || B == 32) {
+            // wide records: the quad loads its 4 lanes' records as contiguous
+            // 64-B runs (lane q reads chunk 4s + q of each) and a DPP transpose
+            // hands every lane its own (k_march_wq); lane-owned 64 / 128-B
+            // records made every 16-B wave load touch ~64 lines
+            const uint32_t q = lane & 3u;
+            const uint32_t lo = (uint32_t)off, hi = (uint32_t)(off >> 32);
+            float4 Mq[B / 16][4];
+#pragma unroll
+            for (int R = 0; R < 4; R++) {
+                const uint32_t l = (uint32_t)(R == 0 ? bcast_g<0>((int)lo) : R == 1 ? bcast_g<1>((int)lo)
+                                            : R == 2 ? bcast_g<2>((int)lo) : bcast_g<3>((int)lo));
+                const uint32_t h = (uint32_t)(R == 0 ? bcast_g<0>((int)hi) : R == 1 ? bcast_g<1>((int)hi)
+                                            : R == 2 ? bcast_g<2>((int)hi) : bcast_g<3>((int)hi));
+                const float4 *src = reinterpret_cast<const float4 *>(
+                    vbase + (((uint64_t)h << 32) | l) * (uint64_t)B);
+#pragma unroll
+                for (int c = 0; c < B / 16; c++) Mq[c][R] = src[4 * c + q];
+            }
+#pragma unroll
+            for (int c = 0; c < B / 16; c++) {
+                quad_transpose(Mq[c], q);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    rec[g][16 * c + 4 * k + 0] = Mq[c][k].x;
+                    rec[g][16 * c + 4 * k + 1] = Mq[c][k].y;
+                    rec[g][16 * c + 4 * k + 2] = Mq[c][k].z;
+                    rec[g][16 * c + 4 * k + 3] = Mq[c][k].w;
+                }
+            }
+        } else {
+            load_rec<B>(vbase, off, rec[g]);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        const int p = p0 + g * 64 + (int)lane;
+        if (p < V) box[p] = record_stat<B, M>(rec[g], P.enorm);
+    }
+}
+
 // Staged path: the wave's footprint box for this step (every voxel any active
 // lane's 8 corners touch) is loaded with consecutive lanes on consecutive
 // voxels of a box row (coalesced), each voxel's statistic is decoded ONCE and
 // parked in the wave's LDS slice, then every lane blends its 8 corners from
 // LDS.  Position p -> (x,y,z) in the box uses float reciprocals, exact for
 // p < 2^11 (box_max <= 1024).  Positions past the box end are clamped to its
-// last voxel so every load is unconditional: all G slots' loads issue
-// back-to-back before the first decode waits on them.
+// last voxel so every load is unconditional: all of a chunk's loads issue
+// back-to-back before the first decode waits on them.  A chunk takes only the
+// 64-voxel groups the box still needs (wave-uniform): a 140-voxel box decodes
+// 192 slots, not 256 (512^3 x 8 at 1080p: boxes of ~130-210 voxels).
 template <int B, int M>
 __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, const Params &P,
                                            float *box, int dx, int dxy, int V, uint32_t lane) {
     constexpr int G0 = B >= 32 ? 1 : (B >= 16 ? 2 : 4);
     constexpr int G = G0 < VR_BOX_G ? G0 : VR_BOX_G;  // voxels per lane in flight
     const float rdx = 1.0f / (float)dx, rdxy = 1.0f / (float)dxy;
-    const uint32_t sy = (uint32_t)P.sy;
     for (int p0 = 0; p0 < V; p0 += 64 * G) {
-        float rec[G][B];
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            const int p = min(p0 + g * 64 + (int)lane, V - 1);
-            const int z = (int)(((float)p + 0.5f) * rdxy);
-            const int r = p - z * dxy;
-            const int y = (int)(((float)r + 0.5f) * rdx);
-            const int x = r - y * dx;
-            const uint64_t off = (uint64_t)(uint32_t)z * P.sz + (uint32_t)(y * sy + x);
-            if constexpr (B == 16 || B == 32) {
-                // wide records: the quad loads its 4 lanes' records as contiguous
-                // 64-B runs (lane q reads chunk 4s + q of each) and a DPP transpose
-                // hands every lane its own (k_march_wq); lane-owned 64 / 128-B
-                // records made every 16-B wave load touch ~64 lines
-                const uint32_t q = lane & 3u;
-                const uint32_t lo = (uint32_t)off, hi = (uint32_t)(off >> 32);
-                float4 Mq[B / 16][4];
-#pragma unroll
-                for (int R = 0; R < 4; R++) {
-                    const uint32_t l = (uint32_t)(R == 0 ? bcast_g<0>((int)lo) : R == 1 ? bcast_g<1>((int)lo)
-                                                : R == 2 ? bcast_g<2>((int)lo) : bcast_g<3>((int)lo));
-                    const uint32_t h = (uint32_t)(R == 0 ? bcast_g<0>((int)hi) : R == 1 ? bcast_g<1>((int)hi)
-                                                : R == 2 ? bcast_g<2>((int)hi) : bcast_g<3>((int)hi));
-                    const float4 *src = reinterpret_cast<const float4 *>(
-                        vbase + (((uint64_t)h << 32) | l) * (uint64_t)B);
-#pragma unroll
-                    for (int c = 0; c < B / 16; c++) Mq[c][R] = src[4 * c + q];
-                }
-#pragma unroll
-                for (int c = 0; c < B / 16; c++) {
-                    quad_transpose(Mq[c], q);
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        rec[g][16 * c + 4 * k + 0] = Mq[c][k].x;
-                        rec[g][16 * c + 4 * k + 1] = Mq[c][k].y;
-                        rec[g][16 * c + 4 * k + 2] = Mq[c][k].z;
-                        rec[g][16 * c + 4 * k + 3] = Mq[c][k].w;
-                    }
-                }
-            } else {
-                load_rec<B>(vbase, off, rec[g]);
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            const int p = p0 + g * 64 + (int)lane;
-            if (p < V) box[p] = record_stat<B, M>(rec[g], P.enorm);
-        }
+        const int left = V - p0;  // wave-uniform
+        if (G >= 4 && left > 192)
+            box_chunk<B, M, (G >= 4 ? 4 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
+        else if (G >= 3 && left > 128)
+            box_chunk<B, M, (G >= 3 ? 3 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
+        else if (G >= 2 && left > 64)
+            box_chunk<B, M, (G >= 2 ? 2 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
+        else
+            box_chunk<B, M, 1>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
     }
 }
 
