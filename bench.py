@@ -103,9 +103,46 @@ def traffic_entry(args, kernel, world):
     if entry.get("kernel") != kernel or entry.get("lib_sha16") != sha:
         return None, (f"PMC entry {key} was measured on {entry.get('kernel')} of libvr.so "
                       f"{entry.get('lib_sha16')}, this run is {kernel} of {sha}")
-    return entry.get("hbm_bytes_per_launch"), (
+    return entry, (
         f"{os.path.relpath(args.traffic_json, ROOT)}[{key}]: FETCH_SIZE x 2 + WRITE_SIZE per "
         f"launch, rocprofv3 --pmc on this libvr.so build ({sha}), {entry.get('measured', '')}")
+
+
+VALU_ISSUE_CYCLES = 2      # SIMD cycles per f32 wave64 VALU instruction (f64 adds: ~4.4,
+SIMDS, CLOCK_HZ = 1024, 2.4e9  # tools/valu_calib.hip); 256 CUs x 4 SIMDs at 2.4 GHz
+
+
+def issue_bounds(pkg, torch, stream, W, H, m, method, kern_ms, pmc):
+    """The bounds of a launch that is not HBM-bound:
+    latency -- the frame cannot end before its longest tile's step chain does: the
+    longest-ray tile rendered ALONE (one 64x4 tile, its list entry first in the
+    longest-first order), min over 5 launches, as a fraction of the frame;
+    valu -- f32-rate VALU issue: SQ_INSTS_VALU of the launch (committed PMC pass on
+    this build) x 2 cycles over 1024 SIMDs x 2.4 GHz x kernel time (f64 decode
+    instructions take ~2x that, so the true VALU busy lies between frac and ~2x)"""
+    lst = pkg.tiles.tile_lists(W, H, 1, m)[0][:1]
+    with torch.cuda.stream(stream):
+        dl = torch.from_numpy(lst.view(np.int32).copy()).to(torch.cuda.current_device())
+        buf = torch.zeros(256, dtype=torch.int32, device=dl.device)
+        d = pkg.make_desc(buf, W, H, m, query_method=method, d_tile_list=dl, n_tiles=1)
+        ts = []
+        for _ in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            pkg.render(d)
+            e1.record(stream)
+            ts.append((e0, e1))
+    torch.cuda.synchronize()
+    t1 = min(a.elapsed_time(b) for a, b in ts[1:])
+    out = {"latency": {"longest_tile_alone_ms": round(t1, 4), "frac": round(t1 / kern_ms, 4),
+                       "kernel": pkg.last_kernel()}}
+    if pmc and pmc.get("valu_insts"):
+        busy = pmc["valu_insts"] * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_HZ * kern_ms * 1e-3)
+        out["valu"] = {"insts_per_launch": int(pmc["valu_insts"]),
+                       "achieved": round(pmc["valu_insts"] / (kern_ms * 1e-3) / 1e12, 4),
+                       "peak": round(SIMDS * CLOCK_HZ / VALU_ISSUE_CYCLES / 1e12, 4),
+                       "unit": "T wave-instr/s", "frac": round(busy, 4)}
+    return out
 
 
 def host_threads():
@@ -401,7 +438,8 @@ def main_gmm(args):
         last = frames[(nframe[0] - 1) % R]
         np.save(args.dump_frame, last.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
-    traffic, traffic_src = traffic_entry(args, kernel, world)
+    pmc, traffic_src = traffic_entry(args, kernel, world)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     alg_bytes = u * rec_bytes + W * H * 4 if u is not None else None
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if alg_bytes else None
     ms_per_step = elapsed / args.steps * 1e3
@@ -607,7 +645,11 @@ def main():
     # HBM bytes per launch from the committed PMC passes of this same workload
     # (tools/pmc_traffic.py; FETCH_SIZE x 2 + WRITE_SIZE), only if they were
     # measured on this very libvr.so build (sha256 of the file) and kernel
-    traffic, traffic_src = traffic_entry(args, kernel, world)
+    pmc, traffic_src = traffic_entry(args, kernel, world)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    # the bounds that apply when the frame is not HBM-bound (the smaller configs)
+    bounds = (issue_bounds(pkg, torch, stream, W, H, m, args.method, kern_ms, pmc)
+              if world == 1 else None)
 
     # parity of the timed frame's view (untimed; full frames at N = 1 are checked
     # against the oracle frame of the CPU baseline below, N > 1 assembled frames
@@ -679,6 +721,7 @@ def main():
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
                 "U_records": int(u) if u is not None else None,
+                "issue_bounds": bounds,
             },
             "parity": parity,
             "cpu_baseline": cpu,

@@ -14,6 +14,7 @@ the guide's HBM section:
 FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB.
 
 usage: python tools/pmc_traffic.py OUT.json KEY BENCH_LOG PASS_DIR [PASS_DIR ...]
+  (an issue pass with SQ_INSTS_VALU / SQ_WAVES / GRBM_GUI_ACTIVE adds the VALU count)
   KEY       entry name, e.g. "1024x8|C0|m1"
   BENCH_LOG stdout of the profiled bench.py (its JSON line names the kernel)
 """
@@ -69,6 +70,14 @@ def main():
         "write_bytes": write_kib * 1024 if write_kib is not None else None,
         "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"] if bench else None,
     }
+    # issue pass (optional): VALU wave-instructions per launch (SQ_INSTS_VALU counts
+    # instructions on gfx950, as SQ_ACTIVE_INST_VALU does: tools/valu_calib.hip) and
+    # the clock cycles of the launch (GRBM_GUI_ACTIVE summed over the 8 XCDs)
+    for c, k in (("SQ_INSTS_VALU", "valu_insts"), ("SQ_INSTS_VMEM_RD", "vmem_rd_insts"),
+                 ("SQ_INSTS_LDS", "lds_insts"), ("SQ_WAVES", "waves"),
+                 ("GRBM_GUI_ACTIVE", "grbm_gui_active")):
+        if c in avg:
+            entry[k] = avg[c]
     if entry["read_bytes"] is not None and entry["write_bytes"] is not None:
         entry["hbm_bytes_per_launch"] = int(entry["read_bytes"] + entry["write_bytes"])
     # the build the passes ran on: bench.py reports this traffic only for it
