@@ -72,15 +72,12 @@ def main():
     steps = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
     pkg.render(pkg.make_desc(full, W, H, m, query_method=args.method, d_steps=steps))
     cost = pkg.tiles.tile_costs_from_frame(steps.cpu().numpy(), W, H)
-    modes = ([("est", w) for w in (2, 4, 8)] + [("cost", w) for w in (2, 4, 8)] +
-             [("band", w) for w in (2, 4, 8)])
+    modes = [("est", w) for w in (2, 4, 8)] + [("cost", w) for w in (2, 4, 8)]
     for mode, world in modes:
         if mode == "est":
             lists = pkg.tiles.tile_lists(W, H, world, None if args.no_lpt else m)
-        elif mode == "cost":
-            lists = pkg.tiles.tile_lists_by_cost(W, H, world, cost)
         else:
-            lists = pkg.tiles.tile_lists_by_cost_bands(W, H, world, cost)
+            lists = pkg.tiles.tile_lists_by_cost(W, H, world, cost)
         slots = lists.shape[1]
         packed = torch.zeros((world, slots * 256), dtype=torch.int32, device="cuda")
         dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()

@@ -210,58 +210,6 @@ def tile_lists_by_cost(width: int, height: int, world_size: int, cost) -> np.nda
     return out
 
 
-def tile_lists_by_cost_bands(width: int, height: int, world_size: int, cost) -> np.ndarray:
-    """Like tile_lists_by_cost, but each rank gets one compact region: the
-    1x4-tile blocks in row-major order (block rows, alternating direction) are
-    cut into world_size contiguous runs of equal measured cost, and each rank
-    deals its own run to its 8 XCDs (most expensive first, to the least
-    loaded XCD with room; XCD sublists PAD-padded to one length).  Runs hold
-    different block counts, so ranks' lists are PAD-padded to the longest for
-    the equal-size gather.  (Measured against the lattice deal of
-    tile_lists_by_cost by tools/rank_sim.py.)"""
-    tx, ty = tiles_x(width), tiles_y(height)
-    cost = np.asarray(cost, dtype=np.int64).reshape(ty, tx)
-    nbx, nby = (tx + BLOCK_X - 1) // BLOCK_X, (ty + BLOCK_Y - 1) // BLOCK_Y
-    pad = np.zeros((nby * BLOCK_Y, nbx * BLOCK_X), dtype=np.int64)
-    pad[:ty, :tx] = cost
-    bcost = pad.reshape(nby, BLOCK_Y, nbx, BLOCK_X).sum(axis=(1, 3))
-    order = [(by, bx if by % 2 == 0 else nbx - 1 - bx) for by in range(nby) for bx in range(nbx)]
-    c = np.array([bcost[by, bx] for by, bx in order], dtype=np.float64)
-    cum = np.cumsum(c)
-    total = cum[-1] if len(cum) else 0.0
-    cuts = [0] + [int(np.searchsorted(cum, total * r / world_size, side="left")) + 1
-                  for r in range(1, world_size)] + [len(order)]
-    cuts = list(np.maximum.accumulate(np.minimum(cuts, len(order))))
-    ids = []
-    for r in range(world_size):
-        run = order[cuts[r]:cuts[r + 1]]
-        run = sorted(run, key=lambda q: -bcost[q])  # stable: most expensive first
-        lo, extra = divmod(len(run), XCDS)
-        load = np.zeros(XCDS, dtype=np.int64)
-        count = np.zeros(XCDS, dtype=np.int64)
-        lists = [[] for _ in range(XCDS)]
-        n_plus = 0
-        for by, bx in run:
-            room = (count < lo) | ((count == lo) & (n_plus < extra))
-            g = int(np.argmin(np.where(room, load, np.iinfo(np.int64).max)))
-            n_plus += int(count[g] == lo)
-            load[g] += bcost[by, bx]
-            count[g] += 1
-            for y in range(by * BLOCK_Y, min(ty, by * BLOCK_Y + BLOCK_Y)):
-                for x in range(bx * BLOCK_X, min(tx, bx * BLOCK_X + BLOCK_X)):
-                    lists[g].append(y * tx + x)
-        longest = max(len(l) for l in lists)
-        inter = np.full((longest, XCDS), PAD, dtype=np.uint32)
-        for g, l in enumerate(lists):
-            inter[:len(l), g] = l
-        ids.append(inter.reshape(-1))
-    n_slots = max(len(i) for i in ids)
-    out = np.full((world_size, n_slots), PAD, dtype=np.uint32)
-    for r, i in enumerate(ids):
-        out[r, :len(i)] = i
-    return out
-
-
 def gather_packed(packed, world_size: int, rank: int, group=None):
     """Gather every rank's packed tile buffer to rank 0.
 
