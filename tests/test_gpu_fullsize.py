@@ -64,7 +64,11 @@ def _release(pkg):
 
 
 def camera(pkg, cam):
-    return pkg.camera.single_test_inv_view() if cam == "C0" else pkg.camera.display_inv_view()
+    """C0 runSingleTest (C:1024-1043), C1 display() at (30, 45) deg, S a side view
+    (display() at yaw 90: screen x along the volume's z, the z-rows copy)"""
+    if cam == "C0":
+        return pkg.camera.single_test_inv_view()
+    return pkg.camera.display_inv_view((0.0, 90.0) if cam == "S" else (30.0, 45.0))
 
 
 def render_frames(pkg, torch, W, H, m, method, n_frames=2, volume_size=None):
@@ -90,9 +94,9 @@ def render_frames(pkg, torch, W, H, m, method, n_frames=2, volume_size=None):
     ("128x1", "C0", 1), ("128x1", "C1", 1), ("128x1", "C0", 2), ("128x1", "C1", 7),
     ("256x4", "C0", 1), ("256x4", "C1", 1), ("256x4", "C0", 3), ("256x4", "C1", 2),
     ("512x8", "C0", 1), ("512x8", "C1", 1), ("512x8", "C0", 2), ("512x8", "C1", 2),
-    ("512x8", "C0", 3), ("512x8", "C1", 7),
+    ("512x8", "C0", 3), ("512x8", "C1", 7), ("512x8", "S", 1),
     ("1024x8", "C0", 1), ("1024x8", "C1", 1), ("1024x8", "C0", 2), ("1024x8", "C1", 2),
-    ("1024x8", "C0", 7),
+    ("1024x8", "C0", 7), ("1024x8", "S", 1), ("1024x8", "S", 3),
 ])
 def test_full_frame(pkg, orc, gpu, name, cam, method):
     import torch

@@ -894,3 +894,56 @@ def test_environment_does_not_change_the_kernel(pkg, orc, gpu, monkeypatch):
         assert_parity(got, ref, "VR_PATH=0 through vr_set_tuning")
     finally:
         pkg.clear_tuning()
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4, 8])
+def test_side_views_take_the_zrows_copy(pkg, orc, gpu, nb, tune):
+    """views whose screen x runs along the volume's z (|M[8]| >= 0.95) march the
+    z-rows copy with the per-ray pipelined march (vr_api.cpp ensure_zrows):
+    full frames and rank tile lists bit-identical to the oracle, the copy
+    dropped with the volume (a new volume renders its own frame) and by
+    vr_release_stats, VR_ZROWS=0 keeps the x rows.  (Frames below the ray-segmented
+    thresholds keep that march, so this small frame sets VR_SEG_RAYS=0 and a volume
+    finer than the frame)"""
+    import torch
+    tune.set("VR_SEG_RAYS", "0")
+    vol = orc.synth_volume(48, 40, 44, nb)
+    pkg.init_distribution(vol)
+    W, H = 88, 68
+    for rot in ((0.0, 90.0), (12.0, 95.0), (-10.0, -80.0), (8.0, 265.0)):  # M[8] = cos rx sin ry
+        m = pkg.camera.display_inv_view(rot)
+        assert abs(m[8]) >= 0.95
+        for method in (1, 2, 3):
+            got = gpu_render(pkg, None, W, H, m, method, torch)
+            assert pkg.last_kernel().startswith("k_march_pipe_zrows<"), pkg.last_kernel()
+            ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+            assert_parity(got, ref, f"side {rot} nb={nb} m{method}")
+    # a rank's packed tile list
+    m = pkg.camera.display_inv_view((0.0, 90.0))
+    lists = pkg.tiles.tile_lists(W, H, 3, m)
+    n_slots = lists.shape[1]
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    packed = torch.full((3, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    for r in range(3):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+        assert pkg.last_kernel().startswith("k_march_pipe_zrows<"), pkg.last_kernel()
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, 3, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    ref8 = orc.render(vol, orc.make_params(W, H, m, query_method=1), want_float=False,
+                      want_steps=False)[0]
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref8)
+    # the copy follows the volume
+    vol2 = orc.synth_volume(48, 40, 44, nb, seed=5)
+    pkg.init_distribution(vol2)
+    got = gpu_render(pkg, None, W, H, m, 1, torch)
+    assert_parity(got, orc.render(vol2, orc.make_params(W, H, m, query_method=1))[:3], "vol2")
+    pkg.release_stats()
+    got = gpu_render(pkg, None, W, H, m, 2, torch)
+    assert pkg.last_kernel().startswith("k_march_pipe_zrows<"), pkg.last_kernel()
+    assert_parity(got, orc.render(vol2, orc.make_params(W, H, m, query_method=2))[:3], "rebuilt")
+    tune.set("VR_ZROWS", "0")
+    got = gpu_render(pkg, None, W, H, m, 1, torch)
+    assert not pkg.last_kernel().startswith("k_march_pipe_zrows"), pkg.last_kernel()
+    assert_parity(got, orc.render(vol2, orc.make_params(W, H, m, query_method=1))[:3], "x rows")

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--step", type=float, default=5.0)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--paths", default="2,0", help="forced VR_PATH values to time beside the default")
+    ap.add_argument("--knob", default="VR_ZROWS=0",
+                    help="one more column: the default dispatch under this tuning knob")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
@@ -52,8 +54,9 @@ def main():
 
     paths = [p for p in args.paths.split(",") if p]
     print(f"{args.config} m{args.method} {W}x{H}: median kernel ms over {args.reps} frames")
+    kk, kv = args.knob.split("=") if args.knob else (None, None)
     print(f"{'rx':>4} {'ry':>5} {'m00':>6}  {'default':>8} kernel" +
-          "".join(f"   VR_PATH={p:>2}" for p in paths))
+          "".join(f"   VR_PATH={p:>2}" for p in paths) + (f"   {args.knob}" if kk else ""))
     for rx in (float(v) for v in args.rx.split(",")):
         for ry in np.arange(0.0, 90.0 + 1e-6, args.step):
             m = pkg.camera.display_inv_view((rx, float(ry)))
@@ -66,6 +69,11 @@ def main():
                 t, _ = timed(desc)
                 row += f"   {t:8.3f}"
             pkg.clear_tuning()
+            if kk:
+                pkg.set_tuning(kk, kv)
+                t, _ = timed(desc)
+                row += f"   {t:8.3f}"
+                pkg.clear_tuning()
             print(row, flush=True)
 
 

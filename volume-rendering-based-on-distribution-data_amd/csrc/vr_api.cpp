@@ -76,6 +76,10 @@ struct State {
     // of oblique views (ensure_brick, brick_index); nullptr = not made
     float *brick = nullptr;
     uint64_t bsy = 0, bsz = 0;
+    // z-rows copy of an owned B <= 8 volume for side views (ensure_zrows,
+    // zrows_index); nullptr = not made
+    float *zrows = nullptr;
+    uint64_t zsx = 0, zsy = 0;
     // bumped whenever a resident volume / codec / flexible-block set is
     // released, so an order learned on old data is not reused (the order is a
     // scheduling hint only: any order renders the same image)
@@ -130,9 +134,16 @@ void release_brick() {
     g.bsy = g.bsz = 0;
 }
 
+void release_zrows() {
+    if (g.zrows) (void)hipFree(g.zrows);
+    g.zrows = nullptr;
+    g.zsx = g.zsy = 0;
+}
+
 void release_volume() {
     release_stats();
     release_brick();
+    release_zrows();
     g.volume_epoch++;
     if (g.vol && g.owned) (void)hipFree(g.vol);
     g.vol = nullptr;
@@ -773,6 +784,49 @@ bool ensure_brick() {
     return true;
 }
 
+// Views whose screen x runs along the volume's z axis (side views: |M[8]| >=
+// 0.95, e.g. the display() camera at yaw 90 deg) see the x rows across: a
+// wave's 64 rays sit at consecutive z, each reading its own lines.  A copy of
+// the records with z contiguous (zrows_index) gives them what x rows give the
+// runSingleTest view -- consecutive lanes on consecutive records -- and the
+// per-ray pipelined march reads it (1024^3 x 8, yaw 90: DESIGN.md 4.7).  Made
+// on the first such frame of an owned volume with B <= 8 (as ensure_brick:
+// synchronous, only with max(4 GiB, 5 %) of HBM left free); VR_ZROWS=0
+// (vr_set_tuning) disables it.
+bool ensure_zrows() {
+    if (const char *e = vr::tuning("VR_ZROWS"))
+        if (std::atoi(e) == 0) return false;
+    if (g.zrows) return true;
+    if (!g.vol || !g.owned || !(g.nb == 1 || g.nb == 2 || g.nb == 4 || g.nb == 8)) return false;
+    const uint64_t zsy = (uint64_t)g.nz, zsx = zsy * (uint64_t)g.ny;
+    const uint64_t bytes = zsx * (uint64_t)g.nx * (uint64_t)g.nb * sizeof(float);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
+        free_b < bytes + std::max<uint64_t>(4ull << 30, total_b / 20)) {
+        (void)hipGetLastError();
+        return false;
+    }
+    float *buf = nullptr;
+    if (hipMalloc(&buf, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    vr::Params P;
+    std::memset(&P, 0, sizeof P);
+    P.nx = g.nx; P.ny = g.ny; P.nz = g.nz; P.nb = g.nb;
+    P.sy = g.sy; P.sz = g.sz;
+    if (vr::launch_zrows(g.vol, P, buf, zsx, zsy, g.stream) != hipSuccess ||
+        hipStreamSynchronize(g.stream) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(buf);
+        return false;
+    }
+    g.zrows = buf;
+    g.zsx = zsx;
+    g.zsy = zsy;
+    return true;
+}
+
 }  // namespace
 
 namespace vr {
@@ -1323,7 +1377,17 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
         const char *eq = vr::tuning("VR_M7_QUAD");
         const bool m7_quad = qm == 7 && P.oblique && P.m7x == P.nx && P.m7y == P.ny &&
                              P.m7z == P.nz && !(eq && std::atoi(eq) == 0);
-        if (g.nb == 8 && ((P.path == 0 && qm >= 1 && qm <= 3) || m7_quad) && ensure_brick()) {
+        // side views (screen x along the volume's z) read the z-rows copy with
+        // the per-ray pipelined march instead of the quad march / x-row pipe
+        const bool side = !P.oblique ? false : std::fabs(desc->inv_view[8]) >= 0.95f;
+        if (side && qm >= 1 && qm <= 3 && (P.path == 0 || P.path == 2) && g.nb <= 8 &&
+            !vr::tuning("VR_PATH") && ensure_zrows()) {
+            P.path = 2;
+            P.zvol = g.zrows;
+            P.zsx = g.zsx;
+            P.zsy = g.zsy;
+        } else if (g.nb == 8 && ((P.path == 0 && qm >= 1 && qm <= 3) || m7_quad) &&
+                   ensure_brick()) {
             P.bvol = g.brick;
             P.bsy = g.bsy;
             P.bsz = g.bsz;
@@ -1794,7 +1858,8 @@ int vr_bake_stats(void) { return bake_stats(); }
 int vr_release_stats(void) {
     release_stats();
     release_cstats();
-    release_brick();  // the micro-brick copy is derived from the records too
+    release_brick();  // the layout copies are derived from the records too
+    release_zrows();
     return VR_OK;
 }
 

@@ -53,6 +53,12 @@ struct Params {
     // in records (brick_index); the launch passes it as vol with sy / sz = bsy / bsz
     const float *bvol;
     uint64_t bsy, bsz;
+    // z-rows copy of the records (B <= 8) for views whose screen x runs along
+    // the volume's z axis (side views): record (x, y, z) at x * zsx + y * zsy + z
+    // (zrows_index); the launch passes it as vol with sx / sy / sz = zsx / zsy / 1
+    const float *zvol;
+    uint64_t zsx, zsy;
+    uint64_t sx;                 // record stride of x (gather MODE 3 only; 1 in x rows)
     // fractal/template codec (methods 4/5/6): codebook int4 per voxel, templates
     // [ntpl][nb], (bin, value) errors [voxel][err_slots]
     const int4 *cb;
@@ -91,6 +97,13 @@ struct Params {
 __host__ __device__ __forceinline__ uint64_t brick_index(uint64_t x, uint64_t y, uint64_t z,
                                                          uint64_t bsy, uint64_t bsz) {
     return z * bsz + (y >> 1) * bsy + (x >> 1) * 4u + (y & 1u) * 2u + (x & 1u);
+}
+
+// Record index of voxel (x, y, z) in the z-rows copy: z fastest, then y, then x
+// (zsy = Z records per (x, y) row, zsx = Y * Z per x-plane).
+__host__ __device__ __forceinline__ uint64_t zrows_index(uint64_t x, uint64_t y, uint64_t z,
+                                                         uint64_t zsx, uint64_t zsy) {
+    return x * zsx + y * zsy + z;
 }
 
 // Baked statistics planes (basicDataProcessing, vr_stats.hip): 16 x 2 x 1

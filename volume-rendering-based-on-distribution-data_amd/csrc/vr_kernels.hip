@@ -552,14 +552,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
 #ifndef VR_PIPE_MAXWAVES
 #define VR_PIPE_MAXWAVES(B) ((B) >= 8 ? 3 : 8)
 #endif
-template <int B, int M>
+template <int B, int M, int GM = kGatherMode<M>>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_PIPE_WAVES, VR_PIPE_MAXWAVES(B)))) void k_march_pipe(const float *__restrict__ vol, Params P) {
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
     unsigned long long t0 = 0;
     if (P.wave_clock) t0 = wall_clock64();
-    const int n = march_pipe_tile<B, M>(vol, P, slot, tile, threadIdx.x);
+    const int n = march_pipe_tile<B, M, GM>(vol, P, slot, tile, threadIdx.x);
     if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
     if (P.wave_clock && (threadIdx.x & 63) == 0) {
         unsigned long long *w = P.wave_clock + ((uint64_t)slot * 4u + threadIdx.x / 64u) * 3u;
@@ -2248,6 +2248,21 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         if (B < 8 && P.path == 0) P.path = 2;  // per-ray pipelined for narrow records
         if constexpr (B == 1) {  // baked statistics (vr_stats.hip, bricked planes): paths 2, 7 only
             if (method <= 0) P.path = 2;
+        }
+        if (P.path == 2 && P.zvol && method >= 1 && method <= 3) {
+            // side views on the z-rows copy (vr_api.cpp ensure_zrows): the same
+            // march, gathers addressed z-contiguous
+            note_kernel("k_march_pipe_zrows", B, method);
+            Params Q = P;
+            Q.sx = P.zsx;
+            Q.sy = P.zsy;
+            Q.sz = 1;
+            switch (method) {
+            case 1: hipLaunchKernelGGL((k_march_pipe<B, 1, 3>), grid, block, occupancy_lds(P), s, P.zvol, Q); break;
+            case 2: hipLaunchKernelGGL((k_march_pipe<B, 2, 3>), grid, block, occupancy_lds(P), s, P.zvol, Q); break;
+            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3, 3>), grid, block, occupancy_lds(P), s, P.zvol, Q); break;
+            }
+            return hipGetLastError();
         }
         if (P.path == 2 && method >= -1 && method <= 3) {
             note_kernel("k_march_pipe", B, method);

@@ -155,7 +155,8 @@ typedef float vr_f2a4 __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ vr_f2a4 load_pair64(const float *__restrict__ vol, uint64_t i) {
     return *reinterpret_cast<const vr_f2a4 *>(vol + i);
 }
-// MODE 0: records in x rows (P.sy / P.sz record pitches).  MODE 1 / 2: a baked
+// MODE 0: records in x rows (P.sy / P.sz record pitches).  MODE 3: the z-rows
+// copy (P.sx / P.sy strides, z contiguous; zrows_index).  MODE 1 / 2: a baked
 // statistics plane (B = 1) in 16 x 2 x 1 bricks (plane_index; P.sy / P.sz the
 // plane pitches): each (y, z) row's x-pair is one 8-byte load; MODE 1 forms the
 // index with 24-bit multiplies in 32 bits (pitches < 2^24, plane < 2^32 floats:
@@ -163,7 +164,7 @@ __device__ __forceinline__ vr_f2a4 load_pair64(const float *__restrict__ vol, ui
 template <int B, int MODE = 0>
 __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Params &P,
                                         const Foot &f, float (&rec)[8][B]) {
-    if constexpr (MODE != 0) {
+    if constexpr (MODE == 1 || MODE == 2) {
         static_assert(B == 1, "baked planes hold one float per voxel");
         const uint32_t bx = plane_bx((uint32_t)f.x0);
         const bool ox = f.x1 != f.x0;
@@ -191,6 +192,19 @@ __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Par
         rec[5][0] = ox ? c.y : c.x;
         rec[6][0] = d.x;
         rec[7][0] = ox ? d.y : d.x;
+        return;
+    }
+    if constexpr (MODE == 3) {  // z-rows copy: x and y strided, z contiguous
+        const uint64_t x0 = (uint64_t)f.x0 * P.sx, x1 = (uint64_t)f.x1 * P.sx;
+        const uint64_t y0 = (uint64_t)f.y0 * P.sy, y1 = (uint64_t)f.y1 * P.sy;
+        load_rec<B>(vol, x0 + y0 + f.z0, rec[0]);
+        load_rec<B>(vol, x1 + y0 + f.z0, rec[1]);
+        load_rec<B>(vol, x0 + y1 + f.z0, rec[2]);
+        load_rec<B>(vol, x1 + y1 + f.z0, rec[3]);
+        load_rec<B>(vol, x0 + y0 + f.z1, rec[4]);
+        load_rec<B>(vol, x1 + y0 + f.z1, rec[5]);
+        load_rec<B>(vol, x0 + y1 + f.z1, rec[6]);
+        load_rec<B>(vol, x1 + y1 + f.z1, rec[7]);
         return;
     }
     const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
@@ -227,7 +241,7 @@ __device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][
 // tfar) wastes one step of gathers.  The loop is unrolled by two so
 // the two register sets swap roles without copies.  t: thread index inside
 // the 256-thread tile; slot: the tile's launch slot (packed output position).
-template <int B, int M>
+template <int B, int M, int GM = kGatherMode<M>>
 __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, const Params &P,
                                                uint32_t slot, uint32_t tile, uint32_t tid) {
     uint32_t lx, ly;
@@ -250,7 +264,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
     bool alive = true;
     Foot fa = footprint(P, px, py, pz), fb;
     float ra[8][B], rb[8][B];
-    gather8<B, kGatherMode<M>>(vol, P, fa, ra);
+    gather8<B, GM>(vol, P, fa, ra);
     // one step: decode (fc, rc) while the gathers of the next step go to (fn, rn)
     auto step = [&](int i, const Foot &fc, const float (&rc)[8][B], Foot &fn,
                     float (&rn)[8][B]) {
@@ -266,7 +280,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
         // footprint instead -- cache hits -- measured 2.4 ms against 1.36:
         // the select changed the schedule again.)
         fn = footprint(P, nx, ny, nz);
-        gather8<B, kGatherMode<M>>(vol, P, fn, rn);
+        gather8<B, GM>(vol, P, fn, rn);
         const float sample = decode8<B, M>(P, rc, fc);
         n = i + 1;
         if (composite(P, sample, sx, sy, sz, sw) || !cont) {
