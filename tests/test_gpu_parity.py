@@ -897,9 +897,9 @@ def test_environment_does_not_change_the_kernel(pkg, orc, gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("nb", [1, 2, 4, 8])
-def test_side_views_take_the_zrows_copy(pkg, orc, gpu, nb, tune):
-    """views whose screen x runs along the volume's z (|M[8]| >= 0.95) march the
-    z-rows copy with the per-ray pipelined march (vr_api.cpp ensure_zrows):
+def test_axis_views_take_an_axis_rows_copy(pkg, orc, gpu, nb, tune):
+    """views whose screen x runs along the volume's z or y (|M[8]| or |M[4]| >= 0.95)
+    march an axis-rows copy with the per-ray pipelined march (ensure_axis_copy):
     full frames and rank tile lists bit-identical to the oracle, the copy
     dropped with the volume (a new volume renders its own frame) and by
     vr_release_stats, VR_ZROWS=0 keeps the x rows.  (Frames below the ray-segmented
@@ -910,14 +910,18 @@ def test_side_views_take_the_zrows_copy(pkg, orc, gpu, nb, tune):
     vol = orc.synth_volume(48, 40, 44, nb)
     pkg.init_distribution(vol)
     W, H = 88, 68
-    for rot in ((0.0, 90.0), (12.0, 95.0), (-10.0, -80.0), (8.0, 265.0)):  # M[8] = cos rx sin ry
+    # M[8] = cos rx sin ry (screen x along z), M[4] = sin rx sin ry (along y): the
+    # copies of both axes, one resident at a time, alternating views rebuild them
+    for rot, kern in (((0.0, 90.0), "zrows"), ((12.0, 95.0), "zrows"), ((90.0, 90.0), "yrows"),
+                      ((-10.0, -80.0), "zrows"), ((80.0, 95.0), "yrows"),
+                      ((-85.0, 80.0), "yrows"), ((8.0, 265.0), "zrows")):
         m = pkg.camera.display_inv_view(rot)
-        assert abs(m[8]) >= 0.95
+        assert abs(m[8 if kern == "zrows" else 4]) >= 0.95
         for method in (1, 2, 3):
             got = gpu_render(pkg, None, W, H, m, method, torch)
-            assert pkg.last_kernel().startswith("k_march_pipe_zrows<"), pkg.last_kernel()
+            assert pkg.last_kernel().startswith(f"k_march_pipe_{kern}<"), pkg.last_kernel()
             ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
-            assert_parity(got, ref, f"side {rot} nb={nb} m{method}")
+            assert_parity(got, ref, f"axis view {rot} nb={nb} m{method}")
     # a rank's packed tile list
     m = pkg.camera.display_inv_view((0.0, 90.0))
     lists = pkg.tiles.tile_lists(W, H, 3, m)

@@ -76,10 +76,11 @@ struct State {
     // of oblique views (ensure_brick, brick_index); nullptr = not made
     float *brick = nullptr;
     uint64_t bsy = 0, bsz = 0;
-    // z-rows copy of an owned B <= 8 volume for side views (ensure_zrows,
-    // zrows_index); nullptr = not made
-    float *zrows = nullptr;
-    uint64_t zsx = 0, zsy = 0;
+    // axis-rows copy of an owned B <= 8 volume for views along y or z
+    // (ensure_axis_copy, axis_copy_strides); nullptr = not made
+    float *acopy = nullptr;
+    int acopy_axis = 0;
+    uint64_t asx = 0, asy = 0, asz = 0;
     // bumped whenever a resident volume / codec / flexible-block set is
     // released, so an order learned on old data is not reused (the order is a
     // scheduling hint only: any order renders the same image)
@@ -134,16 +135,17 @@ void release_brick() {
     g.bsy = g.bsz = 0;
 }
 
-void release_zrows() {
-    if (g.zrows) (void)hipFree(g.zrows);
-    g.zrows = nullptr;
-    g.zsx = g.zsy = 0;
+void release_axis_copy() {
+    if (g.acopy) (void)hipFree(g.acopy);
+    g.acopy = nullptr;
+    g.acopy_axis = 0;
+    g.asx = g.asy = g.asz = 0;
 }
 
 void release_volume() {
     release_stats();
     release_brick();
-    release_zrows();
+    release_axis_copy();
     g.volume_epoch++;
     if (g.vol && g.owned) (void)hipFree(g.vol);
     g.vol = nullptr;
@@ -784,22 +786,26 @@ bool ensure_brick() {
     return true;
 }
 
-// Views whose screen x runs along the volume's z axis (side views: |M[8]| >=
-// 0.95, e.g. the display() camera at yaw 90 deg) see the x rows across: a
-// wave's 64 rays sit at consecutive z, each reading its own lines.  A copy of
-// the records with z contiguous (zrows_index) gives them what x rows give the
+// Views whose screen x runs along the volume's z or y axis (|M[8]| or |M[4]|
+// >= 0.95: side views, e.g. the display() camera at yaw 90 deg, and top views
+// at pitch and yaw 90 deg) see the x rows across: a wave's 64 rays sit at
+// consecutive z (y), each reading its own lines.  A copy of the records with
+// that axis contiguous (axis_copy_strides) gives them what x rows give the
 // runSingleTest view -- consecutive lanes on consecutive records -- and the
-// per-ray pipelined march reads it (1024^3 x 8, yaw 90: DESIGN.md 4.7).  Made
-// on the first such frame of an owned volume with B <= 8 (as ensure_brick:
-// synchronous, only with max(4 GiB, 5 %) of HBM left free); VR_ZROWS=0
-// (vr_set_tuning) disables it.
-bool ensure_zrows() {
+// per-ray pipelined march reads it (1024^3 x 8, yaw 90: 3.01 -> 1.63 ms,
+// DESIGN.md 4.7).  One axis copy is resident at a time (a view along the other
+// axis replaces it).  Made on the first such frame of an owned volume with
+// B <= 8 (as ensure_brick: synchronous, only with max(4 GiB, 5 %) of HBM left
+// free); VR_ZROWS=0 (vr_set_tuning) disables it.
+bool ensure_axis_copy(int axis) {
     if (const char *e = vr::tuning("VR_ZROWS"))
         if (std::atoi(e) == 0) return false;
-    if (g.zrows) return true;
+    if (g.acopy && g.acopy_axis == axis) return true;
     if (!g.vol || !g.owned || !(g.nb == 1 || g.nb == 2 || g.nb == 4 || g.nb == 8)) return false;
-    const uint64_t zsy = (uint64_t)g.nz, zsx = zsy * (uint64_t)g.ny;
-    const uint64_t bytes = zsx * (uint64_t)g.nx * (uint64_t)g.nb * sizeof(float);
+    release_axis_copy();
+    uint64_t sx = 0, sy = 0, sz = 0;
+    vr::axis_copy_strides(axis, (uint64_t)g.nx, (uint64_t)g.ny, (uint64_t)g.nz, sx, sy, sz);
+    const uint64_t bytes = (uint64_t)g.nx * g.ny * (uint64_t)g.nz * (uint64_t)g.nb * sizeof(float);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
         free_b < bytes + std::max<uint64_t>(4ull << 30, total_b / 20)) {
@@ -815,15 +821,17 @@ bool ensure_zrows() {
     std::memset(&P, 0, sizeof P);
     P.nx = g.nx; P.ny = g.ny; P.nz = g.nz; P.nb = g.nb;
     P.sy = g.sy; P.sz = g.sz;
-    if (vr::launch_zrows(g.vol, P, buf, zsx, zsy, g.stream) != hipSuccess ||
+    if (vr::launch_axis_copy(g.vol, P, buf, sx, sy, sz, g.stream) != hipSuccess ||
         hipStreamSynchronize(g.stream) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFree(buf);
         return false;
     }
-    g.zrows = buf;
-    g.zsx = zsx;
-    g.zsy = zsy;
+    g.acopy = buf;
+    g.acopy_axis = axis;
+    g.asx = sx;
+    g.asy = sy;
+    g.asz = sz;
     return true;
 }
 
@@ -1377,15 +1385,20 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
         const char *eq = vr::tuning("VR_M7_QUAD");
         const bool m7_quad = qm == 7 && P.oblique && P.m7x == P.nx && P.m7y == P.ny &&
                              P.m7z == P.nz && !(eq && std::atoi(eq) == 0);
-        // side views (screen x along the volume's z) read the z-rows copy with
-        // the per-ray pipelined march instead of the quad march / x-row pipe
-        const bool side = !P.oblique ? false : std::fabs(desc->inv_view[8]) >= 0.95f;
-        if (side && qm >= 1 && qm <= 3 && (P.path == 0 || P.path == 2) && g.nb <= 8 &&
-            !vr::tuning("VR_PATH") && ensure_zrows()) {
+        // views whose screen x runs along the volume's z or y read that axis'
+        // rows copy with the per-ray pipelined march instead of the quad march /
+        // x-row pipe
+        const int axis = !P.oblique                               ? 0
+                         : std::fabs(desc->inv_view[8]) >= 0.95f ? 2
+                         : std::fabs(desc->inv_view[4]) >= 0.95f ? 1
+                                                                  : 0;
+        if (axis && qm >= 1 && qm <= 3 && (P.path == 0 || P.path == 2) && g.nb <= 8 &&
+            !vr::tuning("VR_PATH") && ensure_axis_copy(axis)) {
             P.path = 2;
-            P.zvol = g.zrows;
-            P.zsx = g.zsx;
-            P.zsy = g.zsy;
+            P.avol = g.acopy;
+            P.asx = g.asx;
+            P.asy = g.asy;
+            P.asz = g.asz;
         } else if (g.nb == 8 && ((P.path == 0 && qm >= 1 && qm <= 3) || m7_quad) &&
                    ensure_brick()) {
             P.bvol = g.brick;
@@ -1859,7 +1872,7 @@ int vr_release_stats(void) {
     release_stats();
     release_cstats();
     release_brick();  // the layout copies are derived from the records too
-    release_zrows();
+    release_axis_copy();
     return VR_OK;
 }
 

@@ -53,11 +53,11 @@ struct Params {
     // in records (brick_index); the launch passes it as vol with sy / sz = bsy / bsz
     const float *bvol;
     uint64_t bsy, bsz;
-    // z-rows copy of the records (B <= 8) for views whose screen x runs along
-    // the volume's z axis (side views): record (x, y, z) at x * zsx + y * zsy + z
-    // (zrows_index); the launch passes it as vol with sx / sy / sz = zsx / zsy / 1
-    const float *zvol;
-    uint64_t zsx, zsy;
+    // axis-rows copy of the records (B <= 8) for views whose screen x runs along
+    // the volume's y or z axis: record (x, y, z) at x * asx + y * asy + z * asz
+    // (axis_copy_strides); the launch passes it as vol with sx / sy / sz = asx / asy / asz
+    const float *avol;
+    uint64_t asx, asy, asz;
     uint64_t sx;                 // record stride of x (gather MODE 3 only; 1 in x rows)
     // fractal/template codec (methods 4/5/6): codebook int4 per voxel, templates
     // [ntpl][nb], (bin, value) errors [voxel][err_slots]
@@ -99,11 +99,18 @@ __host__ __device__ __forceinline__ uint64_t brick_index(uint64_t x, uint64_t y,
     return z * bsz + (y >> 1) * bsy + (x >> 1) * 4u + (y & 1u) * 2u + (x & 1u);
 }
 
-// Record index of voxel (x, y, z) in the z-rows copy: z fastest, then y, then x
-// (zsy = Z records per (x, y) row, zsx = Y * Z per x-plane).
-__host__ __device__ __forceinline__ uint64_t zrows_index(uint64_t x, uint64_t y, uint64_t z,
-                                                         uint64_t zsx, uint64_t zsy) {
-    return x * zsx + y * zsy + z;
+// Record strides of the axis-rows copy whose rows run along `axis` (1 = y,
+// 2 = z): that axis is contiguous, then the other two in x, y, z order of
+// increasing stride (y rows: y, x, z; z rows: z, y, x -- the z-slice order of
+// the x-row layout for the slowest axis where it can be kept).
+__host__ __device__ __forceinline__ void axis_copy_strides(int axis, uint64_t nx, uint64_t ny,
+                                                           uint64_t nz, uint64_t &sx,
+                                                           uint64_t &sy, uint64_t &sz) {
+    if (axis == 1) {
+        sy = 1; sx = ny; sz = nx * ny;
+    } else {
+        sz = 1; sy = nz; sx = nz * ny;
+    }
 }
 
 // Baked statistics planes (basicDataProcessing, vr_stats.hip): 16 x 2 x 1

@@ -88,9 +88,10 @@ hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, uint64
 // pitches bsy (records per brick row) and bsz (records per slice), brick_index
 hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t bsy,
                          uint64_t bsz, hipStream_t s);
-// z-rows copy of a B <= 8 volume (side views, vr_stats.hip): zrows_index strides
-hipError_t launch_zrows(const float *vol, const Params &P, float *out, uint64_t zsx, uint64_t zsy,
-                        hipStream_t s);
+// axis-rows copy of a B <= 8 volume (views along y / z, vr_stats.hip) with the
+// record strides of axis_copy_strides
+hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint64_t asx,
+                            uint64_t asy, uint64_t asz, hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,

@@ -2249,18 +2249,18 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         if constexpr (B == 1) {  // baked statistics (vr_stats.hip, bricked planes): paths 2, 7 only
             if (method <= 0) P.path = 2;
         }
-        if (P.path == 2 && P.zvol && method >= 1 && method <= 3) {
-            // side views on the z-rows copy (vr_api.cpp ensure_zrows): the same
-            // march, gathers addressed z-contiguous
-            note_kernel("k_march_pipe_zrows", B, method);
+        if (P.path == 2 && P.avol && method >= 1 && method <= 3) {
+            // views along the volume's y / z on the axis-rows copy (vr_api.cpp
+            // ensure_axis_copy): the same march, gathers addressed with its strides
+            note_kernel(P.asy == 1 ? "k_march_pipe_yrows" : "k_march_pipe_zrows", B, method);
             Params Q = P;
-            Q.sx = P.zsx;
-            Q.sy = P.zsy;
-            Q.sz = 1;
+            Q.sx = P.asx;
+            Q.sy = P.asy;
+            Q.sz = P.asz;
             switch (method) {
-            case 1: hipLaunchKernelGGL((k_march_pipe<B, 1, 3>), grid, block, occupancy_lds(P), s, P.zvol, Q); break;
-            case 2: hipLaunchKernelGGL((k_march_pipe<B, 2, 3>), grid, block, occupancy_lds(P), s, P.zvol, Q); break;
-            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3, 3>), grid, block, occupancy_lds(P), s, P.zvol, Q); break;
+            case 1: hipLaunchKernelGGL((k_march_pipe<B, 1, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+            case 2: hipLaunchKernelGGL((k_march_pipe<B, 2, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
             }
             return hipGetLastError();
         }

@@ -155,8 +155,8 @@ typedef float vr_f2a4 __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ vr_f2a4 load_pair64(const float *__restrict__ vol, uint64_t i) {
     return *reinterpret_cast<const vr_f2a4 *>(vol + i);
 }
-// MODE 0: records in x rows (P.sy / P.sz record pitches).  MODE 3: the z-rows
-// copy (P.sx / P.sy strides, z contiguous; zrows_index).  MODE 1 / 2: a baked
+// MODE 0: records in x rows (P.sy / P.sz record pitches).  MODE 3: an axis-rows
+// copy (P.sx / P.sy / P.sz strides; axis_copy_strides).  MODE 1 / 2: a baked
 // statistics plane (B = 1) in 16 x 2 x 1 bricks (plane_index; P.sy / P.sz the
 // plane pitches): each (y, z) row's x-pair is one 8-byte load; MODE 1 forms the
 // index with 24-bit multiplies in 32 bits (pitches < 2^24, plane < 2^32 floats:
@@ -194,17 +194,18 @@ __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Par
         rec[7][0] = ox ? d.y : d.x;
         return;
     }
-    if constexpr (MODE == 3) {  // z-rows copy: x and y strided, z contiguous
+    if constexpr (MODE == 3) {  // axis-rows copy: all three axes strided
         const uint64_t x0 = (uint64_t)f.x0 * P.sx, x1 = (uint64_t)f.x1 * P.sx;
         const uint64_t y0 = (uint64_t)f.y0 * P.sy, y1 = (uint64_t)f.y1 * P.sy;
-        load_rec<B>(vol, x0 + y0 + f.z0, rec[0]);
-        load_rec<B>(vol, x1 + y0 + f.z0, rec[1]);
-        load_rec<B>(vol, x0 + y1 + f.z0, rec[2]);
-        load_rec<B>(vol, x1 + y1 + f.z0, rec[3]);
-        load_rec<B>(vol, x0 + y0 + f.z1, rec[4]);
-        load_rec<B>(vol, x1 + y0 + f.z1, rec[5]);
-        load_rec<B>(vol, x0 + y1 + f.z1, rec[6]);
-        load_rec<B>(vol, x1 + y1 + f.z1, rec[7]);
+        const uint64_t z0 = (uint64_t)f.z0 * P.sz, z1 = (uint64_t)f.z1 * P.sz;
+        load_rec<B>(vol, x0 + y0 + z0, rec[0]);
+        load_rec<B>(vol, x1 + y0 + z0, rec[1]);
+        load_rec<B>(vol, x0 + y1 + z0, rec[2]);
+        load_rec<B>(vol, x1 + y1 + z0, rec[3]);
+        load_rec<B>(vol, x0 + y0 + z1, rec[4]);
+        load_rec<B>(vol, x1 + y0 + z1, rec[5]);
+        load_rec<B>(vol, x0 + y1 + z1, rec[6]);
+        load_rec<B>(vol, x1 + y1 + z1, rec[7]);
         return;
     }
     const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;

@@ -140,29 +140,30 @@ __global__ __launch_bounds__(256) void k_brick8(const float *__restrict__ vol, P
     d4[1] = b;
 }
 
-// z-rows copy (side views): one thread per record, x-row reads coalesced
+// axis-rows copy (views along y / z): one thread per record, x-row reads coalesced
 template <int B>
-__global__ __launch_bounds__(256) void k_zrows(const float *__restrict__ vol, Params P,
-                                               float *__restrict__ out, uint64_t zsx, uint64_t zsy) {
+__global__ __launch_bounds__(256) void k_axis_copy(const float *__restrict__ vol, Params P,
+                                                   float *__restrict__ out, uint64_t asx,
+                                                   uint64_t asy, uint64_t asz) {
     const uint32_t x = blockIdx.x * 256u + threadIdx.x;
     if (x >= (uint32_t)P.nx) return;
     const uint32_t y = blockIdx.y, z = blockIdx.z;
     float r[B];
     load_rec<B>(vol, (uint64_t)z * P.sz + (uint64_t)y * P.sy + x, r);
-    float *d = out + zrows_index(x, y, z, zsx, zsy) * B;
+    float *d = out + (x * asx + y * asy + z * asz) * B;
 #pragma unroll
     for (int i = 0; i < B; i++) d[i] = r[i];
 }
 
-hipError_t launch_zrows(const float *vol, const Params &P, float *out, uint64_t zsx, uint64_t zsy,
-                        hipStream_t s) {
+hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint64_t asx,
+                            uint64_t asy, uint64_t asz, hipStream_t s) {
     dim3 grid;
     if (!bake_grid(P, grid)) return hipErrorInvalidValue;
     switch (P.nb) {
-    case 1: hipLaunchKernelGGL(k_zrows<1>, grid, dim3(256), 0, s, vol, P, out, zsx, zsy); break;
-    case 2: hipLaunchKernelGGL(k_zrows<2>, grid, dim3(256), 0, s, vol, P, out, zsx, zsy); break;
-    case 4: hipLaunchKernelGGL(k_zrows<4>, grid, dim3(256), 0, s, vol, P, out, zsx, zsy); break;
-    case 8: hipLaunchKernelGGL(k_zrows<8>, grid, dim3(256), 0, s, vol, P, out, zsx, zsy); break;
+    case 1: hipLaunchKernelGGL(k_axis_copy<1>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
+    case 2: hipLaunchKernelGGL(k_axis_copy<2>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
+    case 4: hipLaunchKernelGGL(k_axis_copy<4>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
+    case 8: hipLaunchKernelGGL(k_axis_copy<8>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
