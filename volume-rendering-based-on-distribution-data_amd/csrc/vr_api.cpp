@@ -542,6 +542,19 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
     P.oblique = along_rows ? 0 : 1;
     device_lds(P.lds_cu, P.lds_wg);
+    // Views whose screen x runs along the volume's z or y (|M[8]| / |M[4]| >=
+    // 0.95) march an axis-rows copy of an owned B <= 8 volume with the per-ray
+    // pipelined march (ensure_axis_copy); for the choices below
+    // they count as row-aligned (their x-row seg / quad alternatives read the
+    // x rows across).  VR_ZROWS=0 keeps them oblique.
+    const char *ez = vr::tuning("VR_ZROWS");
+    P.axis_view = 0;
+    if (!along_rows && !codec && !flex && g.owned && d->query_method >= 1 &&
+        d->query_method <= 3 && (g.nb == 1 || g.nb == 2 || g.nb == 4 || g.nb == 8) &&
+        !(ez && std::atoi(ez) == 0))
+        P.axis_view = std::fabs(d->inv_view[8]) >= 0.95f ? 2 : std::fabs(d->inv_view[4]) >= 0.95f ? 1 : 0;
+    const bool row_like = along_rows || P.axis_view != 0;
+    if (P.axis_view) P.path = 2;
     // Launches of few rays (a rank's tile list at 4 or 8 GPUs, 1080p) are bound
     // by the per-ray step chain, not by HBM: there the pipelined ray-segmented
     // march (2 lanes per ray, next window gathered before this one decodes,
@@ -562,7 +575,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // pipelined 2-lane segmented march beats the quad march (512^3 x 8 C1: m1
     // 2.05 -> 1.77 ms, m2 1.87 -> 1.63; at 1024^3, 2 pixels per voxel, the quad
     // march stays ahead: 3.49 vs 5.23 ms; profiles/r02/paths_512x8.log).
-    if (!along_rows && g.nb == 8 && (d->query_method == 1 || d->query_method == 2) &&
+    if (!row_like && g.nb == 8 && (d->query_method == 1 || d->query_method == 2) &&
         (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
         P.path = 7;
     // Row-aligned full frames of such a coarse volume: a wave's 64 rays cover
@@ -593,17 +606,21 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     int small_seg = 0;
     {
         const uint64_t rays = (uint64_t)d->width * d->height;
-        const bool nb_ok = g.nb == 1 || g.nb == 2 || g.nb == 4 || (g.nb == 8 && along_rows);
-        const uint64_t limit = along_rows ? std::min<uint64_t>(seg_rays, 131072) : seg_rays;
+        const bool nb_ok = g.nb == 1 || g.nb == 2 || g.nb == 4 || (g.nb == 8 && row_like);
+        const uint64_t limit = row_like ? std::min<uint64_t>(seg_rays, 131072) : seg_rays;
         if (!d->d_tile_list && !codec && !flex && rays <= limit && nb_ok &&
             (d->query_method == 1 || d->query_method == 2)) {
             P.path = 7;
             small_seg = rays <= 131072 ? -4 : -2;
         }
     }
+    if (P.path != 2) P.axis_view = 0;  // a small frame keeps the segmented march
     if (const char *e = vr::tuning("VR_PATH")) {
         const int v = std::atoi(e);
-        if (v == 0 || v == 1 || v == 2 || v == 4 || v == 7) P.path = v;
+        if (v == 0 || v == 1 || v == 2 || v == 4 || v == 7) {
+            P.path = v;
+            P.axis_view = 0;  // a forced path reads the x rows
+        }
     }
     P.wave_clock = g.wave_clock;
     P.tile_cost = record;
@@ -1386,15 +1403,13 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
         const bool m7_quad = qm == 7 && P.oblique && P.m7x == P.nx && P.m7y == P.ny &&
                              P.m7z == P.nz && !(eq && std::atoi(eq) == 0);
         // views whose screen x runs along the volume's z or y read that axis'
-        // rows copy with the per-ray pipelined march instead of the quad march /
-        // x-row pipe
-        const int axis = !P.oblique                               ? 0
-                         : std::fabs(desc->inv_view[8]) >= 0.95f ? 2
-                         : std::fabs(desc->inv_view[4]) >= 0.95f ? 1
-                                                                  : 0;
-        if (axis && qm >= 1 && qm <= 3 && (P.path == 0 || P.path == 2) && g.nb <= 8 &&
-            !vr::tuning("VR_PATH") && ensure_axis_copy(axis)) {
-            P.path = 2;
+        // rows copy with the per-ray pipelined march (fill_params); if the copy
+        // cannot be made (HBM), the oblique view's march on the x rows / bricks
+        if (P.axis_view && !ensure_axis_copy(P.axis_view)) {
+            P.axis_view = 0;
+            P.path = 0;
+        }
+        if (P.axis_view) {
             P.avol = g.acopy;
             P.asx = g.asx;
             P.asy = g.asy;

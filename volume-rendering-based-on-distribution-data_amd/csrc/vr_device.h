@@ -58,6 +58,7 @@ struct Params {
     // (axis_copy_strides); the launch passes it as vol with sx / sy / sz = asx / asy / asz
     const float *avol;
     uint64_t asx, asy, asz;
+    int axis_view;               // host dispatch: 1 / 2 = the view runs along y / z (fill_params)
     uint64_t sx;                 // record stride of x (gather MODE 3 only; 1 in x rows)
     // fractal/template codec (methods 4/5/6): codebook int4 per voxel, templates
     // [ntpl][nb], (bin, value) errors [voxel][err_slots]
