@@ -57,7 +57,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="1024x8", choices=sorted(CONFIGS) + sorted(GMM_CONFIGS))
     ap.add_argument("--method", type=int, default=1, choices=[1, 2, 3, 4, 5, 6, 7])
-    ap.add_argument("--camera", default="C0", choices=["C0", "C1"])
+    ap.add_argument("--camera", default="C0", choices=["C0", "C1", "S"],
+                    help="C0 runSingleTest (C:1024-1043), C1 display() at (30, 45) deg, "
+                         "S display() at yaw 90 deg (screen x along the volume's z)")
     ap.add_argument("--baked", action="store_true",
                     help="basicDataProcessing first: frames filter the baked statistics "
                          "planes (vr_stats.hip) instead of decoding records per step")
@@ -75,6 +77,12 @@ def parse():
                     help="PMC-measured HBM bytes per launch (tools/pmc_traffic.py) for "
                          "roofline.traffic; used only when the kernel matches")
     return ap.parse_args()
+
+
+def camera_matrix(pkg, cam):
+    if cam == "C0":
+        return pkg.camera.single_test_inv_view()
+    return pkg.camera.display_inv_view((0.0, 90.0) if cam == "S" else (30.0, 45.0))
 
 
 def lib_sha16(path):
@@ -303,8 +311,7 @@ def main_gmm(args):
     n, K, W, H = GMM_CONFIGS[args.config]
     if args.method not in (1, 2):
         raise SystemExit("GMM volumes support --method 1 (mean) and 2 (variance)")
-    m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
-         else pkg.camera.display_inv_view((30.0, 45.0)))
+    m = camera_matrix(pkg, args.camera)
     rec_bytes = 8 * K if args.method == 1 else 12 * K
     free, _ = torch.cuda.mem_get_info(dev)
     stream = torch.cuda.Stream(device=dev)
@@ -526,8 +533,7 @@ def main():
 
     pkg = graft.load_package()
     n, nb, W, H = CONFIGS[args.config]
-    m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
-         else pkg.camera.display_inv_view((30.0, 45.0)))
+    m = camera_matrix(pkg, args.camera)
 
     stream = torch.cuda.Stream(device=dev)
     pkg.set_stream(stream)

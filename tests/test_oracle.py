@@ -296,3 +296,25 @@ def test_bin_centres_fit_29_bits(nb):
     for i in range(nb):
         c = float(np.float32(bw * np.float32(i))) + half
         assert _sig_bits(c) <= 29, (nb, i, c)
+
+
+def test_config1_at_size_matches_numpy(orc, cams):
+    """BASELINE config 1 at its own size -- 128^3 x 1-bin volume, 256 x 256 -- the
+    CPU-only case: the oracle's whole frame equals the independent numpy
+    restatement (both cameras, methods 1 and 7) and the frame's
+    known answers hold (misses untouched, ~44.5 % hits at C0)"""
+    vol = orc.synth_volume(128, 128, 128, 1)
+    W = H = 256
+    for cam in ("C0", "C1"):
+        for method in (1, 7):
+            p = orc.make_params(W, H, cams[cam], query_method=method, m7_dims=(128, 128, 128))
+            o8, of, on, _ = orc.render(vol, p, nthreads=0)
+            f, n = rn.render(vol, W, H, cams[cam], method, m7_dims=(128, 128, 128))
+            rows = slice(0, H, 1)
+            assert np.array_equal(n[rows], on[rows]), f"{cam} m{method}: samples differ"
+            assert np.array_equal(f[rows], of[rows]), f"{cam} m{method}: RGBA differs"
+            assert np.array_equal(np.where(n[rows] >= 0, rn.pack(f[rows]), 0), o8[rows])
+            miss = on < 0
+            assert np.all(o8[miss] == 0)
+            if cam == "C0":
+                assert abs(float(np.mean(~miss)) - 0.445) < 0.01
