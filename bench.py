@@ -64,6 +64,10 @@ def parse():
                     help="basicDataProcessing first: frames filter the baked statistics "
                          "planes (vr_stats.hip) instead of decoding records per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-issue-bounds", action="store_true",
+                    help="skip the untimed one-tile latency probe (roofline.issue_bounds): "
+                         "profiling runs use it so a kernel's rocprofv3 average holds only "
+                         "whole-frame launches")
     ap.add_argument("--no-balance", action="store_true",
                     help="N > 1: keep the estimate-dealt tile lists (no measured-cost re-deal)")
     ap.add_argument("--dump-frame", default="",
@@ -655,7 +659,7 @@ def main():
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     # the bounds that apply when the frame is not HBM-bound (the smaller configs)
     bounds = (issue_bounds(pkg, torch, stream, W, H, m, args.method, kern_ms, pmc)
-              if world == 1 else None)
+              if world == 1 and not args.no_issue_bounds else None)
 
     # parity of the timed frame's view (untimed; full frames at N = 1 are checked
     # against the oracle frame of the CPU baseline below, N > 1 assembled frames
