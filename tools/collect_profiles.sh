@@ -16,7 +16,7 @@ for f in $R/bench_*.log; do
 done
 for c in C0 C1; do [ -f $R/rank_sim_$c.log ] && grep -v amdgpu.ids $R/rank_sim_$c.log > $D/rank_sim_1024x8_$c.log; done
 [ -f $R/pytest_gpu.log ] && cp $R/pytest_gpu.log $D/pytest_gpu.log
-python3 - "$R/traffic.json" <<'PY'
+[ -f $R/traffic.json ] && python3 - "$R/traffic.json" <<'PY'
 import json, sys
 new = json.load(open(sys.argv[1]))
 db = json.load(open("profiles/traffic.json"))
@@ -25,3 +25,4 @@ json.dump(db, open("profiles/traffic.json", "w"), indent=1, sort_keys=True)
 print("traffic.json:", sorted(new))
 PY
 ls $D
+true
