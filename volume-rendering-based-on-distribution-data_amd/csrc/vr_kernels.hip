@@ -232,7 +232,12 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
     const uint32_t lane = threadIdx.x & 63u;
     float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
     uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
+    if (P.wq_map) {  // a wave takes a 16x4 pixel block (a compact footprint box)
+        lx = (threadIdx.x >> 6) * 16u + ((threadIdx.x & 63u) >> 2);
+        ly = threadIdx.x & 3u;
+    } else {
+        tile_pixel(threadIdx.x, lx, ly);
+    }
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     const bool valid = x < P.CW && y < P.CH;
@@ -2326,6 +2331,10 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         }
     }
     if (!COUNT) note_kernel(method == 7 ? "k_march_m7" : "k_march", B, method);
+    if (method >= 1 && method <= 3) {
+        P.wq_map = 0;  // the LDS-box march: a 64-pixel row per wave unless VR_BOX_MAP
+        if (const char *em = tuning("VR_BOX_MAP")) P.wq_map = std::atoi(em) != 0;
+    }
     switch (method) {
     case 0:
     case -1:  // baked statistics: the pipelined / segmented marches only (bricked planes)
