@@ -951,3 +951,23 @@ def test_axis_views_take_an_axis_rows_copy(pkg, orc, gpu, nb, tune):
     got = gpu_render(pkg, None, W, H, m, 1, torch)
     assert not pkg.last_kernel().startswith("k_march_pipe_zrows"), pkg.last_kernel()
     assert_parity(got, orc.render(vol2, orc.make_params(W, H, m, query_method=1))[:3], "x rows")
+
+
+def test_wide32_row_aligned_frames_take_box_march(pkg, orc, gpu, tune):
+    """32-bin records, row-aligned full frames above the segmented threshold, a
+    volume fine for the frame: the LDS-box march with 16x4-pixel wave blocks
+    (decode once per wave-step), methods 1/2/3, bit-identical; the 64-pixel-row
+    box (VR_BOX_MAP=0) too"""
+    import torch
+    tune.set("VR_SEG_RAYS", "1000")
+    vol = orc.synth_volume(60, 50, 20, 32)
+    pkg.init_distribution(vol)
+    m = pkg.camera.display_inv_view((0.0, 0.0), translation=(0.05, -0.1, 0.0))
+    W, H = 96, 64  # 6144 rays < 4 x 60 x 50 pixels per voxel face
+    for bmap in ("1", "0"):
+        tune.set("VR_BOX_MAP", bmap)
+        for method in (1, 2, 3):
+            got = gpu_render(pkg, None, W, H, m, method, torch)
+            assert pkg.last_kernel().startswith("k_march<B=32"), pkg.last_kernel()
+            ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+            assert_parity(got, ref, f"32 bins box map {bmap} m{method}")

@@ -595,6 +595,14 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         (uint64_t)d->width * d->height > seg_rays &&
         (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
         P.path = 1;
+    // 32-bin records (the reference's own width) are decode-bound at any volume
+    // size, and with a 16x4-pixel block per wave the box decodes each record
+    // once per wave-step instead of once per touching ray: row-aligned full
+    // frames at 1024^3 x 32, 1080p, C0: m1 6.67 -> 6.18 ms, m2 10.42 -> 9.05,
+    // m3 41.0 -> 35.0 (16 bins: no gain; profiles/r03/box_map.log)
+    if (along_rows && !d->d_tile_list && g.nb == 32 && d->query_method >= 1 &&
+        d->query_method <= 3 && (uint64_t)d->width * d->height > seg_rays)
+        P.path = 1;
     // Small full frames (BASELINE configs 1 and 2: 128^3 x 1 at 256^2, 256^3 x 4
     // at 512^2) cannot fill the GPU with one ray per lane, so the per-ray step
     // chain sets the time, as for a rank's tile list: the pipelined
