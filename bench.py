@@ -65,7 +65,7 @@ def parse():
                          "planes (vr_stats.hip) instead of decoding records per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-issue-bounds", action="store_true",
-                    help="skip the untimed one-tile latency probe (roofline.issue_bounds): "
+                    help="skip the untimed one-tile latency probe (roofline.compute): "
                          "profiling runs use it so a kernel's rocprofv3 average holds only "
                          "whole-frame launches")
     ap.add_argument("--no-balance", action="store_true",
@@ -124,7 +124,7 @@ VALU_ISSUE_CYCLES = 2      # SIMD cycles per f32 wave64 VALU instruction (f64 ad
 SIMDS, CLOCK_HZ = 1024, 2.4e9  # tools/valu_calib.hip); 256 CUs x 4 SIMDs at 2.4 GHz
 
 
-def issue_bounds(pkg, torch, stream, W, H, m, method, kern_ms, pmc):
+def compute_bounds(pkg, torch, stream, W, H, m, method, kern_ms, pmc):
     """The bounds of a launch that is not HBM-bound:
     latency -- the frame cannot end before its longest tile's step chain does: the
     longest-ray tile rendered ALONE (one 64x4 tile, its list entry first in the
@@ -658,7 +658,7 @@ def main():
     pmc, traffic_src = traffic_entry(args, kernel, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     # the bounds that apply when the frame is not HBM-bound (the smaller configs)
-    bounds = (issue_bounds(pkg, torch, stream, W, H, m, args.method, kern_ms, pmc)
+    bounds = (compute_bounds(pkg, torch, stream, W, H, m, args.method, kern_ms, pmc)
               if world == 1 and not args.no_issue_bounds else None)
 
     # parity of the timed frame's view (untimed; full frames at N = 1 are checked
@@ -731,7 +731,7 @@ def main():
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
                 "U_records": int(u) if u is not None else None,
-                "issue_bounds": bounds,
+                "compute": bounds,
             },
             "parity": parity,
             "cpu_baseline": cpu,

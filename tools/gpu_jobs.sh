@@ -1,0 +1,34 @@
+#!/bin/bash
+# Named GPU experiments of round 3 (each writes gpurun_out/<job>/ and is the
+# source of the profiles/r03 log named beside it).  The round's bench lines,
+# kernel traces and PMC passes: tools/gpu_round.sh; the GPU suite: tools/gpu_suite.sh.
+#   bash tools/gpu_jobs.sh sweep   -> rot_sweep_1024x8*.log, rot_sweep_512x8_axis_copies.log
+#   bash tools/gpu_jobs.sh calib   -> valu_calib.log, valu_calib_pmc.csv
+#   bash tools/gpu_jobs.sh steps   -> gpurun_out/steps_C*.npy for tools/footprint_sim.c (footprint_planes.log)
+#   bash tools/gpu_jobs.sh box     -> box_map.log (LDS-box march: wave maps, wide records, oblique views)
+#   bash tools/gpu_jobs.sh ranks   -> rank_sim_1024x8_C*.log
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
+J=${1:?job}; O=gpurun_out/$J; mkdir -p $O
+guard() { rc=$1; if [ $rc -ne 0 ]; then echo "$2 failed rc=$rc"; tail -30 $3; exit $rc; fi; }
+case $J in
+sweep)
+  timeout -k 10 400 python -u tools/rot_sweep.py --rx 0,30,90 --step 10 > $O/rot_1024x8.log 2>&1; guard $? rot $O/rot_1024x8.log
+  timeout -k 10 300 python -u tools/rot_sweep.py --config 512x8 --rx 0 --step 10 --paths 7 > $O/rot_512x8.log 2>&1; guard $? rot512 $O/rot_512x8.log ;;
+calib)
+  mkdir -p tools/build && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/valu_calib.hip -o tools/build/valu_calib 2> /dev/null || exit 1
+  timeout -k 10 120 tools/build/valu_calib > $O/valu_calib.log 2>&1; guard $? calib $O/valu_calib.log
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/pmc -o calib -- tools/build/valu_calib > $O/pmc.log 2>&1; guard $? pmc $O/pmc.log ;;
+steps)
+  timeout -k 10 300 python -u tools/dump_steps.py > $O/dump.log 2>&1; guard $? dump $O/dump.log ;;
+box)
+  for CC in 512x8:1:C0 512x8:2:C0 1024x8:1:C0 1024x16:1:C0 1024x16:2:C0 1024x16:3:C0 1024x32:1:C0 1024x32:2:C0 1024x32:3:C0 512x8:1:C1 1024x32:1:C1; do
+    IFS=: read CFG M CAM <<< "$CC"
+    timeout -k 10 400 python -u tools/bench_variants.py --config $CFG --rounds 2 --reps 3 --method $M --cameras $CAM --env "" "VR_PATH=1" "VR_PATH=1,VR_BOX_MAP=0" > $O/box_${CFG}_m${M}_$CAM.log 2>&1; guard $? box-$CC $O/box_${CFG}_m${M}_$CAM.log
+  done ;;
+ranks)
+  for CAM in C0 C1; do
+    timeout -k 10 300 python -u tools/rank_sim.py --camera $CAM > $O/rank_sim_$CAM.log 2>&1; guard $? rank-$CAM $O/rank_sim_$CAM.log
+  done ;;
+*) echo "unknown job $J"; exit 2 ;;
+esac
+echo done

@@ -38,7 +38,7 @@ def per_dispatch(dirs):
                 if "vr::k_march" not in k or ", true>" in k and ("vr::k_march<" in k or
                                                                   "vr::k_march_gmm<" in k):
                     continue  # the march only (not the footprint-counting variants)
-                # a kernel is keyed with its grid: bench.py's one-tile latency probe
+                # a kernel is keyed with its grid: bench.py's one-tile latency probe (roofline.compute)
                 # may launch the frame's own kernel on a 256-thread grid
                 k = (k, int(r["Grid_Size"]))
                 rows[(k, r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
@@ -50,7 +50,7 @@ def per_dispatch(dirs):
     if not names:
         raise SystemExit("no march dispatches in the PMC output")
     # the frame's launch: the largest grid (bench.py also launches a one-tile
-    # latency probe, issue_bounds, several times), then the most dispatches
+    # latency probe, roofline.compute, several times), then the most dispatches
     kernel = max(names, key=lambda k: (grids[k], names[k]))
     return kernel[0], {c: sum(v) / len(v) for c, v in vals[kernel].items()}
 
