@@ -126,8 +126,11 @@ void dataProcessing(void);
  * Layout copy: the first oblique-view frame of a library-owned 8-bin volume
  * makes a second, 2x2 (x, y) micro-brick copy of its records (DESIGN.md 4.6;
  * as many bytes as the volume, made synchronously, only while HBM keeps
- * max(4 GiB, 5 %) free after it).  vr_release_stats drops it with the planes,
- * so after an in-place modification the next oblique frame rebuilds it. */
+ * max(4 GiB, 5 %) free after it).  Views whose screen x runs along the volume's
+ * z or y axis (|M[8]| or |M[4]| >= 0.95) of an owned volume with 1, 2, 4 or 8
+ * bins get an axis-rows copy (that axis contiguous) on the same terms, one
+ * axis at a time.  vr_release_stats drops the copies with the planes, so after
+ * an in-place modification the next frame that needs one rebuilds it. */
 int vr_bake_stats(void);
 int vr_release_stats(void);
 int vr_stats_info(const float **d_raw, uint64_t *raw_plane, const float **d_codec,
