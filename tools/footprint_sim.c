@@ -22,7 +22,7 @@ static int PF = 0;
 static int ALIGN = 0; /* 1: per-step scopes count a ray's sample s at iteration s + its depth
                          offset round((tnear - tnear_min of the tile) / 0.01) */
 static int LAYOUT = 0; /* 0: x-rows (4 records along x per line), 1: 2x2 (x,y) micro-bricks,
-                          2: 2x1x2 (x,z) micro-bricks */
+                          2: 2x1x2 (x,z) micro-bricks, 3: 1x2x2 (y,z) micro-bricks */
 
 /* LAYOUT=10: baked statistics planes, 4-B voxels, 32 per line, bricks of
    BX x BY x BZ voxels (BX*BY*BZ = 32; default 32x1x1 = x-rows) */
@@ -34,6 +34,8 @@ static uint32_t line_of(uint32_t x, uint32_t y, uint32_t z) {
         return (uint32_t)(((uint64_t)z * (N / 2) + (y >> 1)) * (N / 2) + (x >> 1));
     if (LAYOUT == 2)
         return (uint32_t)(((uint64_t)(z >> 1) * N + y) * (N / 2) + (x >> 1));
+    if (LAYOUT == 3)  /* 1x2x2 (y,z) micro-bricks: a line = 2 y x 2 z records at one x */
+        return (uint32_t)(((uint64_t)(z >> 1) * (N / 2) + (y >> 1)) * N + x);
     return (uint32_t)((((uint64_t)z * N + y) * N + x) >> 2);
 }
 
