@@ -89,6 +89,12 @@ def lib():
         L.orc_render_gmm_rows.argtypes = [ctypes.POINTER(Gmm), ctypes.POINTER(RenderParams),
                                           ctypes.c_int, ctypes.c_int, u32p, ctypes.c_int]
         L.orc_render_gmm_rows.restype = ctypes.c_int64
+        L.orc_gmm_proc_new.argtypes = [ctypes.c_int] * 4 + [ctypes.c_uint64]
+        L.orc_gmm_proc_new.restype = ctypes.c_void_p
+        L.orc_gmm_proc_free.argtypes = [ctypes.c_void_p]
+        L.orc_render_gmm_rows_proc.argtypes = [ctypes.c_void_p, ctypes.POINTER(RenderParams),
+                                               i32p, ctypes.c_int, u32p, i32p, ctypes.c_int]
+        L.orc_render_gmm_rows_proc.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -491,3 +497,31 @@ def render_gmm_rows(wm, sg, dims, params, row_lo, row_hi, nthreads=0):
     s = lib().orc_render_gmm_rows(ctypes.byref(g), ctypes.byref(params), int(row_lo), int(row_hi),
                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), nthreads)
     return out, int(s)
+
+
+def render_gmm_rows_proc(dims, K, params, rows, seed=20261015, nthreads=0):
+    """whole-volume GMM render of the given frame rows with every record computed
+    from its voxel index as a sample reads it (the generator of synth_gmm, no
+    resident volume): for frames of volumes no host holds (config 5, 2048^3 x 16
+    = 1.65 TB).  Returns (out (len(rows), W) uint32, out_n (len(rows), W) int32,
+    -1 where the ray misses the box), samples"""
+    nx, ny, nz = (int(v) for v in dims)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    if rows.size and (rows.min() < 0 or rows.max() >= params.height):
+        raise ValueError("row outside the frame")
+    W = params.width
+    out = np.zeros((rows.size, W), np.uint32)
+    out_n = np.zeros((rows.size, W), np.int32)
+    g = lib().orc_gmm_proc_new(nx, ny, nz, int(K), int(seed))
+    if not g:
+        raise MemoryError("orc_gmm_proc_new")
+    try:
+        s = lib().orc_render_gmm_rows_proc(
+            g, ctypes.byref(params), rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            int(rows.size), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+            out_n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(nthreads))
+    finally:
+        lib().orc_gmm_proc_free(g)
+    if s < 0:
+        raise ValueError(f"K = {K}: the GMM march takes 4..32 components")
+    return out, out_n, int(s)

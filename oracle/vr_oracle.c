@@ -939,58 +939,91 @@ float orc_gmm_stat(const float *wm, const float *sg, int K, int method) {
     return (q - mm) * 16.0f;
 }
 
-void orc_synth_gmm(int nx, int ny, int nz, int K, uint64_t seed, int z_base, int nzs, float *wm,
-                   float *sg, int nthreads) {
+/* the generator's per-axis Gaussian tables; one voxel's
+ * records follow from them and the voxel index alone (gmm_voxel), so the
+ * resident slices and the procedural source below give identical records */
+struct orc_gmm_proc {
+    int nx, ny, nz, K;
+    uint64_t seed;
     float amp[SYN_K];
-    float *gx = (float *)malloc(sizeof(float) * SYN_K * (size_t)nx);
-    float *gy = (float *)malloc(sizeof(float) * SYN_K * (size_t)ny);
-    float *gz = (float *)malloc(sizeof(float) * SYN_K * (size_t)nz);
+    float *gx, *gy, *gz;
+};
+
+orc_gmm_proc *orc_gmm_proc_new(int nx, int ny, int nz, int K, uint64_t seed) {
+    orc_gmm_proc *g = (orc_gmm_proc *)calloc(1, sizeof *g);
+    if (!g) return NULL;
+    g->nx = nx; g->ny = ny; g->nz = nz; g->K = K; g->seed = seed;
+    g->gx = (float *)malloc(sizeof(float) * SYN_K * (size_t)nx);
+    g->gy = (float *)malloc(sizeof(float) * SYN_K * (size_t)ny);
+    g->gz = (float *)malloc(sizeof(float) * SYN_K * (size_t)nz);
+    if (!g->gx || !g->gy || !g->gz) {
+        orc_gmm_proc_free(g);
+        return NULL;
+    }
     for (int k = 0; k < SYN_K; k++) {
         double r[5];
         for (int j = 0; j < 5; j++) r[j] = u01(orc_splitmix64(seed + 0x100u + 8u * (uint64_t)k + (uint64_t)j));
-        amp[k] = (float)(0.3 + 0.7 * r[0]);
-        double s = 0.05 + 0.15 * r[4];
-        axis_table(nx, 0.2 + 0.6 * r[1], s, gx + (size_t)k * nx);
-        axis_table(ny, 0.2 + 0.6 * r[2], s, gy + (size_t)k * ny);
-        axis_table(nz, 0.2 + 0.6 * r[3], s, gz + (size_t)k * nz);
+        g->amp[k] = (float)(0.3 + 0.7 * r[0]);
+        double sd = 0.05 + 0.15 * r[4];
+        axis_table(nx, 0.2 + 0.6 * r[1], sd, g->gx + (size_t)k * nx);
+        axis_table(ny, 0.2 + 0.6 * r[2], sd, g->gy + (size_t)k * ny);
+        axis_table(nz, 0.2 + 0.6 * r[3], sd, g->gz + (size_t)k * nz);
     }
+    return g;
+}
+
+void orc_gmm_proc_free(orc_gmm_proc *g) {
+    if (!g) return;
+    free(g->gx);
+    free(g->gy);
+    free(g->gz);
+    free(g);
+}
+
+/* records of voxel (x, y, z): wm[K][2] (w, mu), sg[K] */
+static void gmm_voxel(const orc_gmm_proc *g, int x, int y, int z, float *wm, float *sg) {
+    const int nx = g->nx, ny = g->ny, K = g->K;
+    float f = 0.0f;
+    for (int k = 0; k < SYN_K; k++)
+        f = f + ((g->amp[k] * g->gx[(size_t)k * nx + x]) * g->gy[(size_t)k * ny + y]) *
+                    g->gz[(size_t)k * g->nz + z];
+    if (f > 1.0f) f = 1.0f;
+    const uint64_t v = ((uint64_t)z * (uint64_t)ny + (uint64_t)y) * (uint64_t)nx + (uint64_t)x;
+    float sum = 0.0f;
+    for (int k = 0; k < K; k++) {
+        uint64_t h = orc_splitmix64(g->seed ^ 0x6A09E667F3BCC909ull ^ (v * (uint64_t)K + (uint64_t)k));
+        sum = sum + (0.05f + (float)((h >> 16) & 0xFFFFFFull) * 0x1p-24f);
+    }
+    for (int k = 0; k < K; k++) {
+        uint64_t h = orc_splitmix64(g->seed ^ 0x6A09E667F3BCC909ull ^ (v * (uint64_t)K + (uint64_t)k));
+        const float u = (float)(h >> 40) * 0x1p-24f;
+        const float r = 0.05f + (float)((h >> 16) & 0xFFFFFFull) * 0x1p-24f;
+        float mu = (f * 0.8f + 0.1f) + (u - 0.5f) * 0.2f;
+        mu = fminf(fmaxf(mu, 0.0f), 1.0f);
+        wm[2 * k] = r / sum;
+        wm[2 * k + 1] = mu;
+        sg[k] = ((float)(h & 0xFFFFull) * 0x1p-16f) * 0.05f + 0.005f;
+    }
+}
+
+void orc_synth_gmm(int nx, int ny, int nz, int K, uint64_t seed, int z_base, int nzs, float *wm,
+                   float *sg, int nthreads) {
+    orc_gmm_proc *g = orc_gmm_proc_new(nx, ny, nz, K, seed);
+    if (!g) return;
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel for schedule(static) num_threads(nthreads)
 #endif
     for (int zl = 0; zl < nzs; zl++) {
-        const int z = zl + z_base;
         for (int y = 0; y < ny; y++) {
             for (int x = 0; x < nx; x++) {
-                float f = 0.0f;
-                for (int k = 0; k < SYN_K; k++)
-                    f = f + ((amp[k] * gx[(size_t)k * nx + x]) * gy[(size_t)k * ny + y]) *
-                                gz[(size_t)k * nz + z];
-                if (f > 1.0f) f = 1.0f;
-                const uint64_t v = ((uint64_t)z * (uint64_t)ny + (uint64_t)y) * (uint64_t)nx + (uint64_t)x;
                 const uint64_t lv = ((uint64_t)zl * (uint64_t)ny + (uint64_t)y) * (uint64_t)nx + (uint64_t)x;
-                float sum = 0.0f;
-                for (int k = 0; k < K; k++) {
-                    uint64_t h = orc_splitmix64(seed ^ 0x6A09E667F3BCC909ull ^ (v * (uint64_t)K + (uint64_t)k));
-                    sum = sum + (0.05f + (float)((h >> 16) & 0xFFFFFFull) * 0x1p-24f);
-                }
-                for (int k = 0; k < K; k++) {
-                    uint64_t h = orc_splitmix64(seed ^ 0x6A09E667F3BCC909ull ^ (v * (uint64_t)K + (uint64_t)k));
-                    const float u = (float)(h >> 40) * 0x1p-24f;
-                    const float r = 0.05f + (float)((h >> 16) & 0xFFFFFFull) * 0x1p-24f;
-                    float mu = (f * 0.8f + 0.1f) + (u - 0.5f) * 0.2f;
-                    mu = fminf(fmaxf(mu, 0.0f), 1.0f);
-                    wm[(lv * (uint64_t)K + (uint64_t)k) * 2] = r / sum;
-                    wm[(lv * (uint64_t)K + (uint64_t)k) * 2 + 1] = mu;
-                    sg[lv * (uint64_t)K + (uint64_t)k] = ((float)(h & 0xFFFFull) * 0x1p-16f) * 0.05f + 0.005f;
-                }
+                gmm_voxel(g, x, y, zl + z_base, wm + lv * 2 * (uint64_t)K, sg + lv * (uint64_t)K);
             }
         }
     }
     (void)nthreads;
-    free(gx);
-    free(gy);
-    free(gz);
+    orc_gmm_proc_free(g);
 }
 
 /* eye ray + intersectBox (K:288-306), as render_pixel */
@@ -1035,8 +1068,10 @@ static inline void gmm_mark(const orc_gmm *v, uint64_t *mark, int x, int y, int 
 
 /* march one ray (state in/out) through the slab; returns 1 if it leaves the
  * slab alive, 0 if it ended (early exit, tfar, 500 samples) */
-static int gmm_march(const orc_gmm *v, const orc_render_params *p, int z_lo, int z_hi, int slab,
-                     f3 d, float tfar, orc_gmm_ray *s, uint64_t *mark) {
+static int gmm_march(const orc_gmm *v, const orc_gmm_proc *proc, const orc_render_params *p,
+                     int z_lo, int z_hi, int slab, f3 d, float tfar, orc_gmm_ray *s,
+                     uint64_t *mark) {
+    float pwm[64], psg[32]; /* proc: one voxel's records, K <= 32 */
     const f3 step = {d.x * 0.01f, d.y * 0.01f, d.z * 0.01f};
     for (;;) {
         int x0, x1, y0, y1, z0, z1;
@@ -1050,7 +1085,12 @@ static int gmm_march(const orc_gmm *v, const orc_render_params *p, int z_lo, int
         for (int j = 0; j < 8; j++) {
             const int X = xs[j & 1], Y = ys[(j >> 1) & 1], Z = zs[j >> 2];
             if (mark) gmm_mark(v, mark, X, Y, Z);
-            sv[j] = orc_gmm_stat(gmm_wm(v, X, Y, Z), gmm_sg(v, X, Y, Z), v->K, p->query_method);
+            if (proc) {
+                gmm_voxel(proc, X, Y, Z, pwm, psg);
+                sv[j] = orc_gmm_stat(pwm, psg, v->K, p->query_method);
+            } else {
+                sv[j] = orc_gmm_stat(gmm_wm(v, X, Y, Z), gmm_sg(v, X, Y, Z), v->K, p->query_method);
+            }
         }
         float c00 = lerpq(sv[0], sv[1], ax), c10 = lerpq(sv[2], sv[3], ax);
         float c01 = lerpq(sv[4], sv[5], ax), c11 = lerpq(sv[6], sv[7], ax);
@@ -1111,7 +1151,7 @@ int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, i
             s.pos[2] = o.z + d.z * tnear;
         }
         const uint32_t n0 = s.n;
-        const int alive = gmm_march(v, p, z_lo, z_hi, slab, d, tfar, &s, mark);
+        const int alive = gmm_march(v, NULL, p, z_lo, z_hi, slab, d, tfar, &s, mark);
         samples += (int64_t)(s.n - n0);
         if (alive) {
             rays_out[k_out++] = s;
@@ -1153,12 +1193,47 @@ int64_t orc_render_gmm_rows(const orc_gmm *v, const orc_render_params *p, int ro
             s.pos[0] = o.x + d.x * tnear;
             s.pos[1] = o.y + d.y * tnear;
             s.pos[2] = o.z + d.z * tnear;
-            gmm_march(v, p, 0, v->nz, 0, d, tfar, &s, NULL);
+            gmm_march(v, NULL, p, 0, v->nz, 0, d, tfar, &s, NULL);
             acc += s.n;
             const float rgba[4] = {s.sum[0] * p->brightness, s.sum[1] * p->brightness,
                                    s.sum[2] * p->brightness, s.sum[3] * p->brightness};
             if (out) out[s.pix] = orc_pack(rgba);
         }
+    }
+    (void)nthreads;
+    return acc;
+}
+
+int64_t orc_render_gmm_rows_proc(const orc_gmm_proc *g, const orc_render_params *p,
+                                 const int32_t *rows, int nrows, uint32_t *out, int32_t *out_n,
+                                 int nthreads) {
+    if (!g || g->K < 4 || g->K > 32) return -1;
+    const orc_gmm v = {NULL, NULL, g->nx, g->ny, g->nz, g->K, 0, g->nz};
+    const int W = p->width;
+    int64_t acc = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads) reduction(+ : acc)
+#endif
+    for (int64_t i = 0; i < (int64_t)nrows * W; i++) {
+        const int r = (int)(i / W), x = (int)(i % W), y = rows[r];
+        out[i] = 0;
+        out_n[i] = -1;
+        f3 o, d;
+        float tnear, tfar;
+        if (!gmm_ray(p, x, y, &o, &d, &tnear, &tfar)) continue;
+        orc_gmm_ray s;
+        memset(&s, 0, sizeof s);
+        s.t = tnear;
+        s.pos[0] = o.x + d.x * tnear;
+        s.pos[1] = o.y + d.y * tnear;
+        s.pos[2] = o.z + d.z * tnear;
+        gmm_march(&v, g, p, 0, g->nz, 0, d, tfar, &s, NULL);
+        acc += s.n;
+        const float rgba[4] = {s.sum[0] * p->brightness, s.sum[1] * p->brightness,
+                               s.sum[2] * p->brightness, s.sum[3] * p->brightness};
+        out[i] = orc_pack(rgba);
+        out_n[i] = (int32_t)s.n;
     }
     (void)nthreads;
     return acc;

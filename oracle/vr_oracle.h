@@ -170,6 +170,21 @@ int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, i
                        uint32_t *n_out, uint32_t *out, float *out_f, int32_t *out_n,
                        uint64_t *mark);
 
+/* The synthetic GMM volume as a procedural source: each record computed from
+ * its voxel index when a sample reads it (orc_synth_gmm fills its slices through
+ * the same function), for frames whose volume no host holds (config 5: 2048^3 x
+ * 16 = 1.65 TB). */
+typedef struct orc_gmm_proc orc_gmm_proc;
+orc_gmm_proc *orc_gmm_proc_new(int nx, int ny, int nz, int K, uint64_t seed);
+void orc_gmm_proc_free(orc_gmm_proc *g);
+
+/* whole-volume render of the given rows (any order) of the frame from the
+ * procedural source: out / out_n [nrows][width] (out_n -1 = ray misses the box,
+ * out 0 there); returns the samples taken, -1 on a bad K (4..32) */
+int64_t orc_render_gmm_rows_proc(const orc_gmm_proc *g, const orc_render_params *p,
+                                 const int32_t *rows, int nrows, uint32_t *out, int32_t *out_n,
+                                 int nthreads);
+
 /* CPU baseline: camera rays of rows [row_lo, row_hi), whole resident volume,
  * OpenMP over rows; returns the samples taken */
 int64_t orc_render_gmm_rows(const orc_gmm *v, const orc_render_params *p, int row_lo, int row_hi,

@@ -100,6 +100,26 @@ def test_synth_gmm_properties(orc):
     assert np.array_equal(part[0], wm[5:12]) and np.array_equal(part[1], sg[5:12])
 
 
+@pytest.mark.parametrize("view", ["C0", (30.0, 45.0), (180.0, 0.0)])
+@pytest.mark.parametrize("method", [1, 2])
+def test_procedural_rows_equal_resident_render(orc, pkg, view, method):
+    """the procedural source (records computed from the voxel index, used where
+    no host holds the volume: config 5 at size, test_gpu_gmm.py) renders rows
+    identical to the render of the generated volume, in any row order"""
+    dims, K, W, H = (30, 26, 22), 16, 96, 64
+    wm, sg = orc.synth_gmm(*dims, K, seed=7)
+    m = pkg.camera.single_test_inv_view() if view == "C0" else pkg.camera.display_inv_view(view)
+    p = orc.make_params(W, H, m, query_method=method, density=0.2)
+    ref = orc.render_gmm(wm, sg, dims, p)
+    rows = np.array([63, 0, 17, 32, 5, 17], np.int32)
+    out, out_n, samples = orc.render_gmm_rows_proc(dims, K, p, rows, seed=7)
+    want_n = np.where(ref["out_n"][rows] == -2, -1, ref["out_n"][rows])
+    assert np.array_equal(out, ref["out"][rows]) and np.array_equal(out_n, want_n)
+    assert samples == int(want_n[want_n > 0].sum()) > 0
+    with pytest.raises(ValueError):
+        orc.render_gmm_rows_proc(dims, K, p, np.array([H], np.int32))
+
+
 def test_gmm_render_known_answers(orc, pkg):
     """constant mixtures: every sample has the same statistic, so the composite is
     the closed form of a constant-alpha ray (the methods-1/2 march semantics)"""

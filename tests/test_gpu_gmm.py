@@ -227,3 +227,56 @@ def test_gmm_streamed_slabs(pkg, orc, gpu, c, S, method):
     torch.cuda.synchronize()
     assert torch.equal(out, first)
     pkg.set_stream(None)
+
+
+def test_config5_at_size(pkg, orc, gpu):
+    """BASELINE config 5 at its size: 2048^3 x 16-component GMM (1.65 TB) at
+    3840x2160, C0, method 1, rendered on one GPU as the 8-rank z-slab chain
+    renders it -- each rank's slab (its slices + halo, 207 GB) generated in HBM
+    in turn, the alive list handed on in HBM -- against the oracle's
+    whole-volume render of 64 rows, whose records it computes from the voxel
+    index as a sample reads them (no host holds the volume).  Slabs after the
+    one that ends the last ray receive no rays and are not generated."""
+    import torch
+    n, K, W, H = 2048, 16, 3840, 2160
+    pkg.freeCudaBuffers()
+    pkg.free_gmm()
+    torch.cuda.empty_cache()
+    m = pkg.camera.single_test_inv_view()
+    direction = pkg.slabs.march_direction(m, W, H)
+    bounds = pkg.slabs.slab_bounds(n, 8, direction)
+    zb, ns = pkg.slabs.resident_slices(*bounds[0], n)
+    need = n * n * ns * K * 12 + 2 * W * H * 48 + (2 << 30)
+    free, _ = torch.cuda.mem_get_info()
+    assert free >= need, f"{free / 2**30:.0f} GiB free, a slab needs {need / 2**30:.0f}"
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    steps = torch.full((W * H,), -2, dtype=torch.int32, device="cuda")
+    d = pkg.make_desc(frame, W, H, m, query_method=1, volume_size=(1, 1, 1), d_steps=steps)
+    bufs = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    n_in, done = 0, 0
+    try:
+        for i, (z_lo, z_hi) in enumerate(bounds):
+            if i and n_in == 0:
+                break
+            zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
+            pkg.synthesize_gmm((n, n, n), K, 20261015, z_base=zb, nslices=ns)
+            cnt.zero_()
+            pkg.render_gmm(d, pkg.gmm_slab(z_lo, z_hi, bufs[i % 2], cnt,
+                                           d_rays_in=bufs[(i + 1) % 2] if i else None,
+                                           n_rays_in=n_in))
+            torch.cuda.synchronize()
+            n_in = int(cnt.item())
+            done = i + 1
+            print(f"slab {i} z [{z_lo}, {z_hi}): {n_in} rays alive", flush=True)
+    finally:
+        pkg.free_gmm()
+    assert n_in == 0 and done >= 2
+    rows = np.linspace(0, H - 1, 64).round().astype(np.int32)
+    ref, ref_n, samples = orc.render_gmm_rows_proc(
+        (n, n, n), K, orc.make_params(W, H, m, query_method=1), rows, nthreads=orc.max_threads())
+    got = frame.cpu().numpy().view(np.uint32).reshape(H, W)[rows]
+    got_n = steps.cpu().numpy().reshape(H, W)[rows]
+    assert int(np.sum(ref_n > 0)) > 64 * W // 4 and samples > 0
+    assert np.array_equal(got_n, ref_n), f"{int(np.sum(got_n != ref_n))} sample counts differ"
+    assert np.array_equal(got, ref), f"{int(np.sum(got != ref))} RGBA8 pixels differ"
