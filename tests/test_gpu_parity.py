@@ -423,6 +423,7 @@ def test_errors_do_not_exit(pkg, gpu):
     # occupancy caps (LDS requests) on the ray-segmented, LDS-box and pipelined launches
     ("7", {"VR_SEG": "-2", "VR_WG_PER_CU": "3"}), ("1", {"VR_BOX_MAX": "64", "VR_WG_PER_CU": "3"}),
     ("2", {"VR_WG_PER_CU": "2"}), ("0", {"VR_WG_PER_CU": "3"}),
+    ("0", {"VR_QUAD2": "1"}), ("0", {"VR_QUAD2": "1", "VR_WG_PER_CU": "1"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
@@ -478,6 +479,53 @@ def test_segmented_march_early_exit(pkg, orc, gpu, seg, nb, tune):
                                  n_tiles=n_slots))
     name = f"k_march_segp{seg[1:]}" if seg.startswith("-") else f"k_march_seg{seg}"
     assert pkg.last_kernel().startswith(name)
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full)
+
+
+@pytest.mark.parametrize("brick", ["1", "0"])
+def test_quad_two_lanes_per_ray(pkg, orc, gpu, brick, tune):
+    """k_march_quad2 (the quad march with two lanes per ray: halves of a wave take
+    alternate steps and composite both in order): early exits on even and odd
+    steps, frames whose edges cut tiles and workgroups, and tile lists whose slot
+    count is not a multiple of 8 give the one-lane march's results bit for bit,
+    on the x rows and on the micro-brick copy"""
+    import torch
+    tune.set("VR_PATH", "0")
+    tune.set("VR_QUAD2", "1")
+    tune.set("VR_BRICK", brick)
+    vol = orc.synth_volume(30, 26, 22, 8)
+    pkg.init_distribution(vol)
+    cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),
+            pkg.camera.display_inv_view((-60.0, 110.0))]
+    for cam in cams:
+        for density, bright in ((0.05, 1.0), (0.6, 1.3), (3.0, 0.7)):
+            for method in (1, 2, 3):
+                got = gpu_render(pkg, None, 72, 42, cam, method, torch, density=density,
+                                 brightness=bright)
+                ref = orc.render(vol, orc.make_params(72, 42, cam, query_method=method,
+                                                      density=density, brightness=bright))[:3]
+                assert_parity(got, ref, f"quad2 brick={brick} m{method} d={density}")
+                assert pkg.last_kernel().startswith("k_march_quad2")
+    # tile lists (multi-GPU ranks): packed slots, misses cleared, 3 ranks
+    W, H = 136, 72
+    m = cams[1]
+    full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    tune.set("VR_QUAD2", "0")
+    pkg.render(pkg.make_desc(full, W, H, m, query_method=1))
+    tune.set("VR_QUAD2", "1")
+    world = 3
+    lists = pkg.tiles.tile_lists(W, H, world, m)
+    n_slots = lists.shape[1]
+    assert n_slots % 8 != 0 or world == 3
+    packed = torch.full((world, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    for r in range(world):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+        assert pkg.last_kernel().startswith("k_march_quad2")
     frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
     torch.cuda.synchronize()
@@ -842,7 +890,8 @@ def test_quad_march_brick_layout(pkg, orc, gpu, dims, brick, tune):
     for r in range(world):
         pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
                                  n_tiles=n_slots))
-        assert pkg.last_kernel().startswith(want)
+        # a short list takes two lanes per ray (k_march_quad2)
+        assert pkg.last_kernel().startswith(want.replace("quad", "quad2"))
     frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
     torch.cuda.synchronize()

@@ -7,6 +7,7 @@
 #   bash tools/gpu_jobs.sh steps   -> gpurun_out/steps_C*.npy for tools/footprint_sim.c (footprint_planes.log)
 #   bash tools/gpu_jobs.sh box     -> box_map.log (LDS-box march: wave maps, wide records, oblique views)
 #   bash tools/gpu_jobs.sh ranks   -> rank_sim_1024x8_C*.log
+#   bash tools/gpu_jobs.sh quad2   -> quad2 parity, C1 rank wave timelines, rank_sim_1024x8_C1_quad2.log
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
 J=${1:?job}; O=gpurun_out/$J; mkdir -p $O
 guard() { rc=$1; if [ $rc -ne 0 ]; then echo "$2 failed rc=$rc"; tail -30 $3; exit $rc; fi; }
@@ -28,6 +29,15 @@ box)
 ranks)
   for CAM in C0 C1; do
     timeout -k 10 300 python -u tools/rank_sim.py --camera $CAM > $O/rank_sim_$CAM.log 2>&1; guard $? rank-$CAM $O/rank_sim_$CAM.log
+  done ;;
+quad2)
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "quad_two_lanes or (every_kernel_path and QUAD2)" -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -2 $O/pytest.log
+  for E in "" VR_QUAD2=1; do
+    timeout -k 10 300 python -u tools/wave_timeline.py --camera C1 --world 8 --ranks 0,3 --env "$E" --cost > $O/wt_$E.log 2>&1; guard $? wt $O/wt_$E.log
+  done
+  for E in "" VR_QUAD2=1 VR_QUAD2=1,VR_WG_PER_CU=2 VR_QUAD2=1,VR_WG_PER_CU=3; do
+    timeout -k 10 300 python -u tools/rank_sim.py --camera C1 --env "$E" > $O/rs_$E.log 2>&1; guard $? rs $O/rs_$E.log
   done ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac

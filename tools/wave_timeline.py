@@ -1,11 +1,14 @@
-"""Wave occupancy timeline of the per-ray pipelined march (tooling).
+"""Wave occupancy timeline of the per-ray pipelined and quad marches (tooling).
 
 Runs a full frame and the tile lists of a multi-GPU split (each rank's list
 rendered alone, as tools/rank_sim.py does) with vr_debug_wave_clock on, and
 prints for each launch: span, live waves over time (per XCD), when the live
 count falls below 90 / 50 / 10 % of its peak, and wave-duration statistics.
 
-  python tools/wave_timeline.py [--camera C0] [--world 8] [--ranks 0,1] [--env VR_PATH=2]
+  python tools/wave_timeline.py [--camera C0] [--world 8] [--ranks 0,1] [--env VR_PATH=2] [--cost]
+
+--cost deals the rank lists by the measured per-tile costs of a full frame
+(tiles.tile_lists_by_cost, what bench.py uses at N > 1) instead of the estimate.
 """
 import argparse
 import os
@@ -60,6 +63,7 @@ def main():
     ap.add_argument("--ranks", default="0")
     ap.add_argument("--env", default="VR_PATH=2",
                     help="tuning knobs NAME=VALUE[,NAME=VALUE] (vr_set_tuning)")
+    ap.add_argument("--cost", action="store_true", help="cost-dealt rank lists")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
@@ -75,7 +79,7 @@ def main():
     steps = torch.zeros(W * H, dtype=torch.int32, device="cuda")
 
     def run(desc, nslots, name):
-        buf = torch.zeros(nslots * 12, dtype=torch.int64, device="cuda")
+        buf = torch.zeros(nslots * 24, dtype=torch.int64, device="cuda")  # <= 8 waves per slot
         pkg.render(desc)
         torch.cuda.synchronize()
         pkg.debug_wave_clock(buf)
@@ -91,7 +95,14 @@ def main():
     full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     tx, ty = pkg.tiles.tiles_x(W), pkg.tiles.tiles_y(H)
     run(pkg.make_desc(full, W, H, m), tx * ty, f"{args.config} {args.camera} full frame")
-    lists = pkg.tiles.tile_lists(W, H, args.world, m)
+    if args.cost:
+        st = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+        pkg.render(pkg.make_desc(full, W, H, m, d_steps=st))
+        torch.cuda.synchronize()
+        cost = pkg.tiles.tile_costs_from_frame(st.cpu().numpy(), W, H)
+        lists = pkg.tiles.tile_lists_by_cost(W, H, args.world, cost)
+    else:
+        lists = pkg.tiles.tile_lists(W, H, args.world, m)
     slots = lists.shape[1]
     dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
     for r in (int(x) for x in args.ranks.split(",")):

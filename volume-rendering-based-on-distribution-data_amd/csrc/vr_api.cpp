@@ -630,6 +630,15 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
             P.axis_view = 0;  // a forced path reads the x rows
         }
     }
+    // The quad march (path 0: oblique views, B = 8, methods 1-3) of a rank's tile
+    // list of <= 700 K rays (N >= 4 GPUs at 1080p) takes two lanes per ray
+    // (k_march_quad2): such a launch is bound by its longest waves' step chains,
+    // which halve.  Cost-dealt 1024^3 x 8 C1 lists, max over ranks: N = 8
+    // 0.586 -> 0.455 ms, N = 4 0.955 -> 0.880; N = 2 (1 M rays) 1.64 -> 1.68 and
+    // the full frame 3.15 -> 3.35 keep one lane per ray (tools/rank_sim.py,
+    // profiles/r03/rank_sim_1024x8_C1_quad2.log).  VR_QUAD2=0/1 overrides.
+    P.quad2 = d->d_tile_list && (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= 700000u;
+    if (const char *e = vr::tuning("VR_QUAD2")) P.quad2 = std::atoi(e) != 0;
     P.wave_clock = g.wave_clock;
     P.tile_cost = record;
     P.seg_lanes = small_seg ? small_seg : -2;  // VR_SEG=S: S lanes per ray, negative = pipelined windows

@@ -90,6 +90,7 @@ struct Params {
     uint4 *rays_out;             // alive rays leaving the slab (nullptr: slab = whole volume)
     uint32_t *n_rays_out;
     int wq_map;                  // k_march_wq pixel map: 0 a 64-pixel row per wave, 1 16x4 blocks
+    int quad2;                   // quad march with two lanes per ray (k_march_quad2)
 };
 
 // Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one

@@ -1004,6 +1004,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
         copy_logtab(s_lt);
         __syncthreads();
     }
+    unsigned long long t0 = 0;
+    if (P.wave_clock) t0 = wall_clock64();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 2, g = lane & 3u;
 #if VR_QUAD_MAP == 1  // wave = one 64-pixel row, quad = 4 consecutive pixels
@@ -1060,7 +1062,123 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAV
 #pragma unroll
         for (int k = 0; k < 4; k++) lc[k] = ln[k];
     }
+    if (P.wave_clock && lane == 0) {  // tooling (vr_debug_wave_clock, tools/wave_timeline.py)
+        unsigned long long *w = P.wave_clock + ((uint64_t)slot * 4u + wave) * 3u;
+        w[0] = t0;
+        w[1] = wall_clock64();
+        w[2] = __smid();
+    }
     if (!valid) return;
+    if (!hit) {
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
+// ---- the quad march with two lanes per ray (short launches: a rank's list) ----
+// The halves h = lane >> 5 of a wave take alternate steps of the same 8x4-pixel
+// block: h = 0 gathers and decodes the even steps of its quad's rays, h = 1 the
+// odd ones, each half with k_march_quad's quad gathers, pair swaps and blends.
+// Every lane keeps its ray's even-step chain (t and position accumulated one
+// step at a time, K:701, 706), so both halves hold the same float values; after
+// one cross-half exchange of the two samples both composite them in order and
+// end the ray at the same step -- the one-lane march's float operations in the
+// same order.  A ray's chain of dependent gathers is halved, which is what
+// bounds a short launch: at N = 8 a C1 rank's longest wave took 0.55 of its
+// 0.59 ms (tools/wave_timeline.py).  A 64x4 tile is two workgroups; workgroup b
+// renders half (b >> 3) & 1 of launch slot (b >> 4) * 8 + (b & 7), on XCD b % 8
+// = the slot's XCD.
+template <int M, bool BR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_QUAD_WAVES, 8))) void k_march_quad2(const float *__restrict__ vol, Params P) {
+    extern __shared__ __attribute__((aligned(32))) LogEnt s_lt2[];
+    const uint32_t vb = (blockIdx.x >> 4) * 8u + (blockIdx.x & 7u), part = (blockIdx.x >> 3) & 1u;
+    if (vb >= P.n_tiles) return;  // uniform per workgroup
+    const uint32_t slot = (P.tile_list || P.perm) ? vb : xcd_slot(vb, P.n_tiles);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;
+    if constexpr (M == 3) {
+        copy_logtab(s_lt2);
+        __syncthreads();
+    }
+    unsigned long long t0 = 0;
+    if (P.wave_clock) t0 = wall_clock64();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t h = lane >> 5, q = (lane >> 2) & 7u, g = lane & 3u;
+    const uint32_t lx = part * 32u + wave * 8u + q, ly = g;
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.CW && y < P.CH;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    const bool hit = alive;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;  // the chain at the iteration's even step i
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    float4 L0[4], L1[4], L2[4], L3[4];
+    FootPacked fc;
+    {
+        const float t1 = t + kTStep;
+        const bool live = h ? alive && !(t1 > r.tfar) && (1 < kMaxSteps) : alive;
+        fc = h ? pack_foot(footprint(P, px + stx, py + sty, pz + stz), live)
+               : pack_foot(footprint(P, px, py, pz), live);
+    }
+    bool lc[4];
+    lc[0] = qc_gather<0, BR>(vol, P, fc, g, L0);
+    lc[1] = qc_gather<1, BR>(vol, P, fc, g, L1);
+    lc[2] = qc_gather<2, BR>(vol, P, fc, g, L2);
+    lc[3] = qc_gather<3, BR>(vol, P, fc, g, L3);
+    for (int i = 0; i < kMaxSteps; i += 2) {
+        if (!wave_any(alive)) break;
+        // steps i+1, i+2, i+3 of the chain; this half's next gather is step
+        // i+2 (h = 0) or i+3 (h = 1), speculative (assumes no early exit)
+        const float ta = t + kTStep, tb = ta + kTStep, tc = tb + kTStep;   // K:701
+        const float ax = px + stx, ay = py + sty, az = pz + stz;            // K:706
+        const float bx = ax + stx, by = ay + sty, bz = az + stz;
+        const float nx = h ? bx + stx : bx, ny = h ? by + sty : by, nz = h ? bz + stz : bz;
+        const bool nl = h ? alive && !(tc > r.tfar) && (i + 3 < kMaxSteps)
+                          : alive && !(tb > r.tfar) && (i + 2 < kMaxSteps);
+        const FootPacked fn = pack_foot(footprint(P, nx, ny, nz), nl);
+        bool ln[4];
+        const float b0 = qc_group<0, M, BR>(vol, P, fc, lc[0], fn, ln[0], g, L0, s_lt2);
+        const float b1 = qc_group<1, M, BR>(vol, P, fc, lc[1], fn, ln[1], g, L1, s_lt2);
+        const float b2 = qc_group<2, M, BR>(vol, P, fc, lc[2], fn, ln[2], g, L2, s_lt2);
+        const float b3 = qc_group<3, M, BR>(vol, P, fc, lc[3], fn, ln[3], g, L3, s_lt2);
+        const float mine = g == 0 ? b0 : (g == 1 ? b1 : (g == 2 ? b2 : b3));
+        const float other = __shfl_xor(mine, 32);
+        const float s_even = h ? other : mine, s_odd = h ? mine : other;
+        if (alive) {
+            n = i + 1;
+            if (composite(P, s_even, sx, sy, sz, sw) || !(!(ta > r.tfar) && (i + 1 < kMaxSteps))) {
+                alive = false;  // K:698, 703, 381
+            } else {
+                n = i + 2;
+                if (composite(P, s_odd, sx, sy, sz, sw) || !(!(tb > r.tfar) && (i + 2 < kMaxSteps))) {
+                    alive = false;
+                } else {
+                    t = tb;
+                    px = bx;
+                    py = by;
+                    pz = bz;
+                }
+            }
+        }
+        fc = fn;
+#pragma unroll
+        for (int k = 0; k < 4; k++) lc[k] = ln[k];
+    }
+    if (P.wave_clock && lane == 0) {  // tooling (vr_debug_wave_clock, tools/wave_timeline.py)
+        unsigned long long *w = P.wave_clock + ((uint64_t)slot * 8u + part * 4u + wave) * 3u;
+        w[0] = t0;
+        w[1] = wall_clock64();
+        w[2] = __smid();
+    }
+    if (!valid || h) return;
     if (!hit) {
         write_miss(P, o);
         return;
@@ -2223,6 +2341,25 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             const int qcap = P.wg_per_cu > 0 ? P.wg_per_cu
                              : (P.tile_list && (uint64_t)nslots * 256u <= 400000u) ? 1 : 2;
             const size_t qlds = cap_lds(P, qcap);
+            if (P.quad2) {  // two lanes per ray, two workgroups per tile
+                note_kernel(P.bvol ? "k_march_quad2_brick" : "k_march_quad2", B, method);
+                const dim3 grid2(((nslots + 7u) / 8u) * 16u);
+                Params Q = P;
+                if (P.bvol) {
+                    Q.sy = P.bsy;
+                    Q.sz = P.bsz;
+                }
+                const float *v = P.bvol ? P.bvol : vol;
+                switch (method * 2 + (P.bvol ? 1 : 0)) {
+                case 2: hipLaunchKernelGGL((k_march_quad2<1, false>), grid2, block, qlds, s, v, Q); break;
+                case 3: hipLaunchKernelGGL((k_march_quad2<1, true>), grid2, block, qlds, s, v, Q); break;
+                case 4: hipLaunchKernelGGL((k_march_quad2<2, false>), grid2, block, qlds, s, v, Q); break;
+                case 5: hipLaunchKernelGGL((k_march_quad2<2, true>), grid2, block, qlds, s, v, Q); break;
+                case 6: hipLaunchKernelGGL((k_march_quad2<3, false>), grid2, block, qlds, s, v, Q); break;
+                case 7: hipLaunchKernelGGL((k_march_quad2<3, true>), grid2, block, qlds, s, v, Q); break;
+                }
+                return hipGetLastError();
+            }
             if (P.bvol) {
                 Params Q = P;
                 Q.sy = P.bsy;
