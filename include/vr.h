@@ -295,10 +295,12 @@ uint32_t vr_tiles_y(uint32_t height);
  * render_kernel call launched (e.g. "k_march_quad<B=8,M=1>"), "" before any */
 const char *vr_last_kernel(void);
 
-/* Tooling: while d_buf is non-null, every launch of the per-ray pipelined
- * march writes 3 uint64 per wave at d_buf[(slot*4 + wave)*3]: wall clock at
- * the wave's start and end (100 MHz) and __smid() (CU id, XCC id in the high
- * bits).  d_buf must hold 12 * n_slots values.  nullptr turns it off. */
+/* Tooling: while d_buf is non-null, every launch of the per-ray pipelined,
+ * quad and ray-segmented marches writes 3 uint64 per wave: wall clock at the
+ * wave's start and end (100 MHz) and __smid() (CU id, XCC id in the high
+ * bits), at d_buf[(slot*4 + wave)*3] (pipelined, quad), d_buf[(slot*8 +
+ * half*4 + wave)*3] (k_march_quad2) or d_buf[(slot*16 + part*4 + wave)*3]
+ * (segmented).  d_buf must hold 48 * n_slots values.  nullptr turns it off. */
 int vr_debug_wave_clock(uint64_t *d_buf);
 
 /* Device self-test: compares the entropy decode's fast float logarithms (the

@@ -8,6 +8,8 @@
 #   bash tools/gpu_jobs.sh box     -> box_map.log (LDS-box march: wave maps, wide records, oblique views)
 #   bash tools/gpu_jobs.sh ranks   -> rank_sim_1024x8_C*.log
 #   bash tools/gpu_jobs.sh quad2   -> quad2 parity, C1 rank wave timelines, rank_sim_1024x8_C1_quad2.log
+#   bash tools/gpu_jobs.sh segc0   -> C0 rank lists: wave timeline and the ray-segmented variants
+#   bash tools/gpu_jobs.sh baked   -> baked full frames: wave timeline, segmented / pipelined variants
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
 J=${1:?job}; O=gpurun_out/$J; mkdir -p $O
 guard() { rc=$1; if [ $rc -ne 0 ]; then echo "$2 failed rc=$rc"; tail -30 $3; exit $rc; fi; }
@@ -39,6 +41,14 @@ quad2)
   for E in "" VR_QUAD2=1 VR_QUAD2=1,VR_WG_PER_CU=2 VR_QUAD2=1,VR_WG_PER_CU=3; do
     timeout -k 10 300 python -u tools/rank_sim.py --camera C1 --env "$E" > $O/rs_$E.log 2>&1; guard $? rs $O/rs_$E.log
   done ;;
+segc0)
+  timeout -k 10 300 python -u tools/wave_timeline.py --camera C0 --world 8 --ranks 0,3 --env "" --cost > $O/wt.log 2>&1; guard $? wt $O/wt.log
+  for E in "" VR_SEG=-4 VR_SEG=4 VR_WG_PER_CU=3 VR_WG_PER_CU=4 VR_SEG=-4,VR_WG_PER_CU=4; do
+    timeout -k 10 300 python -u tools/rank_sim.py --camera C0 --env "$E" > $O/rs_$E.log 2>&1; guard $? rs $O/rs_$E.log
+  done ;;
+baked)
+  timeout -k 10 300 python -u tools/wave_timeline.py --camera C0 --world 8 --ranks 0 --env "" --cost --baked > $O/wt.log 2>&1; guard $? wt $O/wt.log
+  timeout -k 10 600 python -u tools/bench_variants.py --config 1024x8 --baked --rounds 3 --reps 5 --cameras C0,C1 --env "" VR_PATH=2 VR_PATH=7,VR_SEG=-2 VR_PATH=7,VR_SEG=2 VR_PATH=7,VR_SEG=4 VR_PATH=7,VR_SEG=-4 > $O/variants.log 2>&1; guard $? var $O/variants.log ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done

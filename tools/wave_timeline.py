@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--env", default="VR_PATH=2",
                     help="tuning knobs NAME=VALUE[,NAME=VALUE] (vr_set_tuning)")
     ap.add_argument("--cost", action="store_true", help="cost-dealt rank lists")
+    ap.add_argument("--baked", action="store_true", help="bake the statistics planes first")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
@@ -74,12 +75,14 @@ def main():
         pkg.set_tuning(k, v)
     n, nb, W, H = bench.CONFIGS[args.config]
     pkg.synthesize((n, n, n), nb, bench.SEED)
+    if args.baked:
+        pkg.bake_stats()
     m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
          else pkg.camera.display_inv_view((30.0, 45.0)))
     steps = torch.zeros(W * H, dtype=torch.int32, device="cuda")
 
     def run(desc, nslots, name):
-        buf = torch.zeros(nslots * 24, dtype=torch.int64, device="cuda")  # <= 8 waves per slot
+        buf = torch.zeros(nslots * 48, dtype=torch.int64, device="cuda")  # <= 16 waves per slot
         pkg.render(desc)
         torch.cuda.synchronize()
         pkg.debug_wave_clock(buf)

@@ -72,7 +72,9 @@ struct Params {
     const float4 *flex;
     int nflex;                   // blocks per axis
     // tooling (vr_debug_wave_clock): per wave {start, end, hw id} of the
-    // per-ray pipelined march, nullptr = off
+    // per-ray pipelined, quad and ray-segmented marches, nullptr = off; slot
+    // s's waves at [s * 4 + wave] (pipe, quad), [s * 8 + half * 4 + wave]
+    // (quad2), [s * 16 + part * 4 + wave] (segmented)
     unsigned long long *wave_clock;
     // adaptive tile order: per-tile cost record of the pipelined march
     // (record_tile_cost), indexed by tile id, nullptr = off

@@ -175,7 +175,16 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
 template <int B, int M, int S, bool PIPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVES, 8))) void k_march_seg(const float *__restrict__ vol, Params P) {
     const uint32_t b = blockIdx.x;
-    march_seg_part<B, M, S, PIPE>(vol, P, (b & 7u) + 8u * (b / (8u * S)), (b >> 3) % S);
+    const uint32_t slot = (b & 7u) + 8u * (b / (8u * S)), part = (b >> 3) % S;
+    unsigned long long t0 = 0;
+    if (P.wave_clock) t0 = wall_clock64();
+    march_seg_part<B, M, S, PIPE>(vol, P, slot, part);
+    if (P.wave_clock && (threadIdx.x & 63u) == 0 && slot < P.n_tiles) {  // tooling
+        unsigned long long *w = P.wave_clock + ((uint64_t)slot * 16u + part * 4u + threadIdx.x / 64u) * 3u;
+        w[0] = t0;
+        w[1] = wall_clock64();
+        w[2] = __smid();
+    }
 }
 
 template <int B, int S, bool PIPE>
