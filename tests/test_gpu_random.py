@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 # kernel-path overrides a case may take (vr_api.cpp fill_params / baked_path)
 PATHS = [{}, {}, {"VR_PATH": "0"}, {"VR_PATH": "1"}, {"VR_PATH": "1", "VR_BOX_MAX": "64"},
          {"VR_PATH": "2"}, {"VR_PATH": "4"}, {"VR_PATH": "7", "VR_SEG": "-4"},
-         {"VR_PATH": "7", "VR_SEG": "-2"}, {"VR_PATH": "7", "VR_SEG": "4"}, {"VR_WG_PER_CU": "2"}]
+         {"VR_PATH": "7", "VR_SEG": "-2"}, {"VR_PATH": "7", "VR_SEG": "4"}, {"VR_WG_PER_CU": "2"},
+         {"VR_PATH": "0", "VR_QUAD2": "1"}]
 
 
 def draw_camera(pkg, rng):
@@ -71,6 +72,49 @@ def test_random_histogram_case(pkg, orc, gpu, seed, tune):
                                 f"baked {baked} kernel {pkg.last_kernel()}")
     finally:
         pkg.release_stats()
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_tile_list_case(pkg, orc, gpu, seed, tune):
+    """a multi-GPU split of a random frame: every rank's tile list rendered through
+    the kernel the library picks for a list of that size (or a random path
+    override), the packed slots assembled by k_unscatter, equals the oracle frame"""
+    import torch
+    rng = np.random.default_rng(3000 + seed)
+    dims = tuple(int(v) for v in rng.integers(2, 41, 3))
+    nb = int(rng.choice([1, 2, 4, 8, 8, 8]))
+    W, H = int(rng.integers(1, 321)), int(rng.integers(1, 201))
+    method = int(rng.choice([1, 2, 3]))
+    world = int(rng.integers(2, 9))
+    m = draw_camera(pkg, rng)
+    prm = draw_params(rng)
+    env = PATHS[int(rng.integers(0, len(PATHS)))]
+    for k, v in env.items():
+        tune.set(k, v)
+    vol = orc.synth_volume(*dims, nb, seed=seed)
+    pkg.init_distribution(vol)
+    ref = orc.render(vol, orc.make_params(
+        W, H, m, density=prm["density"], brightness=prm["brightness"],
+        transfer_offset=prm["toff"], transfer_scale=prm["tscale"], query_method=method),
+        want_float=False, want_steps=False)[0]
+    lists = pkg.tiles.tile_lists(W, H, world, m)
+    n_slots = lists.shape[1]
+    packed = torch.full((world, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    kernels = set()
+    for r in range(world):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=method, d_tile_list=dl[r],
+                                 n_tiles=n_slots, density=prm["density"],
+                                 brightness=prm["brightness"], transfer_offset=prm["toff"],
+                                 transfer_scale=prm["tscale"]))
+        kernels.add(pkg.last_kernel())
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    got = frame.cpu().numpy().view(np.uint32).reshape(H, W)
+    assert np.array_equal(got, ref), (
+        f"seed {seed}: {dims}x{nb} {W}x{H} m{method} world {world} env {env} {kernels}: "
+        f"{int(np.sum(got != ref))} pixels differ")
 
 
 @pytest.mark.parametrize("seed", range(48))
