@@ -661,6 +661,17 @@ def main():
     bounds = (compute_bounds(pkg, torch, stream, W, H, m, args.method, kern_ms, pmc)
               if world == 1 and not args.no_issue_bounds else None)
 
+    # the measured read ceiling of this GPU beside the 8 TB/s peak:
+    # the resident record volume streamed by a coalesced read kernel (vr_stream_read)
+    ceiling = None
+    if world == 1:
+        rb, rms, rmean = pkg.stream_read(5)
+        ceiling = {"kernel": "k_stream_read", "bytes": rb, "ms": round(rms, 4),
+                   "mean_ms": round(rmean, 4), "GBps": round(rb / (rms * 1e-3) / 1e9, 1),
+                   "frac_of_peak": round(rb / (rms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "what": "the resident record volume (pitches included) read once per "
+                           "pass, 16 B per lane, fastest of 5 timed passes"}
+
     # parity of the timed frame's view (untimed; full frames at N = 1 are checked
     # against the oracle frame of the CPU baseline below, N > 1 assembled frames
     # against rank 0's own whole-frame render)
@@ -677,6 +688,9 @@ def main():
                  gf.cpu().numpy().reshape(H, W, 4), gn.cpu().numpy().reshape(H, W),
                  pkg.last_kernel())
 
+    gather_bytes = None
+    if check is not None and world == 1 and args.method in (1, 2, 3):
+        gather_bytes = int(check[2][check[2] > 0].astype(np.int64).sum()) * 8 * rec_bytes
     ms_per_step = elapsed / args.steps * 1e3
     value = W * H / (elapsed / args.steps) / 1e6
     out = None
@@ -732,6 +746,14 @@ def main():
                 "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
                 "U_records": int(u) if u is not None else None,
                 "compute": bounds,
+                "read_ceiling": ceiling,
+                "frac_of_read_ceiling": (round(achieved / ceiling["GBps"], 4)
+                                         if achieved and ceiling else None),
+                "traffic_GBps": (round(traffic / (kern_ms * 1e-3) / 1e9, 1)
+                                 if traffic else None),
+                # informational: every sample's 8 corner records
+                # as if none were shared, samples * 8 * S_rec
+                "gather_bytes_per_launch": gather_bytes,
             },
             "parity": parity,
             "cpu_baseline": cpu,

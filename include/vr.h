@@ -310,6 +310,14 @@ int vr_debug_wave_clock(uint64_t *d_buf);
  * double-log fallback (summed). */
 int vr_selftest_logf(uint64_t counts[2]);
 
+/* Measured read ceiling of this device (bench.py reports the
+ * march's traffic against it beside the 8 TB/s peak): the resident record
+ * volume (all B * 4 bytes of every record, pitches included, rounded down to
+ * 16 B) is streamed once untimed and then reps times by a coalesced 16-B-per-
+ * lane read kernel on the library's stream.  ms[0] = fastest pass, ms[1] =
+ * mean; *bytes (optional) = bytes per pass.  Synchronous. */
+int vr_stream_read(int reps, float ms[2], uint64_t *bytes);
+
 /* ---- the reference's input files ---- */
 
 /* Parse a codebook file (loadCodebook's format, C:558-642): int nSteps,

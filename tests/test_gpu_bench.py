@@ -34,6 +34,10 @@ def test_bench_single_and_two_rank_frames_agree(gpu, tmp_path):
     assert out1["n_gpus"] == 1 and out1["value"] > 0
     rf = out1["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"].startswith("k_march")
+    # the measured read ceiling streams the whole resident 256^3 x 4 volume
+    rc = rf["read_ceiling"]
+    assert rc["bytes"] == 256 ** 3 * 4 * 4 and rc["GBps"] > 100 and rc["ms"] <= rc["mean_ms"]
+    assert rf["frac_of_read_ceiling"] > 0 and rf["gather_bytes_per_launch"] > 0
     f2 = str(tmp_path / "f2.npy")
     out2 = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                  "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", "29533",

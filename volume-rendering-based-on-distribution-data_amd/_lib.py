@@ -98,7 +98,7 @@ EXPORTS = [
     "vr_load_flex_files", "vr_debug_wave_clock",
     "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_render_gmm",
     "vr_gmm_count_footprint", "vr_bake_stats", "vr_release_stats", "vr_stats_info",
-    "vr_set_tuning", "vr_clear_tuning",
+    "vr_set_tuning", "vr_clear_tuning", "vr_stream_read",
 ]
 
 _lib = None
@@ -166,6 +166,8 @@ def load() -> ctypes.CDLL:
     L.vr_load_reference_files.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                           Extent, i32]
     L.vr_load_reference_files.restype = i32
+    L.vr_stream_read.argtypes = [i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint64)]
+    L.vr_stream_read.restype = i32
     L.vr_selftest_logf.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.vr_selftest_logf.restype = ctypes.c_int
     L.vr_init_codec.argtypes = [vp, Extent, vp, i32, vp, i32, i32, i32]

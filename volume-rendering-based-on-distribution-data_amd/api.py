@@ -398,6 +398,16 @@ def last_kernel() -> str:
     return _lib.load().vr_last_kernel().decode()
 
 
+def stream_read(reps: int = 5):
+    """Measured read ceiling: the resident record volume streamed by a coalesced
+    16-B-per-lane read kernel (vr_stream_read).  Returns (bytes per pass,
+    fastest ms, mean ms)."""
+    ms = (ctypes.c_float * 2)()
+    nbytes = ctypes.c_uint64(0)
+    check(_lib.load().vr_stream_read(int(reps), ms, ctypes.byref(nbytes)))
+    return int(nbytes.value), float(ms[0]), float(ms[1])
+
+
 def debug_wave_clock(d_buf) -> None:
     """Tooling: per-wave {start, end, __smid} clocks of the per-ray pipelined
     march into a device uint64 buffer of 12 * n_slots values (None = off)."""
@@ -494,7 +504,7 @@ __all__ = [
     "flex_process", "flex_info", "load_flex_files", "parse_flex_files", "synthesize", "synthesize_codec", "codec_info",
     "volume_info",
     "volume_layout",
-    "set_stream", "set_tuning", "clear_tuning", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "version",
+    "set_stream", "set_tuning", "clear_tuning", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "stream_read", "version",
     "init_gmm", "synthesize_gmm", "gmm_info", "free_gmm", "gmm_slab", "render_gmm",
     "gmm_count_footprint", "bake_stats", "release_stats", "stats_info",
     "VRError", "PAD",

@@ -927,6 +927,48 @@ const char *vr_version(void) { return "vrdd-amd 0.1 (gfx950)"; }
 
 const char *vr_last_kernel(void) { return vr::last_march_kernel(); }
 
+// Measured read ceiling: the resident record volume streamed
+// once per rep by k_stream_read on the library's stream, timed with HIP events.
+int vr_stream_read(int reps, float *ms, uint64_t *bytes) {
+    if (!ms || reps < 1) return fail(VR_ERR_ARG, "vr_stream_read: ms null or reps < 1");
+    if (!g.vol) return fail(VR_ERR_STATE, "no volume resident");
+    const uint64_t nbytes = (g.sz * (uint64_t)g.nz * (uint64_t)g.nb * 4u) & ~(uint64_t)15;
+    hipDevice_t dev;
+    int dev_id = 0, cus = 0;
+    VR_HIP(hipGetDevice(&dev_id));
+    (void)dev;
+    VR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id));
+    const uint32_t nblocks = (uint32_t)(cus > 0 ? cus : 256) * 8u;  // 8 workgroups per CU
+    uint32_t *d = nullptr;
+    VR_HIP(hipMalloc(&d, nblocks * sizeof(uint32_t)));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    float best = 0.0f, sum = 0.0f;
+    // one untimed pass first (clocks, address translation)
+    if (e == hipSuccess) e = vr::launch_stream_read(g.vol, nbytes, d, nblocks, g.stream);
+    for (int r = 0; r < reps && e == hipSuccess; r++) {
+        e = hipEventRecord(e0, g.stream);
+        if (e == hipSuccess) e = vr::launch_stream_read(g.vol, nbytes, d, nblocks, g.stream);
+        if (e == hipSuccess) e = hipEventRecord(e1, g.stream);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        float t = 0.0f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+        if (e == hipSuccess) {
+            best = (r == 0 || t < best) ? t : best;
+            sum += t;
+        }
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "vr_stream_read");
+    ms[0] = best;
+    ms[1] = sum / (float)reps;
+    if (bytes) *bytes = nbytes;
+    return VR_OK;
+}
+
 int vr_selftest_logf(uint64_t *counts) {
     if (!counts) return fail(VR_ERR_ARG, "null pointer");
     unsigned long long *d = nullptr;

@@ -179,12 +179,15 @@ __device__ __forceinline__ int point_axis(float u, int n) {
 }
 
 // transfer function (K:2323-2326), linear / normalised / clamp (K:2337-2339)
+// The 9 entries as bit masks (entry i = bit i; g in 2-bit fields of halves):
+// r 0,1,1,1,0,0,0,1,0  g 0,0,.5,1,1,1,0,0,0  b 0,0,0,0,0,1,1,1,0  a 0,1,1,1,1,1,1,1,0
+// -- one bit-field extract + convert per channel instead of compare chains.
 __device__ __forceinline__ float4 tf_entry(int i) {
-    // branch-free table: r,g,b,a of the 9 entries
-    const float r = (i == 1 || i == 2 || i == 3 || i == 7) ? 1.0f : 0.0f;
-    const float g = (i == 3 || i == 4 || i == 5) ? 1.0f : (i == 2 ? 0.5f : 0.0f);
-    const float b = (i == 5 || i == 6 || i == 7) ? 1.0f : 0.0f;
-    const float a = (i >= 1 && i <= 7) ? 1.0f : 0.0f;
+    const uint32_t u = (uint32_t)i;  // 0 <= i <= 8 (lin_axis clamps)
+    const float r = (float)((0x08Eu >> u) & 1u);
+    const float g = (float)((0xA90u >> (2u * u)) & 3u) * 0.5f;
+    const float b = (float)((0x0E0u >> u) & 1u);
+    const float a = (float)((0x0FEu >> u) & 1u);
     return make_float4(r, g, b, a);
 }
 

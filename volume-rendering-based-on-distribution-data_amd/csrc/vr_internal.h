@@ -92,6 +92,10 @@ hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t
 // record strides of axis_copy_strides
 hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint64_t asx,
                             uint64_t asy, uint64_t asz, hipStream_t s);
+// streaming read of bytes (a multiple of 16, 16-B aligned) by nblocks workgroups
+// of 256 threads; one xor word per workgroup into out (bench read ceiling)
+hipError_t launch_stream_read(const void *buf, uint64_t bytes, uint32_t *out, uint32_t nblocks,
+                              hipStream_t s);
 hipError_t launch_logcheck(unsigned long long *cnt, hipStream_t s);
 hipError_t launch_synth(float *vol, const SynthArgs &a, hipStream_t s);
 hipError_t launch_unscatter(const uint32_t *packed, const uint32_t *lists, uint32_t ntiles,

@@ -177,4 +177,47 @@ hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t
     return hipGetLastError();
 }
 
+// Streaming read of a resident buffer (bench.py's measured read ceiling,
+// SURVEY.md 8(d)): every 16-B chunk read once, coalesced (16 B per lane, 4
+// loads in flight per lane), grid-strided over a fixed grid; the chunks are
+// folded into one xor per thread and one word per workgroup so no load is dead.
+__global__ __launch_bounds__(256) void k_stream_read(const uint4 *__restrict__ p, uint64_t n,
+                                                     uint32_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    uint32_t acc = 0;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w;
+        acc ^= c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n; i += stride) {
+        const uint4 a = p[i];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+    __shared__ uint32_t red[256];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t v = red[threadIdx.x] ^ red[threadIdx.x + 64] ^ red[threadIdx.x + 128] ^
+                           red[threadIdx.x + 192];
+        red[threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t v = 0;
+        for (int k = 0; k < 64; k++) v ^= red[k];
+        out[blockIdx.x] = v;
+    }
+}
+
+hipError_t launch_stream_read(const void *buf, uint64_t bytes, uint32_t *out, uint32_t nblocks,
+                              hipStream_t s) {
+    if (!buf || !out || nblocks == 0 || (reinterpret_cast<uintptr_t>(buf) & 15u))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_stream_read, dim3(nblocks), dim3(256), 0, s,
+                       reinterpret_cast<const uint4 *>(buf), bytes / 16u, out);
+    return hipGetLastError();
+}
+
 }  // namespace vr
