@@ -591,6 +591,21 @@ def main():
     alg_bytes = (vol_bytes + pixels * 4) if vol_bytes is not None else None
     torch.cuda.synchronize()
 
+    # the measured read ceiling of this GPU beside the 8 TB/s peak (SURVEY.md 8(d)):
+    # the resident record volume streamed by a coalesced read kernel (vr_stream_read),
+    # ~50 ms of saturating reads before the warm-up frames, so those start on the
+    # clocks of a loaded GPU (the frame time settles over the first ~50 ms of work,
+    # DESIGN.md section 6)
+    ceiling = None
+    if world == 1:
+        rb, rms, rmean = pkg.stream_read(8)
+        ceiling = {"kernel": "k_stream_read", "bytes": rb, "ms": round(rms, 4),
+                   "mean_ms": round(rmean, 4), "GBps": round(rb / (rms * 1e-3) / 1e9, 1),
+                   "frac_of_peak": round(rb / (rms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "what": "the resident record volume (pitches included) read once per "
+                           "pass, 16 B per lane, fastest of 8 timed passes"}
+    torch.cuda.synchronize()
+
     ev = []
     nframe = [0]
 
@@ -660,17 +675,6 @@ def main():
     # the bounds that apply when the frame is not HBM-bound (the smaller configs)
     bounds = (compute_bounds(pkg, torch, stream, W, H, m, args.method, kern_ms, pmc)
               if world == 1 and not args.no_issue_bounds else None)
-
-    # the measured read ceiling of this GPU beside the 8 TB/s peak (SURVEY.md 8(d)):
-    # the resident record volume streamed by a coalesced read kernel (vr_stream_read)
-    ceiling = None
-    if world == 1:
-        rb, rms, rmean = pkg.stream_read(5)
-        ceiling = {"kernel": "k_stream_read", "bytes": rb, "ms": round(rms, 4),
-                   "mean_ms": round(rmean, 4), "GBps": round(rb / (rms * 1e-3) / 1e9, 1),
-                   "frac_of_peak": round(rb / (rms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "what": "the resident record volume (pitches included) read once per "
-                           "pass, 16 B per lane, fastest of 5 timed passes"}
 
     # parity of the timed frame's view (untimed; full frames at N = 1 are checked
     # against the oracle frame of the CPU baseline below, N > 1 assembled frames
