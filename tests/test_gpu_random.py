@@ -158,3 +158,54 @@ def test_random_gmm_case(pkg, orc, gpu, seed):
                                                        density=density))
     check(got, ref, f"seed {seed}: GMM {dims} K={K} {W}x{H} m{method}")
     pkg.free_gmm()
+
+
+def draw_dispatch_camera(pkg, rng):
+    """views around the library's kernel-choice thresholds (vr_api.cpp fill_params):
+    screen x near the voxel rows' 0.95 cosine, along the volume's z (side views) or
+    y (top views), row-aligned and oblique"""
+    kind = int(rng.integers(0, 5))
+    dist = -float(rng.uniform(2.2, 4.5))
+    if kind == 0:  # yaw across the 18.2 deg row-aligned / oblique threshold
+        ang = (float(rng.uniform(-12, 12)), float(rng.choice([-1, 1]) * rng.uniform(14, 23)))
+    elif kind == 1:  # side views: screen x along z
+        ang = (float(rng.uniform(-12, 12)), float(rng.choice([90, 270]) + rng.uniform(-12, 12)))
+    elif kind == 2:  # top views: screen x along y
+        ang = (float(rng.choice([90, 270]) + rng.uniform(-12, 12)),
+               float(90 + rng.uniform(-12, 12)))
+    elif kind == 3:
+        ang = (0.0, 0.0)
+    else:
+        ang = (float(rng.uniform(-180, 180)), float(rng.uniform(-180, 180)))
+    return pkg.camera.display_inv_view(ang, (float(rng.uniform(-0.3, 0.3)),
+                                             float(rng.uniform(-0.3, 0.3)), dist)), kind, ang
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_random_midsize_default_dispatch(pkg, orc, gpu, seed):
+    """mid-size volumes (64-192 voxels an axis) and frames (up to 800 x 600) through
+    the library's own kernel choice -- no tuning knobs -- so the size- and
+    view-dependent dispatch (LDS box for coarse row-aligned frames, micro-brick and
+    axis-rows copies, wide-record marches, baked planes) is exercised at the shapes
+    it is tuned for, whole frames against the oracle"""
+    import torch
+    rng = np.random.default_rng(3000 + seed)
+    dims = tuple(int(v) for v in rng.integers(64, 193, 3))
+    nb = int(rng.choice([1, 2, 4, 8, 8, 8, 16, 32]))
+    W, H = int(rng.integers(320, 801)), int(rng.integers(240, 601))
+    method = int(rng.choice([1, 1, 2, 3, 7]))
+    m, kind, ang = draw_dispatch_camera(pkg, rng)
+    baked = bool(rng.integers(0, 3) == 0)
+    vol = orc.synth_volume(*dims, nb, seed=seed)
+    pkg.init_distribution(vol)
+    if baked:
+        pkg.bake_stats()
+    try:
+        got = gpu_render(pkg, None, W, H, m, method, torch, m7=dims if method == 7 else None)
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=method, m7_dims=dims))[:3]
+        what = (f"seed {seed}: {dims}x{nb} {W}x{H} m{method} view {kind} "
+                f"({ang[0]:.1f}, {ang[1]:.1f}) baked {baked} kernel {pkg.last_kernel()}")
+        print(what)
+        assert_parity(got, ref, what)
+    finally:
+        pkg.release_stats()
