@@ -209,3 +209,48 @@ def test_random_midsize_default_dispatch(pkg, orc, gpu, seed):
         assert_parity(got, ref, what)
     finally:
         pkg.release_stats()
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_midsize_tile_lists_default_dispatch(pkg, orc, gpu, seed):
+    """multi-GPU splits of mid-size frames (up to 1280 x 800, 1-8 ranks: tile lists
+    of ~30 K to ~1 M rays, across the library's 400 K / 700 K ray thresholds for
+    the ray-segmented, two-lanes-per-ray quad and one-lane marches) through the
+    default dispatch, per-step or baked, assembled by k_unscatter, against the
+    oracle frame"""
+    import torch
+    rng = np.random.default_rng(4000 + seed)
+    dims = tuple(int(v) for v in rng.integers(64, 161, 3))
+    nb = int(rng.choice([1, 4, 8, 8, 8]))
+    W, H = int(rng.integers(480, 1281)), int(rng.integers(320, 801))
+    method = int(rng.choice([1, 1, 2, 3]))
+    world = int(rng.choice([1, 2, 3, 4, 8]))
+    m, kind, ang = draw_dispatch_camera(pkg, rng)
+    baked = bool(rng.integers(0, 3) == 0)
+    vol = orc.synth_volume(*dims, nb, seed=seed)
+    pkg.init_distribution(vol)
+    if baked:
+        pkg.bake_stats()
+    try:
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=method),
+                         want_float=False, want_steps=False)[0]
+        lists = pkg.tiles.tile_lists(W, H, world, m)
+        n_slots = lists.shape[1]
+        packed = torch.full((world, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+        kernels = set()
+        for r in range(world):
+            pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=method, d_tile_list=dl[r],
+                                     n_tiles=n_slots))
+            kernels.add(pkg.last_kernel())
+        frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        pkg.unscatter_tiles(packed, dl, world, n_slots, frame, W, H)
+        torch.cuda.synchronize()
+        got = frame.cpu().numpy().view(np.uint32).reshape(H, W)
+        what = (f"seed {seed}: {dims}x{nb} {W}x{H} m{method} world {world} "
+                f"({n_slots * 256} rays a list) view {kind} ({ang[0]:.1f}, {ang[1]:.1f}) "
+                f"baked {baked} {sorted(kernels)}")
+        print(what)
+        assert np.array_equal(got, ref), f"{what}: {int(np.sum(got != ref))} pixels differ"
+    finally:
+        pkg.release_stats()
