@@ -254,3 +254,57 @@ def test_random_midsize_tile_lists_default_dispatch(pkg, orc, gpu, seed):
         assert np.array_equal(got, ref), f"{what}: {int(np.sum(got != ref))} pixels differ"
     finally:
         pkg.release_stats()
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_midsize_codec_default_dispatch(pkg, orc, gpu, seed):
+    """fractal/template codec volumes (methods 4/5/6) of 48-128 voxels an axis at
+    frames up to 640 x 480 through the default dispatch (codec marches chosen by
+    view and bin count), per-step or baked, against the oracle"""
+    import torch
+    rng = np.random.default_rng(5000 + seed)
+    dims = tuple(int(v) for v in rng.integers(48, 129, 3))
+    nb = int(rng.choice([4, 8, 8, 16, 32]))
+    W, H = int(rng.integers(240, 641)), int(rng.integers(160, 481))
+    method = int(rng.choice([4, 5, 6]))
+    m, kind, ang = draw_dispatch_camera(pkg, rng)
+    baked = bool(rng.integers(0, 3) == 0)
+    cb, t, e = orc.synth_codec(*dims, nb, ntemplates=int(rng.integers(8, 65)),
+                               slots=int(rng.integers(0, min(nb, 8) + 1)), seed=seed)
+    pkg.init_codec(cb, t, e)
+    if baked:
+        pkg.bake_stats()
+    try:
+        got = codec_render(pkg, W, H, m, method, torch)
+        ref = orc.render_codec(cb, t, e, orc.make_params(W, H, m, query_method=method))[:3]
+        what = (f"seed {seed}: codec {dims}x{nb} {W}x{H} m{method} view {kind} "
+                f"({ang[0]:.1f}, {ang[1]:.1f}) baked {baked} kernel {pkg.last_kernel()}")
+        print(what)
+        assert_parity(got, ref, what)
+    finally:
+        pkg.release_stats()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_midsize_gmm_default_dispatch(pkg, orc, gpu, seed):
+    """GMM volumes (K = 8 / 16 / 32) of 40-96 voxels an axis at frames up to
+    512 x 384 against the oracle's GMM march"""
+    import torch
+    from test_gpu_gmm import check, gmm_render
+    rng = np.random.default_rng(6000 + seed)
+    dims = tuple(int(v) for v in rng.integers(40, 97, 3))
+    K = int(rng.choice([8, 16, 32]))
+    W, H = int(rng.integers(192, 513)), int(rng.integers(128, 385))
+    method = int(rng.choice([1, 2]))
+    m, kind, ang = draw_dispatch_camera(pkg, rng)
+    wm, sg = orc.synth_gmm(*dims, K, seed=seed)
+    pkg.init_gmm(wm, sg)
+    try:
+        got = gmm_render(pkg, W, H, m, method, torch)
+        ref = orc.render_gmm(wm, sg, dims, orc.make_params(W, H, m, query_method=method))
+        what = (f"seed {seed}: GMM {dims} K={K} {W}x{H} m{method} view {kind} "
+                f"({ang[0]:.1f}, {ang[1]:.1f}) kernel {pkg.last_kernel()}")
+        print(what)
+        check(got, ref, what)
+    finally:
+        pkg.free_gmm()
