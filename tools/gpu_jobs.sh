@@ -10,6 +10,9 @@
 #   bash tools/gpu_jobs.sh quad2   -> quad2 parity, C1 rank wave timelines, rank_sim_1024x8_C1_quad2.log
 #   bash tools/gpu_jobs.sh segc0   -> C0 rank lists: wave timeline and the ray-segmented variants
 #   bash tools/gpu_jobs.sh baked   -> baked full frames: wave timeline, segmented / pipelined variants
+#   bash tools/gpu_jobs.sh pmcb    -> pmc_issue_baked_vs_headline.log (tools/pmc_sets.txt passes; summary:
+#                                     tools/pmc_summary.py gpurun_out/pmcb/<C0baked|C1baked|C0> <kernel>)
+#   bash tools/gpu_jobs.sh wide    -> bench_1024x16_*, bench_1024x32_*, bench_512x32_* (no CPU baseline)
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
 J=${1:?job}; O=gpurun_out/$J; mkdir -p $O
 guard() { rc=$1; if [ $rc -ne 0 ]; then echo "$2 failed rc=$rc"; tail -30 $3; exit $rc; fi; }
@@ -49,6 +52,20 @@ segc0)
 baked)
   timeout -k 10 300 python -u tools/wave_timeline.py --camera C0 --world 8 --ranks 0 --env "" --cost --baked > $O/wt.log 2>&1; guard $? wt $O/wt.log
   timeout -k 10 600 python -u tools/bench_variants.py --config 1024x8 --baked --rounds 3 --reps 5 --cameras C0,C1 --env "" VR_PATH=2 VR_PATH=7,VR_SEG=-2 VR_PATH=7,VR_SEG=2 VR_PATH=7,VR_SEG=4 VR_PATH=7,VR_SEG=-4 > $O/variants.log 2>&1; guard $? var $O/variants.log ;;
+pmcb)
+  i=0
+  while read -r CTRS; do
+    i=$((i+1))
+    for W in "C0 --baked" "C1 --baked" "C0"; do
+      N=$(echo $W | tr -d ' -')
+      timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d $O/$N/p$i -o p$i -- python bench.py --camera $W --no-cpu-baseline --no-issue-bounds --steps 3 --warmup 1 > $O/${N}_p$i.log 2>&1; guard $? pmc-$N-$i $O/${N}_p$i.log
+    done
+  done < tools/pmc_sets.txt ;;
+wide)
+  for W in "1024x32 C0 1" "1024x32 C1 1" "1024x32 C0 3" "1024x16 C0 1" "1024x16 C1 1" "512x32 C0 1" "512x32 C1 1"; do
+    read CFG CAM M <<< "$W"
+    timeout -k 10 300 python -u bench.py --config $CFG --camera $CAM --method $M --no-cpu-baseline > $O/bench_${CFG}_${CAM}_m$M.log 2>&1; guard $? wide-$CFG $O/bench_${CFG}_${CAM}_m$M.log
+  done ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
