@@ -110,6 +110,29 @@ def test_full_frame(pkg, orc, gpu, name, cam, method):
         assert_parity(got[:3], ref, f"{name} {cam} m{method} frame {k} ({got[3]})")
 
 
+@pytest.mark.parametrize("name,cam", [("256x4", "C0"), ("512x8", "C0"), ("512x8", "C1"),
+                                      ("1024x8", "C0"), ("1024x8", "C1"), ("1024x8", "S")])
+def test_footprint_count_at_size(pkg, orc, gpu, name, cam):
+    """U of SURVEY.md 8(d) -- the distinct records under every sample's footprint,
+    the numerator of the bench's roofline -- counted on the GPU
+    (vr_count_footprint) equals the oracle's count of the same frame at the
+    BASELINE size (1024^3 x 8 C0: 220 435 750, C1: 399 031 053;
+    tools/oracle_footprint.py, profiles/r03/oracle_U_1024x8.log)"""
+    import torch
+    n, nb, W, H = CONFIGS[name]
+    vol = scene(pkg, orc, name)
+    m = camera(pkg, cam)
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    for method in (1, 3):
+        u = pkg.count_footprint(pkg.make_desc(out, W, H, m, query_method=method))
+        ref = orc.count_footprint(vol, orc.make_params(W, H, m, query_method=method))
+        assert u == ref, f"{name} {cam} m{method}: GPU U {u} != oracle {ref}"
+        if (name, cam, method) == ("1024x8", "C0", 1):
+            assert u == 220435750
+        if (name, cam, method) == ("1024x8", "C1", 1):
+            assert u == 399031053
+
+
 @pytest.mark.parametrize("cam", ["C0", "C1"])
 def test_full_frame_baked(pkg, orc, gpu, cam):
     """config 4 after basicDataProcessing (the reference's own order, C:1200-1221):
