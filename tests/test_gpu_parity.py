@@ -945,6 +945,44 @@ def test_environment_does_not_change_the_kernel(pkg, orc, gpu, monkeypatch):
         pkg.clear_tuning()
 
 
+
+@pytest.mark.parametrize("nb", [1, 2, 4, 8])
+def test_axis_views_segmented(pkg, orc, gpu, nb):
+    """small frames and rank tile lists of views along the volume's z or y take the
+    pipelined ray-segmented march over the axis-rows copy (k_march_segp4_zrows /
+    segp2 / _yrows) by the default dispatch: bit-identical
+    to the oracle, method 3 keeping the one-lane march"""
+    import torch
+    vol = orc.synth_volume(48, 40, 44, nb)
+    pkg.init_distribution(vol)
+    W, H = 88, 68
+    for rot, kern in (((0.0, 90.0), "zrows"), ((90.0, 90.0), "yrows"), ((-10.0, -80.0), "zrows")):
+        m = pkg.camera.display_inv_view(rot)
+        for method in (1, 2, 3):
+            got = gpu_render(pkg, None, W, H, m, method, torch)
+            want = f"k_march_segp4_{kern}<" if method < 3 else f"k_march_pipe_{kern}<"
+            assert pkg.last_kernel().startswith(want), pkg.last_kernel()
+            ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+            assert_parity(got, ref, f"segmented axis view {rot} nb={nb} m{method}")
+        # a 3-rank split: each rank's packed list through the 2-lane windows
+        lists = pkg.tiles.tile_lists(W, H, 3, m)
+        n_slots = lists.shape[1]
+        dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+        packed = torch.full((3, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        for method in (1, 2):
+            for r in range(3):
+                pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=method,
+                                         d_tile_list=dl[r], n_tiles=n_slots))
+                assert pkg.last_kernel().startswith(f"k_march_segp2_{kern}<"), pkg.last_kernel()
+            frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            pkg.unscatter_tiles(packed, dl, 3, n_slots, frame, W, H)
+            torch.cuda.synchronize()
+            ref8 = orc.render(vol, orc.make_params(W, H, m, query_method=method),
+                              want_float=False, want_steps=False)[0]
+            assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref8), (
+                f"segmented axis lists {rot} nb={nb} m{method}")
+
+
 @pytest.mark.parametrize("nb", [1, 2, 4, 8])
 def test_axis_views_take_an_axis_rows_copy(pkg, orc, gpu, nb, tune):
     """views whose screen x runs along the volume's z or y (|M[8]| or |M[4]| >= 0.95)

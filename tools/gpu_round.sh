@@ -32,7 +32,7 @@ for W in $WL; do
   echo "$N $(grep -o '"kernel": "[^"]*", "kernel_ms": [0-9.]*' $O/bench_$N.log)"
 done
 if [ "${RANKSIM:-1}" = 1 ]; then
-  for CAM in C0 C1; do
+  for CAM in C0 C1 S; do
     timeout -k 10 300 python -u tools/rank_sim.py --camera $CAM > $O/rank_sim_$CAM.log 2>&1; guard $? rank-sim-$CAM $O/rank_sim_$CAM.log
   done
 fi

@@ -39,7 +39,7 @@ def main():
         k, v = kv.split("=")
         pkg.set_tuning(k, v)  # tuning knobs: the library reads no environment
     m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
-         else pkg.camera.display_inv_view((30.0, 45.0)))
+         else pkg.camera.display_inv_view((0.0, 90.0) if args.camera == "S" else (30.0, 45.0)))
 
     def timed(fn, warm=3):
         for _ in range(warm):  # a full frame's 2nd render re-deals its tiles (adaptive order)

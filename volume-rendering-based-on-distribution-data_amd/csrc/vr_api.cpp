@@ -566,7 +566,12 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // VR_SEG_RAYS overrides the ray-count threshold.
     uint64_t seg_rays = 700000;
     if (const char *e = vr::tuning("VR_SEG_RAYS")) seg_rays = std::strtoull(e, nullptr, 10);
-    if (along_rows && d->d_tile_list && (d->query_method == 1 || d->query_method == 2) &&
+    // Views along the volume's z or y (axis-rows copy) split the rays of such
+    // lists the same way, the windows' gathers addressed in the copy
+    // (k_march_segp2_zrows: cost-dealt side-view 1024^3 x 8 lists, max over
+    // ranks, N = 8 0.399 -> 0.247 ms, N = 4 0.543 -> 0.445; the one-lane march's
+    // step chain bound them; profiles/r03/rank_sim_1024x8_S*.log).
+    if (row_like && d->d_tile_list && (d->query_method == 1 || d->query_method == 2) &&
         (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= seg_rays)
         P.path = 7;
     // Oblique views of a volume coarse for the frame (>= 4 pixels per voxel of
@@ -622,7 +627,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
             small_seg = rays <= 131072 ? -4 : -2;
         }
     }
-    if (P.path != 2) P.axis_view = 0;  // a small frame keeps the segmented march
+    if (P.path != 2 && P.path != 7) P.axis_view = 0;  // 7: the segmented march reads the copy too
     if (const char *e = vr::tuning("VR_PATH")) {
         const int v = std::atoi(e);
         if (v == 0 || v == 1 || v == 2 || v == 4 || v == 7) {

@@ -65,7 +65,7 @@ __device__ __forceinline__ void composite_window(const Params &P, float smp, uin
 #define VR_SEG_WAVES 1   // minimum waves per SIMD the register allocation must allow
 #endif
 // part `part` (256/S of its rays) of the tile in launch slot `slot`
-template <int B, int M, int S, bool PIPE>
+template <int B, int M, int S, bool PIPE, int GM>
 __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, const Params &P,
                                                uint32_t slot, uint32_t part) {
     constexpr int RPW = 256 / S;  // rays per workgroup
@@ -123,7 +123,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
             if (valid) {
                 const Foot f = footprint(P, px, py, pz);
                 float rec[8][B];
-                gather8<B, kGatherMode<M>>(vol, P, f, rec);
+                gather8<B, GM>(vol, P, f, rec);
                 smp = decode8<B, M>(P, rec, f);
             }
             const uint64_t vm = __ballot(valid);
@@ -138,7 +138,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
         bool va = geom((int)k, t), vb = false;
         if (va) {
             fa = footprint(P, px, py, pz);
-            gather8<B, kGatherMode<M>>(vol, P, fa, ra);
+            gather8<B, GM>(vol, P, fa, ra);
         }
         // one window: gather the next into (fn, rn, vn) while (fc, rc, vc) decodes
         auto window = [&](const Foot &fc, const float (&rc)[8][B], bool vc, Foot &fn,
@@ -148,7 +148,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
             vn = alive && geom(base + S + (int)k, tn);
             if (vn) {
                 fn = footprint(P, nx, ny, nz);
-                gather8<B, kGatherMode<M>>(vol, P, fn, rn);
+                gather8<B, GM>(vol, P, fn, rn);
             }
             float smp = 0.0f;
             if (vc && alive) smp = decode8<B, M>(P, rc, fc);
@@ -172,13 +172,15 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
                     sw * P.brightness);
 }
 
-template <int B, int M, int S, bool PIPE>
+// GM: gather8's addressing (kGatherMode<M>; 3 = an axis-rows copy of the records,
+// the views whose screen x runs along the volume's z or y)
+template <int B, int M, int S, bool PIPE, int GM = kGatherMode<M>>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVES, 8))) void k_march_seg(const float *__restrict__ vol, Params P) {
     const uint32_t b = blockIdx.x;
     const uint32_t slot = (b & 7u) + 8u * (b / (8u * S)), part = (b >> 3) % S;
     unsigned long long t0 = 0;
     if (P.wave_clock) t0 = wall_clock64();
-    march_seg_part<B, M, S, PIPE>(vol, P, slot, part);
+    march_seg_part<B, M, S, PIPE, GM>(vol, P, slot, part);
     if (P.wave_clock && (threadIdx.x & 63u) == 0 && slot < P.n_tiles) {  // tooling
         unsigned long long *w = P.wave_clock + ((uint64_t)slot * 16u + part * 4u + threadIdx.x / 64u) * 3u;
         w[0] = t0;
@@ -212,9 +214,34 @@ static hipError_t seg_launch(int method, const float *vol, const Params &P, uint
     return hipGetLastError();
 }
 
+// pipelined windows over an axis-rows copy (P.avol, strides P.asx / asy / asz):
+// methods 1/2/3, the record march's arithmetic, gathers addressed in the copy
+template <int B, int S>
+static hipError_t seg_axis_launch(int method, const Params &P, uint32_t nslots, hipStream_t s) {
+    const dim3 grid(((nslots + 7u) / 8u) * 8u * S), block(256);
+    Params Q = P;
+    Q.sx = P.asx;
+    Q.sy = P.asy;
+    Q.sz = P.asz;
+    switch (method) {
+    case 1: hipLaunchKernelGGL((k_march_seg<B, 1, S, true, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+    case 2: hipLaunchKernelGGL((k_march_seg<B, 2, S, true, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+    case 3: hipLaunchKernelGGL((k_march_seg<B, 3, S, true, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <int B>
 static bool seg_b(int method, int S, const float *vol, const Params &P, uint32_t nslots,
                   hipStream_t s, hipError_t &err) {
+    if (P.avol && method >= 1 && method <= 3) {  // axis views: pipelined windows only
+        switch (S) {
+        case -2: err = seg_axis_launch<B, 2>(method, P, nslots, s); return true;
+        case -4: err = seg_axis_launch<B, 4>(method, P, nslots, s); return true;
+        default: return false;
+        }
+    }
     // S > 0: plain windows; S < 0: pipelined windows of |S| lanes (the
     // dispatch uses 4, -2 and -4; 2 is kept as the plain counterpart of -2)
     switch (S) {
@@ -239,7 +266,8 @@ bool launch_march_seg(int nb, int method, int S, const float *vol, const Params 
     }
     if (ok) {
         char kind[32];
-        snprintf(kind, sizeof kind, S < 0 ? "k_march_segp%d" : "k_march_seg%d", S < 0 ? -S : S);
+        snprintf(kind, sizeof kind, S < 0 ? "k_march_segp%d%s" : "k_march_seg%d%s", S < 0 ? -S : S,
+                 (P.avol && method >= 1 && method <= 3) ? (P.asy == 1 ? "_yrows" : "_zrows") : "");
         note_kernel(kind, nb, method);
     }
     return ok;
