@@ -558,23 +558,28 @@ def main():
                                args.dist_backend)
     n_slots = lists.shape[1]
     frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    # N > 1: a ring of RING packed buffers (and gather targets on rank 0): frame f
+    # renders into buffer f % RING, so it waits only for the gather and the
+    # assembly of frame f - RING, which had RING - 1 frames to finish.  With two
+    # buffers the next-but-one render waited for the gather of the frame just
+    # before it, which gets its CUs only as that frame's waves drain
+    # (tools/host_cost.py, profiles/r04/host_cost_*.log).
+    RING = 4 if world > 1 else 1
     with torch.cuda.stream(stream):
         if world > 1:
-            # two packed buffers (and two gather targets on rank 0): frame f+1 renders
-            # while the gather and rank 0's assembly of frame f are in flight
-            packed = [torch.zeros(n_slots * 256, dtype=torch.int32, device=dev) for _ in range(2)]
+            packed = [torch.zeros(n_slots * 256, dtype=torch.int32, device=dev) for _ in range(RING)]
             recv = ([torch.empty((world, n_slots * 256), dtype=torch.int32, device=dev)
-                     for _ in range(2)] if rank == 0 else [None, None])
+                     for _ in range(RING)] if rank == 0 else [None] * RING)
             my_list = torch.from_numpy(lists[rank].view(np.int32).copy()).to(dev)
             all_lists = torch.from_numpy(lists.view(np.int32).copy()).to(dev)
             descs = [pkg.make_desc(packed[b], W, H, m, query_method=args.method,
-                                   d_tile_list=my_list, n_tiles=n_slots) for b in range(2)]
+                                   d_tile_list=my_list, n_tiles=n_slots) for b in range(RING)]
         else:
             descs = [pkg.make_desc(frame, W, H, m, query_method=args.method)]
     desc = descs[0]
     torch.cuda.synchronize()
     assemble = torch.cuda.Stream(device=dev) if world > 1 else None
-    works, assembled = [None, None], [None, None]
+    works, assembled = [None] * RING, [None] * RING
 
     # algorithmic bytes of one launch on this rank: the volume bytes
     # under the footprints (U*S_rec; codec: codebook + used error pairs) + pixels*4.
@@ -610,21 +615,25 @@ def main():
     nframe = [0]
 
     def step(timed):
-        b = nframe[0] % 2
+        b = nframe[0] % RING
         nframe[0] += 1
         with torch.cuda.stream(stream):
             if world == 1:
                 frame.zero_()  # C:208 (tile slots need none: misses are written as 0)
             else:
                 if works[b] is not None:
-                    works[b].wait()           # the gather of frame f-2 has read packed[b]
+                    works[b].wait()           # the gather of frame f - RING has read packed[b]
                 if assembled[b] is not None:
                     stream.wait_event(assembled[b])  # rank 0 has unscattered recv[b]
+            # per-frame timing events only at N = 1: between the render, the gather
+            # and the assembly streams of N > 1 they cost the frame loop ~0.1 ms per
+            # frame (tools/host_cost.py); N > 1 times its renders after the loop
+            timed = timed and world == 1
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-            pkg.render(descs[b % len(descs)])
+            pkg.render(descs[b])
             if timed:
                 e1.record(stream)
                 ev.append((e0, e1))
@@ -643,6 +652,9 @@ def main():
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
+    # layout copies the view needed (micro-bricks / axis rows, include/vr.h): made
+    # synchronously inside the first warm-up frame, whose extra cost this reports
+    layout = pkg.layout_info()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -660,7 +672,25 @@ def main():
                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if world > 1:
+        # this rank's render alone (untimed, after the loop): HIP events around 5
+        # renders of its list; the line reports the max over ranks
+        torch.cuda.synchronize()
+        with torch.cuda.stream(stream):
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                pkg.render(descs[0])
+                e1.record(stream)
+                ev.append((e0, e1))
+        torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    render_ms_max = kern_ms
+    if world > 1:
+        t = torch.tensor([kern_ms], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        render_ms_max = float(t.item())
     if args.dump_frame and rank == 0:
         np.save(args.dump_frame, frame.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
@@ -697,6 +727,8 @@ def main():
         gather_bytes = int(check[2][check[2] > 0].astype(np.int64).sum()) * 8 * rec_bytes
     ms_per_step = elapsed / args.steps * 1e3
     value = W * H / (elapsed / args.steps) / 1e6
+    phys = min(world, max(ndev, 1))
+    rehearsal = world > phys
     out = None
     if rank == 0:
         cpu, parity = None, None
@@ -715,13 +747,17 @@ def main():
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
+            # devices the ranks actually ran on: a gloo rehearsal of N ranks on
+            # fewer GPUs is not an N-GPU measurement (scaling null)
+            "physical_gpus": phys,
+            "rehearsal_shared_gpus": rehearsal,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(1e3 / ms_per_step, 2),
             "host_issue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": None if rehearsal else "strong",
             "vs_baseline": None,
             "dtype": "f32 (f64 decode terms)",
             "data": f"synthetic seeded distribution volume (seed {SEED}, DESIGN.md s5)",
@@ -733,6 +769,7 @@ def main():
                 "statistics": ("baked once by basicDataProcessing (f32 statistics planes)"
                                if args.baked else "decoded from the records at every step"),
                 "bake_ms": round(bake_ms, 3) if bake_ms is not None else None,
+                "layout_copies": layout,
                 "tile_deal": (None if world == 1 else "estimate" if args.no_balance
                               else "measured cost (one untimed frame)"),
                 "parallelism": f"image tiles x{world}" + (
@@ -747,6 +784,7 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": kernel,
                 "kernel_ms": round(kern_ms, 4),
+                "render_ms_max_over_ranks": round(render_ms_max, 4) if world > 1 else None,
                 "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
                 "U_records": int(u) if u is not None else None,
                 "compute": bounds,

@@ -129,12 +129,25 @@ void dataProcessing(void);
  * max(4 GiB, 5 %) free after it).  Views whose screen x runs along the volume's
  * z or y axis (|M[8]| or |M[4]| >= 0.95) of an owned volume with 1, 2, 4 or 8
  * bins get an axis-rows copy (that axis contiguous) on the same terms, one
- * axis at a time.  vr_release_stats drops the copies with the planes, so after
- * an in-place modification the next frame that needs one rebuilds it. */
+ * axis (both a y and a z copy when they fit; one is dropped for the other only
+ * when that makes room).  vr_release_stats drops the copies with the planes, so
+ * after an in-place modification the next frame that needs one rebuilds it. */
 int vr_bake_stats(void);
 int vr_release_stats(void);
 int vr_stats_info(const float **d_raw, uint64_t *raw_plane, const float **d_codec,
                   uint64_t *codec_plane);
+
+/* Layout copies (the micro-brick and axis-rows copies above) are made only
+ * within a byte budget: vr_set_layout_budget(bytes) caps their total HBM
+ * (default UINT64_MAX: limited only by the free-memory guard; 0 = never make
+ * one, every view marches the records' x rows) and drops resident copies that
+ * exceed a lowered budget.  vr_layout_info: bytes resident in copies, copies
+ * made since load, and the time and size of the last one made (each is built
+ * synchronously inside the first frame that needs it, so that frame costs
+ * last_build_ms more). */
+int vr_set_layout_budget(uint64_t bytes);
+int vr_layout_info(uint64_t *resident_bytes, int *builds, float *last_build_ms,
+                   uint64_t *last_build_bytes);
 
 /* last error message ("" if none); vr_clear_error resets it */
 const char *vr_last_error(void);

@@ -69,6 +69,8 @@ def lib():
         L.orc_splitmix64.restype = ctypes.c_uint64
         L.orc_max_threads.argtypes = []
         L.orc_max_threads.restype = ctypes.c_int
+        L.orc_set_reading.argtypes = [ctypes.c_int] * 3
+        L.orc_set_reading.restype = None
         L.orc_synth_fill.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_uint64, fp, ctypes.c_int]
         L.orc_flex_corner.argtypes = [ctypes.POINTER(Flex), ctypes.c_int, ctypes.c_int,
@@ -195,6 +197,14 @@ def synth_codec(nx, ny, nz, nbins, ntemplates=24, slots=None, seed=20261015):
 
 def _fp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def set_reading(w_trunc=0, rsqrt_ulps=0, log_ulps=0) -> None:
+    """Parity-margin study only (tools/parity_margin.py): render with another
+    reading of what the reference leaves open -- texture weights truncated
+    (K:601/619/683), rsqrtf moved by ulps (K:295), per-bin logf moved by ulps
+    (K:766).  set_reading() restores the canonical reading."""
+    lib().orc_set_reading(int(w_trunc), int(rsqrt_ulps), int(log_ulps))
 
 
 def max_threads() -> int:

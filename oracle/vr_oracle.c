@@ -44,8 +44,45 @@ static const f4 TF[9] = {
 
 static inline float logf_cr(float x) { return (float)log((double)x); }
 
+/* Alternative readings of the arithmetic the reference leaves open, for the
+ * parity-margin study only (orc_set_reading, tools/parity_margin.py, DESIGN.md
+ * section 3.1); all zero = the canonical reading every test pins:
+ *   g_w_trunc    1: texture filter weights truncated to 8 fractional bits
+ *                (K:601/619/683) instead of rounded to nearest;
+ *   g_rsqrt_ulps rsqrtf of helper_math normalize (K:295) moved this many ulps
+ *                from the correctly rounded 1/sqrtf;
+ *   g_log_ulps   the per-bin float log of the entropy (K:766) moved this many
+ *                ulps from (float)log((double)x). */
+static int g_w_trunc = 0, g_rsqrt_ulps = 0, g_log_ulps = 0;
+
+void orc_set_reading(int w_trunc, int rsqrt_ulps, int log_ulps) {
+    g_w_trunc = w_trunc;
+    g_rsqrt_ulps = rsqrt_ulps;
+    g_log_ulps = log_ulps;
+}
+
+static inline float ulp_step(float x, int k) {
+    for (; k > 0; k--) x = nextafterf(x, INFINITY);
+    for (; k < 0; k++) x = nextafterf(x, -INFINITY);
+    return x;
+}
+
+/* rsqrtf(dot(v, v)) of normalize (K:295) */
+static inline float rsqrt_read(float x) {
+    const float r = 1.0f / sqrtf(x);
+    return g_rsqrt_ulps ? ulp_step(r, g_rsqrt_ulps) : r;
+}
+
+/* log(pr) of the entropy's per-bin term (K:766) */
+static inline float logf_bin(float x) {
+    const float r = logf_cr(x);
+    return (g_log_ulps && r != 0.0f) ? ulp_step(r, g_log_ulps) : r;
+}
+
 /* 9-bit fixed point weight with 8 fractional bits */
-static inline float q8(float a) { return rintf(a * 256.0f) * (1.0f / 256.0f); }
+static inline float q8(float a) {
+    return (g_w_trunc ? floorf(a * 256.0f) : rintf(a * 256.0f)) * (1.0f / 256.0f);
+}
 
 static inline float clamp01(float u) { return fminf(fmaxf(u, 0.0f), 1.0f); }
 
@@ -136,7 +173,7 @@ static void stats3(const float *p, int nbins, float enorm, int want, float out[3
     if (want & 4) {
         for (int i = 0; i < nbins; i++) { /* K:762-767 */
             float pr = p[i];
-            double t = pr <= 0 ? 0.0 : ((double)logf_cr(pr) / LN2_D);
+            double t = pr <= 0 ? 0.0 : ((double)logf_bin(pr) / LN2_D);
             ent = (float)((double)ent + (double)pr * t);
         }
         ent = -ent;          /* K:768 */
@@ -219,7 +256,7 @@ static void codec_stats3(const orc_codec *c, int nbins, float enorm, size_t vidx
     float ent = 0.0f;
     for (int i = 0; i < nbins; i++) {
         float pr = dec[i];
-        double t = pr <= 0 ? 0.0 : ((double)logf_cr(pr) / LN2_D);
+        double t = pr <= 0 ? 0.0 : ((double)logf_bin(pr) / LN2_D);
         ent = (float)((double)ent + (double)pr * t);
     }
     ent = -ent;
@@ -389,7 +426,7 @@ static int render_pixel(const vol_t *v, const orc_render_params *p, int x, int y
     o.y = 0.0f * M[4] + 0.0f * M[5] + 0.0f * M[6] + 1.0f * M[7];
     o.z = 0.0f * M[8] + 0.0f * M[9] + 0.0f * M[10] + 1.0f * M[11];
     f3 d0 = {u, vv, -2.0f};
-    float inv = 1.0f / sqrtf(dot3(d0, d0));
+    float inv = rsqrt_read(dot3(d0, d0));
     d0.x = d0.x * inv; d0.y = d0.y * inv; d0.z = d0.z * inv;
     f3 d;
     d.x = d0.x * M[0] + d0.y * M[1] + d0.z * M[2];
@@ -876,7 +913,7 @@ int orc_flex_process(const orc_flex *f, float *blocks) {
         float ent = 0.0f; /* K:1106-1115 */
         for (int i = 0; i < nb; i++) {
             const float pr = h[i];
-            const double t = pr <= 0 ? 0.0 : ((double)logf_cr(pr) / LN2_D);
+            const double t = pr <= 0 ? 0.0 : ((double)logf_bin(pr) / LN2_D);
             ent = (float)((double)ent + (double)pr * t);
         }
         ent = -ent;
@@ -1036,7 +1073,7 @@ static int gmm_ray(const orc_render_params *p, int x, int y, f3 *o, f3 *d, float
     o->y = 0.0f * M[4] + 0.0f * M[5] + 0.0f * M[6] + 1.0f * M[7];
     o->z = 0.0f * M[8] + 0.0f * M[9] + 0.0f * M[10] + 1.0f * M[11];
     f3 d0 = {u, vv, -2.0f};
-    float inv = 1.0f / sqrtf(dot3(d0, d0));
+    float inv = rsqrt_read(dot3(d0, d0));
     d0.x = d0.x * inv; d0.y = d0.y * inv; d0.z = d0.z * inv;
     d->x = d0.x * M[0] + d0.y * M[1] + d0.z * M[2];
     d->y = d0.x * M[4] + d0.y * M[5] + d0.z * M[6];

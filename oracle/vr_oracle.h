@@ -132,6 +132,10 @@ void orc_synth_codec(int nx, int ny, int nz, int nbins, int ntpl, int slots, uin
                      int32_t *codebook, float *templates, float *errors);
 uint64_t orc_splitmix64(uint64_t x);
 int orc_max_threads(void);
+/* parity-margin study only: alternative readings of the texture weights, rsqrtf
+ * and logf (vr_oracle.c g_w_trunc / g_rsqrt_ulps / g_log_ulps); (0, 0, 0) =
+ * the canonical reading.  Not thread-safe: set it before a render. */
+void orc_set_reading(int w_trunc, int rsqrt_ulps, int log_ulps);
 void orc_synth_fill(int nx, int ny, int nz, int nbins, uint64_t seed, float *vol,
                     int nthreads);
 

@@ -95,11 +95,15 @@ def test_flex_table_validation_without_gpu(pkg, orc):
 
 def test_render_kernel_launch_configuration_without_gpu(pkg):
     """render_kernel validates gridSize / blockSize like a CUDA launch would
-    (K:2397): an empty grid or block, or > 1024 threads per block, is an
-    invalid configuration, recorded before any device call"""
+    (K:2397): an empty grid or block, > 1024 threads per block, a block
+    dimension beyond (1024, 1024, 64) or a grid beyond (2^31 - 1, 65535, 65535)
+    is an invalid configuration, recorded before any device call"""
     L = pkg._lib.load()
     for grid, block in (((0, 1, 1), (16, 16, 1)), ((4, 0, 1), (16, 16, 1)),
-                        ((4, 4, 1), (16, 16, 0)), ((4, 4, 1), (64, 32, 1))):
+                        ((4, 4, 1), (16, 16, 0)), ((4, 4, 1), (64, 32, 1)),
+                        ((4, 4, 1), (1, 1, 65)), ((4, 4, 1), (1, 1025, 1)),
+                        ((4, 65536, 1), (16, 16, 1)), ((4, 4, 65536), (16, 16, 1)),
+                        ((2 ** 31, 1, 1), (16, 16, 1))):
         with pytest.raises(pkg.VRError) as e:
             pkg.render_kernel(grid, block, 0x1000, 64, 64, 0.05, 1.0, 0.0, 1.0, 1, (4, 4, 4))
         assert e.value.status == pkg._lib.VR_ERR_ARG

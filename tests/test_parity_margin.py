@@ -1,0 +1,78 @@
+"""Parity margin against the readings the reference leaves open (CPU).
+
+The oracle pins one canonical reading of what the reference does not fix
+(DESIGN.md section 3): texture filter weights rounded to 8 fractional bits,
+rsqrtf as the correctly rounded 1/sqrtf (helper_math normalize, K:295), the
+float log as (float)log((double)x) (K:766).  tools/parity_margin.py renders the
+BASELINE configs with each alternative reading and counts how far the frame
+moves (profiles/r04/parity_margin.json).  These tests pin
+those figures at the two configs the CPU renders in a second, so a change to the
+oracle's arithmetic cannot silently change the stated risk.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import parity_margin  # noqa: E402
+
+# (config, method, variant) -> (RGBA8 mismatches, pixels over 1e-4, samples mismatches,
+# max byte difference) against the canonical frame, camera C0, whole frame
+PINNED = {
+    ("128x1", 1, "weights truncated"): (4839, 12318, 947, 2),
+    ("128x1", 1, "rsqrtf +1 ulp"): (3, 20, 0, 1),
+    ("128x1", 1, "rsqrtf -2 ulp"): (3, 13, 0, 1),
+    ("256x4", 1, "weights truncated"): (43417, 114894, 8570, 1),
+    ("256x4", 1, "rsqrtf +1 ulp"): (43, 228, 6, 1),
+    ("256x4", 1, "rsqrtf -1 ulp"): (42, 225, 8, 1),
+    ("256x4", 3, "rsqrtf +1 ulp"): (388, 4151, 42, 1),
+    ("256x4", 3, "logf +1 ulp"): (1, 15, 1, 1),
+    ("256x4", 3, "logf -1 ulp"): (1, 18, 0, 1),
+}
+
+
+@pytest.fixture(scope="module")
+def orc():
+    import __graft_entry__ as g
+    o = g.load_oracle()
+    yield o
+    o.set_reading()
+
+
+@pytest.mark.parametrize("cfg", ["128x1", "256x4"])
+def test_margin_figures_are_pinned(orc, cfg):
+    n, nb, W, H = parity_margin.SIZES[cfg]
+    vol = orc.synth_volume(n, n, n, nb, 20261015)
+    m = parity_margin.camera("C0")
+    for method in (1, 3):
+        keys = [k for k in PINNED if k[0] == cfg and k[1] == method]
+        if not keys:
+            continue
+        p = orc.make_params(W, H, m, query_method=method)
+        orc.set_reading()
+        ref = orc.render(vol, p)[:3]
+        for key in keys:
+            orc.set_reading(*parity_margin.VARIANTS[key[2]][0])
+            got = orc.render(vol, p)[:3]
+            orc.set_reading()
+            c = parity_margin.compare(ref, got)
+            assert (c["rgba8_mismatch"], c["over_1e-4"], c["steps_mismatch"],
+                    c["max_byte_diff"]) == PINNED[key], key
+
+
+def test_canonical_reading_is_restored(orc):
+    """set_reading() with no arguments is the reading every other test pins."""
+    vol = orc.synth_volume(24, 20, 16, 8)
+    p = orc.make_params(64, 48, parity_margin.camera("C1"), query_method=1)
+    a = orc.render(vol, p)[0]
+    orc.set_reading(1, 2, 1)
+    b = orc.render(vol, p)[0]
+    orc.set_reading()
+    c = orc.render(vol, p)[0]
+    assert np.array_equal(a, c)
+    assert not np.array_equal(a, b)

@@ -1,0 +1,176 @@
+"""Per-frame host cost of bench.py's N > 1 frame loop, on one GPU (tooling).
+
+bench.py's step() at N > 1 issues, per frame: the wait on the gather that last
+read the packed buffer (a ring of RING buffers), the wait on rank 0's last
+assembly, the render of this rank's tile list (ctypes -> vr_render), the
+asynchronous RCCL gather, and on rank 0 the unscatter on the assembly stream
+(two vr_set_stream calls, an event).  Round 3's loop also recorded two timing
+events per frame and had a ring of 2; both are kept as variants here.  This replays rank 0's loop for an N-rank
+split with a one-rank NCCL group (the gather of an N-rank group cannot be
+issued on one GPU; a one-rank gather's host path is the same torch/RCCL call,
+one peer instead of N) and reports
+
+  * dry: the host time per frame with every render stubbed (tuning knob
+    VR_DRY: the library fills the launch parameters, chooses the kernel and
+    returns without launching) -- what the issuing thread costs a frame;
+  * live: the frame period of the same loop with the real renders of rank 0's
+    list and the unscatter of N buffers -- max(GPU, host) per frame when the
+    host keeps ahead;
+  * the components (render call, gather call, unscatter call) in isolation.
+
+  python tools/host_cost.py [--config 1024x8] [--camera C0] [--world 8] [--frames 300]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="1024x8")
+    ap.add_argument("--camera", default="C0")
+    ap.add_argument("--method", type=int, default=1)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--port", default="29533")
+    ap.add_argument("--env", default="", help="tuning knobs NAME=VALUE[,...] for the live loop")
+    ap.add_argument("--priority", type=int, default=0,
+                    help="torch stream priority of the render stream (-1 = high)")
+    args = ap.parse_args()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", args.port)
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as g
+    import bench
+    pkg = g.load_package()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    n, nb, W, H = bench.CONFIGS[args.config]
+    pkg.synthesize((n, n, n), nb, bench.SEED)
+    for kv in filter(None, args.env.split(",")):
+        k, v = kv.split("=")
+        pkg.set_tuning(k, v)
+    m = bench.camera_matrix(pkg, args.camera)
+    N = args.world
+    # the cost-dealt lists bench.py renders at N > 1 (per-tile costs of one full frame)
+    full = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    steps = torch.full((W * H,), -1, dtype=torch.int32, device=dev)
+    pkg.render(pkg.make_desc(full, W, H, m, query_method=args.method, d_steps=steps))
+    lists = pkg.tiles.tile_lists_by_cost(W, H, N, pkg.tiles.tile_costs_from_frame(
+        steps.cpu().numpy(), W, H))
+    slots = lists.shape[1]
+    stream = torch.cuda.Stream(device=dev, priority=args.priority)
+    assemble = torch.cuda.Stream(device=dev)
+    pkg.set_stream(stream)
+    frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    with torch.cuda.stream(stream):
+        packed = [torch.zeros(slots * 256, dtype=torch.int32, device=dev) for _ in range(4)]
+        recv1 = [torch.empty((1, slots * 256), dtype=torch.int32, device=dev) for _ in range(4)]
+        recvN = torch.zeros((N, slots * 256), dtype=torch.int32, device=dev)
+        my_list = torch.from_numpy(lists[0].view(np.int32).copy()).to(dev)
+        all_lists = torch.from_numpy(lists.view(np.int32).copy()).to(dev)
+        descs = [pkg.make_desc(packed[b], W, H, m, query_method=args.method,
+                               d_tile_list=my_list, n_tiles=slots) for b in range(4)]
+    torch.cuda.synchronize()
+    works, assembled, ev = [None] * 4, [None] * 4, []
+    nframe = [0]
+
+    def step(events=False, gather=True, unscatter=True, ring=4):  # bench.py step(), N > 1, rank 0
+        b = nframe[0] % ring
+        nframe[0] += 1
+        with torch.cuda.stream(stream):
+            if works[b] is not None:
+                works[b].wait()
+            if assembled[b] is not None:
+                stream.wait_event(assembled[b])
+            if events:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            pkg.render(descs[b])
+            if events:
+                e1.record(stream)
+                ev.append((e0, e1))
+            works[b] = (dist.gather(packed[b], gather_list=list(recv1[b].unbind(0)), dst=0,
+                                    async_op=True) if gather else None)
+        if unscatter:
+            with torch.cuda.stream(assemble):
+                if works[b] is not None:
+                    works[b].wait()
+                pkg.set_stream(assemble)
+                pkg.unscatter_tiles(recvN, all_lists, N, slots, frame, W, H)
+                pkg.set_stream(stream)
+                done = torch.cuda.Event()
+                done.record(assemble)
+                assembled[b] = done
+        else:
+            assembled[b] = None
+
+    def loop(k, **kw):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step(**kw)
+        t_issue = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        return t_issue / k * 1e3, (time.perf_counter() - t0) / k * 1e3
+
+    def each(fn, k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        dt = (time.perf_counter() - t0) / k * 1e3
+        torch.cuda.synchronize()
+        return dt
+
+    print(f"{args.config} {args.camera} m{args.method}, rank 0 of {N}: {slots} slots "
+          f"({slots * 256} rays), one-rank NCCL group, GPU_MAX_HW_QUEUES="
+          f"{os.environ.get('GPU_MAX_HW_QUEUES', '(unset)')}, render stream priority "
+          f"{args.priority}", flush=True)
+    # dry: renders stubbed
+    pkg.set_tuning("VR_DRY", "1")
+    loop(50)
+    issue, period = loop(args.frames)
+    with torch.cuda.stream(stream):
+        t_render = each(lambda: pkg.render(descs[0]), args.frames)
+        t_gather = each(lambda: dist.gather(packed[0], gather_list=list(recv1[0].unbind(0)),
+                                            dst=0, async_op=True), args.frames)
+    t_unsc = each(lambda: pkg.unscatter_tiles(recvN, all_lists, N, slots, frame, W, H), args.frames)
+    print(f"  dry  (renders stubbed): host issue {issue:.4f} ms/frame, period {period:.4f} ms/frame",
+          flush=True)
+    print(f"  host calls alone: vr_render {t_render:.4f} ms (no launch), dist.gather {t_gather:.4f} ms, "
+          f"unscatter {t_unsc:.4f} ms", flush=True)
+    pkg.set_tuning("VR_DRY", "0")
+    for kw in ({}, {"ring": 2}, {"events": True, "ring": 2}, {"events": True},
+               {"gather": False, "unscatter": False},
+               {"events": True, "gather": False, "unscatter": False}):
+        works[:] = [None] * 4
+        assembled[:] = [None] * 4
+        ev.clear()
+        loop(50, **kw)
+        ev.clear()
+        issue, period = loop(args.frames, **kw)
+        what = ",".join(f"{k}={v}" for k, v in kw.items()) or "bench step (ring 4, no events)"
+        if ev:
+            kern = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+            gap = float(np.median([ev[i][1].elapsed_time(ev[i + 1][0]) for i in range(len(ev) - 1)]))
+            print(f"  live [{what}] ({pkg.last_kernel()}): host issue {issue:.4f} ms/frame, frame period "
+                  f"{period:.4f} ms, render (HIP events) {kern:.4f} ms, median gap between renders "
+                  f"{gap:.4f} ms", flush=True)
+        else:
+            print(f"  live [{what}]: host issue {issue:.4f} ms/frame, frame period {period:.4f} ms",
+                  flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

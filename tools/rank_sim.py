@@ -26,6 +26,14 @@ def main():
     ap.add_argument("--no-lpt", action="store_true", help="tile lists without longest-first order")
     ap.add_argument("--baked", action="store_true", help="bake the statistics planes first")
     ap.add_argument("--env", default="", help="tuning knobs NAME=VALUE[,NAME=VALUE] (vr_set_tuning) for the renders")
+    ap.add_argument("--envs", nargs="*", default=None,
+                    help="several knob sets (each NAME=VALUE[,...]; '' = defaults) timed in turn "
+                         "on the same lists, so variants share one process and one GPU state")
+    ap.add_argument("--worlds", default="2,4,8")
+    ap.add_argument("--modes", default="est,cost")
+    ap.add_argument("--host-ms", type=float, default=0.0,
+                    help="per-frame host issue cost of the N > 1 frame loop (tools/host_cost.py); "
+                         "reported as a second, conservative speed-up with it added")
     args = ap.parse_args()
     import torch
     import __graft_entry__ as g
@@ -35,9 +43,12 @@ def main():
     pkg.synthesize((n, n, n), nb, bench.SEED)
     if args.baked:
         pkg.bake_stats()
-    for kv in filter(None, args.env.split(",")):
-        k, v = kv.split("=")
-        pkg.set_tuning(k, v)  # tuning knobs: the library reads no environment
+    def knobs(spec):
+        pkg.clear_tuning()
+        for kv in filter(None, spec.split(",")):
+            k, v = kv.split("=")
+            pkg.set_tuning(k, v)  # tuning knobs: the library reads no environment
+    knobs(args.env)
     m = (pkg.camera.single_test_inv_view() if args.camera == "C0"
          else pkg.camera.display_inv_view((0.0, 90.0) if args.camera == "S" else (30.0, 45.0)))
 
@@ -72,7 +83,9 @@ def main():
     steps = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
     pkg.render(pkg.make_desc(full, W, H, m, query_method=args.method, d_steps=steps))
     cost = pkg.tiles.tile_costs_from_frame(steps.cpu().numpy(), W, H)
-    modes = [("est", w) for w in (2, 4, 8)] + [("cost", w) for w in (2, 4, 8)]
+    worlds = [int(w) for w in args.worlds.split(",")]
+    modes = [(md, w) for md in args.modes.split(",") for w in worlds]
+    envs = args.envs if args.envs is not None else [args.env]
     for mode, world in modes:
         if mode == "est":
             lists = pkg.tiles.tile_lists(W, H, world, None if args.no_lpt else m)
@@ -83,17 +96,25 @@ def main():
         dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
         descs = [pkg.make_desc(packed[r], W, H, m, query_method=args.method, d_tile_list=dl[r],
                                n_tiles=slots) for r in range(world)]
-        # two passes over the ranks, the second reported (the first pass's rank 0
-        # ran right after a different launch shape)
-        for _ in range(2):
-            per = [timed(lambda d=d: pkg.render(d), warm=10) for d in descs]
-        frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-        tu = timed(lambda: pkg.unscatter_tiles(packed, dl, world, slots, frame, W, H))
-        torch.cuda.synchronize()
-        ok = torch.equal(frame, full)
-        print(f"  {mode:4s} N={world}: per-rank ms {' '.join(f'{x:.3f}' for x in per)}  max {max(per):.3f}"
-              f"  unscatter {tu:.3f}  -> est. speedup {t1 / (max(per) + tu):.2f}x"
-              f"  frame {'identical' if ok else 'DIFFERS'}")
+        for spec in envs:
+            knobs(spec)
+            packed.zero_()
+            # two passes over the ranks, the second reported (the first pass's rank 0
+            # ran right after a different launch shape)
+            for _ in range(2):
+                per = [timed(lambda d=d: pkg.render(d), warm=10) for d in descs]
+            kern = pkg.last_kernel()
+            frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            tu = timed(lambda: pkg.unscatter_tiles(packed, dl, world, slots, frame, W, H))
+            torch.cuda.synchronize()
+            ok = torch.equal(frame, full)
+            host = (f"  + host {args.host_ms:.3f} -> {t1 / (max(per) + tu + args.host_ms):.2f}x"
+                    if args.host_ms > 0 else "")
+            print(f"  {mode:4s} N={world} [{spec or 'defaults'}] {kern}: per-rank ms "
+                  f"{' '.join(f'{x:.3f}' for x in per)}  max {max(per):.3f}"
+                  f"  unscatter {tu:.3f}  -> est. speedup {t1 / (max(per) + tu):.2f}x{host}"
+                  f"  frame {'identical' if ok else 'DIFFERS'}", flush=True)
+    knobs(args.env)
     t2 = timed(lambda: pkg.render(dfull), warm=30)
     print(f"steady full frame again: {t2:.3f} ms (speedups above use {t1:.3f})")
 

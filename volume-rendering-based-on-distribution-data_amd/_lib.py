@@ -98,7 +98,8 @@ EXPORTS = [
     "vr_load_flex_files", "vr_debug_wave_clock",
     "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_render_gmm",
     "vr_gmm_count_footprint", "vr_bake_stats", "vr_release_stats", "vr_stats_info",
-    "vr_set_tuning", "vr_clear_tuning", "vr_stream_read",
+    "vr_set_tuning", "vr_clear_tuning", "vr_stream_read", "vr_set_layout_budget",
+    "vr_layout_info",
 ]
 
 _lib = None
@@ -215,6 +216,10 @@ def load() -> ctypes.CDLL:
     L.vr_release_stats.restype = i32
     L.vr_stats_info.argtypes = [vp] * 4
     L.vr_stats_info.restype = i32
+    L.vr_set_layout_budget.argtypes = [ctypes.c_uint64]
+    L.vr_set_layout_budget.restype = i32
+    L.vr_layout_info.argtypes = [vp] * 4
+    L.vr_layout_info.restype = i32
     L.vr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     L.vr_set_tuning.restype = i32
     L.vr_clear_tuning.argtypes = []

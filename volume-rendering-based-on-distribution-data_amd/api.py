@@ -255,6 +255,25 @@ def stats_info():
     return (a.value, na.value), (c.value, nc.value)
 
 
+def set_layout_budget(nbytes=None) -> None:
+    """Cap the HBM the library spends on layout copies (micro-brick and
+    axis-rows copies of the records, include/vr.h): None = no cap beyond the
+    free-memory guard, 0 = never make one."""
+    check(_lib.load().vr_set_layout_budget(0xFFFFFFFFFFFFFFFF if nbytes is None else int(nbytes)))
+
+
+def layout_info() -> dict:
+    """Layout copies: bytes resident, copies made since load, and the time (ms)
+    and size of the last one made -- the extra cost of the first frame of a view
+    that needs a copy."""
+    b, n = ctypes.c_uint64(), ctypes.c_int()
+    ms, lb = ctypes.c_float(), ctypes.c_uint64()
+    check(_lib.load().vr_layout_info(ctypes.byref(b), ctypes.byref(n), ctypes.byref(ms),
+                                     ctypes.byref(lb)))
+    return {"resident_bytes": b.value, "builds": n.value, "last_build_ms": round(ms.value, 3),
+            "last_build_bytes": lb.value}
+
+
 def dataProcessing() -> None:
     """dataProcessing, K:1735-1796: flexible-block pre-pass with 6-voxel blocks."""
     _lib.load().dataProcessing()
@@ -409,8 +428,9 @@ def stream_read(reps: int = 5):
 
 
 def debug_wave_clock(d_buf) -> None:
-    """Tooling: per-wave {start, end, __smid} clocks of the per-ray pipelined
-    march into a device uint64 buffer of 12 * n_slots values (None = off)."""
+    """Tooling: per-wave {start, end, __smid} clocks of the pipelined, quad and
+    ray-segmented marches into a device uint64 buffer of 48 * n_slots values
+    (include/vr.h: up to 16 waves of 3 words per launch slot; None = off)."""
     check(_lib.load().vr_debug_wave_clock(None if d_buf is None else _ptr(d_buf)))
 
 
@@ -424,19 +444,26 @@ def init_gmm(wm, sigma, dims=None, z_base: int = 0, adopt: bool = False) -> None
     in place with adopt=True).  dims: the whole volume's (X, Y, Z) when only the
     slices [z_base, z_base + nzs) are given (default: wm's own shape)."""
     L = _lib.load()
+    on_device = hasattr(wm, "data_ptr") and getattr(wm, "is_cuda", False)
+    if not on_device:  # lists and other array-likes, as np.asarray takes them
+        wm = np.asarray(wm, dtype=np.float32)
+        sigma = np.asarray(sigma, dtype=np.float32)
+    if len(wm.shape) != 5 or int(wm.shape[4]) != 2:
+        raise ValueError(f"wm must have shape (nzs, ny, nx, K, 2), got {tuple(wm.shape)}")
     nzs, ny, nx, K = (int(v) for v in wm.shape[:4])
     if dims is None:
         dims = (nx, ny, nzs)
-    if len(wm.shape) != 5 or int(wm.shape[4]) != 2:
-        raise ValueError(f"wm must have shape (nzs, ny, nx, K, 2), got {tuple(wm.shape)}")
     if tuple(int(v) for v in sigma.shape) != (nzs, ny, nx, K):
         raise ValueError(f"sigma must have shape wm.shape[:4] = {(nzs, ny, nx, K)}, "
                          f"got {tuple(sigma.shape)}")
-    if hasattr(wm, "data_ptr") and getattr(wm, "is_cuda", False):
+    if on_device:
         import torch
         for name, t in (("wm", wm), ("sigma", sigma)):
             if not getattr(t, "is_cuda", False):
                 raise ValueError(f"{name} must be a CUDA tensor like wm")
+            if t.device != wm.device:
+                raise ValueError(f"{name} is on {t.device}, wm on {wm.device}: both must be on "
+                                 "the library's device")
             if t.dtype != torch.float32:
                 raise ValueError(f"{name} must be float32, got {t.dtype}")
             if not t.is_contiguous():
@@ -506,6 +533,7 @@ __all__ = [
     "volume_layout",
     "set_stream", "set_tuning", "clear_tuning", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "stream_read", "version",
     "init_gmm", "synthesize_gmm", "gmm_info", "free_gmm", "gmm_slab", "render_gmm",
-    "gmm_count_footprint", "bake_stats", "release_stats", "stats_info",
+    "gmm_count_footprint", "bake_stats", "release_stats", "stats_info", "set_layout_budget",
+    "layout_info",
     "VRError", "PAD",
 ]

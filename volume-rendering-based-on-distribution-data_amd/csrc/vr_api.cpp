@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -76,11 +77,26 @@ struct State {
     // of oblique views (ensure_brick, brick_index); nullptr = not made
     float *brick = nullptr;
     uint64_t bsy = 0, bsz = 0;
-    // axis-rows copy of an owned B <= 8 volume for views along y or z
-    // (ensure_axis_copy, axis_copy_strides); nullptr = not made
-    float *acopy = nullptr;
-    int acopy_axis = 0;
-    uint64_t asx = 0, asy = 0, asz = 0;
+    // axis-rows copies of an owned B <= 8 volume for views along y ([0]) and z
+    // ([1]) (ensure_axis_copy, axis_copy_strides); nullptr = not made
+    struct AxisCopy {
+        float *buf = nullptr;
+        uint64_t sx = 0, sy = 0, sz = 0, bytes = 0;
+    } acopy[2];
+    uint64_t brick_bytes = 0;
+    // axis copies of a baked plane for baked frames of views along y ([0]) or
+    // z ([1]) (ensure_plane_copy, k_plane_axis): which plane, its pitches
+    struct PlaneCopy {
+        float *buf = nullptr;
+        int plane = -1;
+        uint64_t sy = 0, sz = 0, bytes = 0;
+    } pcopy[2];
+    // layout copies (micro-bricks, axis rows): byte budget (vr_set_layout_budget)
+    // and the cost of the last one made (vr_layout_info)
+    uint64_t layout_budget = UINT64_MAX;
+    float layout_last_ms = 0.0f;
+    uint64_t layout_last_bytes = 0;
+    int layout_builds = 0;
     // bumped whenever a resident volume / codec / flexible-block set is
     // released, so an order learned on old data is not reused (the order is a
     // scheduling hint only: any order renders the same image)
@@ -117,7 +133,10 @@ int hip_fail(hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_fail(e_, #call);   \
     } while (0)
 
+void release_plane_copies();
+
 void release_stats() {
+    release_plane_copies();  // copies of the planes go with them
     if (g.stats) (void)hipFree(g.stats);
     g.stats = nullptr;
     g.stats_plane = 0;
@@ -133,13 +152,45 @@ void release_brick() {
     if (g.brick) (void)hipFree(g.brick);
     g.brick = nullptr;
     g.bsy = g.bsz = 0;
+    g.brick_bytes = 0;
+}
+
+void release_axis_copy(int i) {
+    if (g.acopy[i].buf) (void)hipFree(g.acopy[i].buf);
+    g.acopy[i] = State::AxisCopy();
 }
 
 void release_axis_copy() {
-    if (g.acopy) (void)hipFree(g.acopy);
-    g.acopy = nullptr;
-    g.acopy_axis = 0;
-    g.asx = g.asy = g.asz = 0;
+    release_axis_copy(0);
+    release_axis_copy(1);
+}
+
+void release_plane_copy(int i) {
+    if (g.pcopy[i].buf) (void)hipFree(g.pcopy[i].buf);
+    g.pcopy[i] = State::PlaneCopy();
+}
+
+void release_plane_copies() {
+    release_plane_copy(0);
+    release_plane_copy(1);
+}
+
+uint64_t layout_resident() {
+    return g.brick_bytes + g.acopy[0].bytes + g.acopy[1].bytes + g.pcopy[0].bytes + g.pcopy[1].bytes;
+}
+
+// Room for a layout copy of `bytes`: within the budget (vr_set_layout_budget)
+// next to the copies already resident (less `freed`, a copy the caller would
+// drop first), and HBM keeps max(4 GiB, 5 %) free after it for the caller.
+bool layout_room(uint64_t bytes, uint64_t freed = 0) {
+    const uint64_t have = layout_resident() - freed;
+    if (g.layout_budget < have || g.layout_budget - have < bytes) return false;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return (uint64_t)free_b + freed >= bytes + std::max<uint64_t>(4ull << 30, total_b / 20);
 }
 
 void release_volume() {
@@ -651,6 +702,27 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         const int v = std::atoi(e);
         if (v == 2 || v == 4 || v == -2 || v == -4) P.seg_lanes = v;
     }
+    // A rank's list at 8 GPUs (<= 400 K rays, 2-lane windows) is bound by the step
+    // chains of its longest tiles: its first 64 slots -- the 8 longest tiles of
+    // every XCD sublist -- take 4 lanes per ray in the same launch
+    // (k_march_seg_head).  Cost-dealt 1024^3 x 8 lists, max over 8 ranks: C0
+    // 0.216 -> 0.202 ms (32 / 96 / 128 slots: 0.204 / 0.204 / 0.207; 8 lanes:
+    // 0.212), side view 0.254 -> 0.249-0.263; N = 4 lists (~520 K rays) gain
+    // nothing (0.380 both) and keep the plain windows
+    // (profiles/r04/rank_sim_C0_head.log, rank_sim_S_head.log).
+    // VR_HEAD=slots (0 = off), VR_HEAD_SEG=-2/-4/-8, VR_HEAD_TAIL=1 (one-lane
+    // tail, k_march_pipe_head) override.
+    P.head_slots = 0;
+    if (d->d_tile_list && P.path == 7 && P.nb == 8 &&
+        (d->query_method == 1 || d->query_method == 2) &&
+        (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= 400000u)
+        P.head_slots = 64;
+    P.head_lanes = -4;
+    if (const char *e = vr::tuning("VR_HEAD")) P.head_slots = (uint32_t)std::atoi(e) & ~7u;
+    if (const char *e = vr::tuning("VR_HEAD_SEG")) P.head_lanes = std::atoi(e);
+    P.head_tail = 0;
+    if (const char *e = vr::tuning("VR_HEAD_TAIL")) P.head_tail = std::atoi(e);
+    if (!d->d_tile_list) P.head_slots = 0;
     const uint64_t all = (uint64_t)tiles_x(d->width) * tiles_y(d->height);
     if (d->d_tile_list) {
         nslots = d->n_tiles;
@@ -672,7 +744,8 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
 // slower everywhere but 512^3 C1 (within 3 %).  VR_PATH (2 / 7) overrides;
 // P.seg_lanes keeps a VR_SEG setting.
 int baked_path(const vr_render_desc *d, vr::Params &P) {
-    const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
+    // a plane's axis copy (P.plane_axis) makes a side / top view row-aligned
+    const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f || P.plane_axis != 0;
     int path = along_rows ? 2 : 7;
     int seg = 4;
     // A rank's tile list (multi-GPU) has few rays, so its longest step chains
@@ -795,13 +868,7 @@ bool ensure_brick() {
     const uint64_t nxp = (uint64_t)g.nx + (g.nx & 1), nyp = (uint64_t)g.ny + (g.ny & 1);
     const uint64_t bsy = 2 * nxp, bsz = nxp * nyp;
     const uint64_t bytes = bsz * (uint64_t)g.nz * 8 * sizeof(float);
-    // the copy must leave max(4 GiB, 5 % of the device) free for the caller
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
-        free_b < bytes + std::max<uint64_t>(4ull << 30, total_b / 20)) {
-        (void)hipGetLastError();
-        return false;
-    }
+    if (!layout_room(bytes)) return false;
     float *buf = nullptr;
     if (hipMalloc(&buf, bytes) != hipSuccess) {
         (void)hipGetLastError();
@@ -813,15 +880,20 @@ bool ensure_brick() {
     P.sy = g.sy; P.sz = g.sz;
     // synchronous, like the statistics bake: a later frame may run on another
     // stream (vr_set_stream) and must never see a partly written copy
+    const auto t0 = std::chrono::steady_clock::now();
     if (vr::launch_brick8(g.vol, P, buf, bsy, bsz, g.stream) != hipSuccess ||
         hipStreamSynchronize(g.stream) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFree(buf);
         return false;
     }
+    g.layout_last_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    g.layout_last_bytes = bytes;
+    g.layout_builds++;
     g.brick = buf;
     g.bsy = bsy;
     g.bsz = bsz;
+    g.brick_bytes = bytes;
     return true;
 }
 
@@ -839,17 +911,17 @@ bool ensure_brick() {
 bool ensure_axis_copy(int axis) {
     if (const char *e = vr::tuning("VR_ZROWS"))
         if (std::atoi(e) == 0) return false;
-    if (g.acopy && g.acopy_axis == axis) return true;
+    const int i = axis - 1, other = 1 - i;
+    if (g.acopy[i].buf) return true;
     if (!g.vol || !g.owned || !(g.nb == 1 || g.nb == 2 || g.nb == 4 || g.nb == 8)) return false;
-    release_axis_copy();
     uint64_t sx = 0, sy = 0, sz = 0;
     vr::axis_copy_strides(axis, (uint64_t)g.nx, (uint64_t)g.ny, (uint64_t)g.nz, sx, sy, sz);
     const uint64_t bytes = (uint64_t)g.nx * g.ny * (uint64_t)g.nz * (uint64_t)g.nb * sizeof(float);
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
-        free_b < bytes + std::max<uint64_t>(4ull << 30, total_b / 20)) {
-        (void)hipGetLastError();
-        return false;
+    // keep the other axis' copy when both fit; drop it only if that makes room
+    // (checked before anything is released)
+    if (!layout_room(bytes)) {
+        if (!g.acopy[other].buf || !layout_room(bytes, g.acopy[other].bytes)) return false;
+        release_axis_copy(other);
     }
     float *buf = nullptr;
     if (hipMalloc(&buf, bytes) != hipSuccess) {
@@ -860,17 +932,68 @@ bool ensure_axis_copy(int axis) {
     std::memset(&P, 0, sizeof P);
     P.nx = g.nx; P.ny = g.ny; P.nz = g.nz; P.nb = g.nb;
     P.sy = g.sy; P.sz = g.sz;
+    const auto t0 = std::chrono::steady_clock::now();
     if (vr::launch_axis_copy(g.vol, P, buf, sx, sy, sz, g.stream) != hipSuccess ||
         hipStreamSynchronize(g.stream) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFree(buf);
         return false;
     }
-    g.acopy = buf;
-    g.acopy_axis = axis;
-    g.asx = sx;
-    g.asy = sy;
-    g.asz = sz;
+    g.layout_last_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    g.layout_last_bytes = bytes;
+    g.layout_builds++;
+    g.acopy[i].buf = buf;
+    g.acopy[i].sx = sx;
+    g.acopy[i].sy = sy;
+    g.acopy[i].sz = sz;
+    g.acopy[i].bytes = bytes;
+    return true;
+}
+
+// Baked frames of views whose screen x runs along the volume's y or z (side
+// and top views) read the planes' 16 x 2 x 1 bricks across: a wave's 64 rays
+// sit at consecutive z (y), each on its own lines.  The plane the method
+// filters gets a copy with that axis in the brick rows (k_plane_axis), the
+// axis-rows idea of ensure_axis_copy for planes: one per axis, made on the
+// first such frame within the layout budget, dropped with the planes.
+bool ensure_plane_copy(int plane, int axis) {
+    if (const char *e = vr::tuning("VR_ZROWS"))
+        if (std::atoi(e) == 0) return false;
+    const int i = axis - 1;
+    if (g.pcopy[i].buf && g.pcopy[i].plane == plane) return true;
+    if (!g.stats || plane < 0 || plane > 2) return false;
+    const uint32_t nf = axis == 2 ? g.nz : g.ny, np = axis == 2 ? g.ny : g.nx;
+    const uint64_t ns = axis == 2 ? (uint64_t)g.nx : (uint64_t)g.nz;
+    if (nf >= (1u << 16) || np > 65535 || ns > 65535) return false;
+    uint64_t dsy = 0, dsz = 0;
+    vr::plane_pitches(nf, np, dsy, dsz);
+    if (dsz >= (1ull << 32)) return false;  // gather8 MODE 4/5: 32-bit in-slice offsets
+    const uint64_t bytes = (dsz * ns + 4) * sizeof(float);
+    const uint64_t freed = g.pcopy[i].bytes;  // another plane's copy of this axis
+    if (!layout_room(bytes, freed)) return false;
+    release_plane_copy(i);
+    float *buf = nullptr;
+    if (hipMalloc(&buf, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    if (hipMemsetAsync(buf, 0, bytes, g.stream) != hipSuccess ||
+        vr::launch_plane_axis(g.stats + (uint64_t)plane * g.stats_plane, g.stats_sy, g.stats_sz,
+                              buf, dsy, dsz, g.nx, g.ny, g.nz, axis, g.stream) != hipSuccess ||
+        hipStreamSynchronize(g.stream) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(buf);
+        return false;
+    }
+    g.layout_last_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    g.layout_last_bytes = bytes;
+    g.layout_builds++;
+    g.pcopy[i].buf = buf;
+    g.pcopy[i].plane = plane;
+    g.pcopy[i].sy = dsy;
+    g.pcopy[i].sz = dsz;
+    g.pcopy[i].bytes = bytes;
     return true;
 }
 
@@ -1391,6 +1514,27 @@ int vr_synthesize(vr_extent dims, int nbins, uint64_t seed) {
     return VR_OK;
 }
 
+int vr_set_layout_budget(uint64_t bytes) {
+    g.layout_budget = bytes;
+    // copies already resident beyond a lowered budget are dropped (the next
+    // frame that wants one makes it again if it fits)
+    if (layout_resident() > bytes) {
+        release_brick();
+        release_axis_copy();
+        release_plane_copies();
+    }
+    return VR_OK;
+}
+
+int vr_layout_info(uint64_t *resident_bytes, int *builds, float *last_build_ms,
+                   uint64_t *last_build_bytes) {
+    if (resident_bytes) *resident_bytes = layout_resident();
+    if (builds) *builds = g.layout_builds;
+    if (last_build_ms) *last_build_ms = g.layout_last_ms;
+    if (last_build_bytes) *last_build_bytes = g.layout_last_bytes;
+    return VR_OK;
+}
+
 int vr_volume_layout(size_t *row_pitch, size_t *slice_pitch) {
     if (!g.vol) return fail(VR_ERR_STATE, "no volume resident");
     if (row_pitch) *row_pitch = (size_t)g.sy;
@@ -1432,6 +1576,10 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
         if (P.CW == 0 || P.CH == 0) return VR_OK;
         P.tile_cost = nullptr;
     }
+    // VR_DRY (tooling: tools/host_cost.py): the host work of a frame without its
+    // launch, to time what a frame costs the issuing thread
+    if (const char *e = vr::tuning("VR_DRY"))
+        if (std::atoi(e) != 0) return VR_OK;
     hipError_t e;
     const int qm = desc->query_method;
     const float *baked = (qm >= 1 && qm <= 3 && g.stats)   ? g.stats + (uint64_t)(qm - 1) * g.stats_plane
@@ -1450,6 +1598,20 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
         P.nb = 1;
         P.sy = qm <= 3 ? g.stats_sy : g.cstats_sy;
         P.sz = qm <= 3 ? g.stats_sz : g.cstats_sz;
+        // side / top views of the raw planes: the method's plane with the view's
+        // axis in the brick rows (ensure_plane_copy), marched as row-aligned
+        P.plane_axis = 0;
+        if (qm <= 3 && std::fabs(desc->inv_view[0]) < 0.95f) {
+            const int ax = std::fabs(desc->inv_view[8]) >= 0.95f ? 2
+                         : std::fabs(desc->inv_view[4]) >= 0.95f ? 1 : 0;
+            if (ax && ensure_plane_copy(qm - 1, ax)) {
+                const State::PlaneCopy &c = g.pcopy[ax - 1];
+                baked = c.buf;
+                P.sy = c.sy;
+                P.sz = c.sz;
+                P.plane_axis = ax;
+            }
+        }
         P.path = baked_path(desc, P);
         const bool narrow = plane_narrow(P.sy, P.sz, (uint64_t)P.nz);
         e = vr::launch_march(1, narrow ? 0 : -1, baked, P, nslots, false, g.stream);
@@ -1474,10 +1636,11 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
             P.path = 0;
         }
         if (P.axis_view) {
-            P.avol = g.acopy;
-            P.asx = g.asx;
-            P.asy = g.asy;
-            P.asz = g.asz;
+            const State::AxisCopy &c = g.acopy[P.axis_view - 1];
+            P.avol = c.buf;
+            P.asx = c.sx;
+            P.asy = c.sy;
+            P.asz = c.sz;
         } else if (g.nb == 8 && ((P.path == 0 && qm >= 1 && qm <= 3) || m7_quad) &&
                    ensure_brick()) {
             P.bvol = g.brick;
@@ -1834,10 +1997,14 @@ void render_kernel(vr_dim3 gridSize, vr_dim3 blockSize, uint32_t *d_output, uint
     // d_render covers x = blockIdx.x * blockDim.x + threadIdx.x < imageW (and
     // the same in y, K:282-286): a grid smaller than the image leaves the
     // pixels beyond gridSize x blockSize untouched, a larger one is cut at the
-    // image.  An empty or over-sized launch fails like the reference's launch
-    // would (cudaErrorInvalidConfiguration, reported by getLastCudaError, C:214).
+    // image.  A launch the reference's CUDA launch would refuse fails the same
+    // way (cudaErrorInvalidConfiguration, reported by getLastCudaError, C:214):
+    // an empty grid or block, more than 1024 threads per block, a block
+    // dimension beyond (1024, 1024, 64) or a grid beyond (2^31 - 1, 65535, 65535).
     const uint64_t threads = (uint64_t)blockSize.x * blockSize.y * blockSize.z;
-    if (gridSize.x == 0 || gridSize.y == 0 || gridSize.z == 0 || threads == 0 || threads > 1024) {
+    if (gridSize.x == 0 || gridSize.y == 0 || gridSize.z == 0 || threads == 0 || threads > 1024 ||
+        blockSize.x > 1024 || blockSize.y > 1024 || blockSize.z > 64 ||
+        gridSize.x > 0x7FFFFFFFu || gridSize.y > 65535 || gridSize.z > 65535) {
         fail(VR_ERR_ARG, "render_kernel: invalid launch configuration grid (%u,%u,%u) block (%u,%u,%u)",
              gridSize.x, gridSize.y, gridSize.z, blockSize.x, blockSize.y, blockSize.z);
         return;

@@ -93,6 +93,13 @@ struct Params {
     uint32_t *n_rays_out;
     int wq_map;                  // k_march_wq pixel map: 0 a 64-pixel row per wave, 1 16x4 blocks
     int quad2;                   // quad march with two lanes per ray (k_march_quad2)
+    // ray-segmented march of a tile list: the first head_slots slots (a multiple
+    // of 8: the longest tiles of every XCD sublist) take head_lanes lanes per ray
+    // in the same launch (k_march_seg_head), the rest seg_lanes; 0 = off
+    uint32_t head_slots;
+    int head_lanes;
+    int head_tail;               // the rest of such a list: 0 seg_lanes windows, 1 one lane per ray (k_march_pipe_head)
+    int plane_axis;              // baked frame on a plane's axis copy: 1 y rows, 2 z rows (gather8 MODE 3 + axis)
 };
 
 // Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one

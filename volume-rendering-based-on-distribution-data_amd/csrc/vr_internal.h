@@ -92,6 +92,11 @@ hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t
 // record strides of axis_copy_strides
 hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint64_t asx,
                             uint64_t asy, uint64_t asz, hipStream_t s);
+// axis copy of one baked plane (views along y / z, vr_stats.hip k_plane_axis):
+// axis 1 y rows, 2 z rows, into plane_pitches(fast, pair) = (dsy, dsz) bricks
+hipError_t launch_plane_axis(const float *src, uint64_t ssy, uint64_t ssz, float *out,
+                             uint64_t dsy, uint64_t dsz, int nx, int ny, int nz, int axis,
+                             hipStream_t s);
 // streaming read of bytes (a multiple of 16, 16-B aligned) by nblocks workgroups
 // of 256 threads; one xor word per workgroup into out (bench read ceiling)
 hipError_t launch_stream_read(const void *buf, uint64_t bytes, uint32_t *out, uint32_t nblocks,

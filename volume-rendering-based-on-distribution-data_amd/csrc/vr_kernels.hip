@@ -2411,7 +2411,16 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             switch (method) {
             case 0:
                 if constexpr (B == 1) {
-                    hipLaunchKernelGGL((k_march_pipe<1, 0>), grid, block, occupancy_lds(P), s, vol, P);
+                    // a baked plane's y- / z-rows copy (side and top views, gather8 MODE 4 / 5)
+                    if (P.plane_axis == 1) {
+                        note_kernel("k_march_pipe_plane_yrows", B, method);
+                        hipLaunchKernelGGL((k_march_pipe<1, 0, 4>), grid, block, occupancy_lds(P), s, vol, P);
+                    } else if (P.plane_axis == 2) {
+                        note_kernel("k_march_pipe_plane_zrows", B, method);
+                        hipLaunchKernelGGL((k_march_pipe<1, 0, 5>), grid, block, occupancy_lds(P), s, vol, P);
+                    } else {
+                        hipLaunchKernelGGL((k_march_pipe<1, 0>), grid, block, occupancy_lds(P), s, vol, P);
+                    }
                     break;
                 }
                 return hipErrorInvalidValue;

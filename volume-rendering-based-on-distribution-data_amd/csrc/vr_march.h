@@ -156,7 +156,8 @@ __device__ __forceinline__ vr_f2a4 load_pair64(const float *__restrict__ vol, ui
     return *reinterpret_cast<const vr_f2a4 *>(vol + i);
 }
 // MODE 0: records in x rows (P.sy / P.sz record pitches).  MODE 3: an axis-rows
-// copy (P.sx / P.sy / P.sz strides; axis_copy_strides).  MODE 1 / 2: a baked
+// copy (P.sx / P.sy / P.sz strides; axis_copy_strides).  MODE 4 / 5: a baked
+// plane's y- / z-rows copy (P.sy / P.sz its pitches).  MODE 1 / 2: a baked
 // statistics plane (B = 1) in 16 x 2 x 1 bricks (plane_index; P.sy / P.sz the
 // plane pitches): each (y, z) row's x-pair is one 8-byte load; MODE 1 forms the
 // index with 24-bit multiplies in 32 bits (pitches < 2^24, plane < 2^32 floats:
@@ -192,6 +193,41 @@ __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Par
         rec[5][0] = ox ? c.y : c.x;
         rec[6][0] = d.x;
         rec[7][0] = ox ? d.y : d.x;
+        return;
+    }
+    if constexpr (MODE == 4 || MODE == 5) {
+        // a baked plane's axis copy (vr_stats.hip k_plane_axis): the same 16 x 2 x 1
+        // bricks with the axis the view's screen x runs along in the brick rows --
+        // MODE 4: y rows (y fast, x pairs, z slices), MODE 5: z rows (z fast, y
+        // pairs, x slices).  The four pair loads carry y- or z-pairs and are
+        // assigned to the same 8 corners, so the blend is unchanged.
+        static_assert(B == 1, "baked planes hold one float per voxel");
+        const uint32_t sy = (uint32_t)P.sy;  // a slice of the copy is < 2^32 floats
+        if constexpr (MODE == 5) {
+            const uint32_t bz = plane_bx((uint32_t)f.z0);
+            const bool oz = f.z1 != f.z0;
+            const uint32_t y0 = ((uint32_t)f.y0 >> 1) * sy + ((uint32_t)f.y0 & 1u) * 16u + bz;
+            const uint32_t y1 = ((uint32_t)f.y1 >> 1) * sy + ((uint32_t)f.y1 & 1u) * 16u + bz;
+            const uint64_t x0 = (uint64_t)f.x0 * P.sz, x1 = (uint64_t)f.x1 * P.sz;
+            const vr_f2a4 a = load_pair64(vol, x0 + y0), b = load_pair64(vol, x1 + y0);
+            const vr_f2a4 c = load_pair64(vol, x0 + y1), d = load_pair64(vol, x1 + y1);
+            rec[0][0] = a.x; rec[4][0] = oz ? a.y : a.x;
+            rec[1][0] = b.x; rec[5][0] = oz ? b.y : b.x;
+            rec[2][0] = c.x; rec[6][0] = oz ? c.y : c.x;
+            rec[3][0] = d.x; rec[7][0] = oz ? d.y : d.x;
+        } else {
+            const uint32_t by = plane_bx((uint32_t)f.y0);
+            const bool oy = f.y1 != f.y0;
+            const uint32_t x0 = ((uint32_t)f.x0 >> 1) * sy + ((uint32_t)f.x0 & 1u) * 16u + by;
+            const uint32_t x1 = ((uint32_t)f.x1 >> 1) * sy + ((uint32_t)f.x1 & 1u) * 16u + by;
+            const uint64_t z0 = (uint64_t)f.z0 * P.sz, z1 = (uint64_t)f.z1 * P.sz;
+            const vr_f2a4 a = load_pair64(vol, z0 + x0), b = load_pair64(vol, z0 + x1);
+            const vr_f2a4 c = load_pair64(vol, z1 + x0), d = load_pair64(vol, z1 + x1);
+            rec[0][0] = a.x; rec[2][0] = oy ? a.y : a.x;
+            rec[1][0] = b.x; rec[3][0] = oy ? b.y : b.x;
+            rec[4][0] = c.x; rec[6][0] = oy ? c.y : c.x;
+            rec[5][0] = d.x; rec[7][0] = oy ? d.y : d.x;
+        }
         return;
     }
     if constexpr (MODE == 3) {  // axis-rows copy: all three axes strided

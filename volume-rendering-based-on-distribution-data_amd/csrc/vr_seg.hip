@@ -136,20 +136,42 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
         Foot fa, fb;
         float ra[8][B], rb[8][B];
         bool va = geom((int)k, t), vb = false;
+#ifndef VR_SEG_COND
+        fa = footprint(P, px, py, pz);
+        gather8<B, GM>(vol, P, fa, ra);
+#else
         if (va) {
             fa = footprint(P, px, py, pz);
             gather8<B, GM>(vol, P, fa, ra);
         }
+#endif
         // one window: gather the next into (fn, rn, vn) while (fc, rc, vc) decodes
         auto window = [&](const Foot &fc, const float (&rc)[8][B], bool vc, Foot &fn,
                           float (&rn)[8][B], bool &vn) {
             float tn = t, nx = px, ny = py, nz = pz;
             advance(tn, nx, ny, nz);
             vn = alive && geom(base + S + (int)k, tn);
+#ifndef VR_SEG_COND
+            // Gathered unconditionally: without a divergent branch around the
+            // loads the march needs no register copies at the join (B = 8,
+            // mean: 208 -> 170 VGPRs, fewer instructions per window); a lane with no next
+            // step re-reads its current footprint (cache hits), not new lines.
+            // 1024^3 x 8 C0 cost-dealt lists, max over ranks: N = 4 0.405 ->
+            // 0.380 ms, N = 8 0.212 -> 0.213, the longest tile alone 0.154 ->
+            // 0.121 (profiles/r04/rank_sim_C0_uncond.log; VR_SEG_COND builds the
+            // branch)
+            fn = footprint(P, vn ? nx : px, vn ? ny : py, vn ? nz : pz);
+            gather8<B, GM>(vol, P, fn, rn);
+#else
             if (vn) {
                 fn = footprint(P, nx, ny, nz);
                 gather8<B, GM>(vol, P, fn, rn);
             }
+#endif
+            // (decoding unconditionally as well frees registers -- 170 -> 143
+            // VGPRs, 3 waves per SIMD -- but lets the scheduler sink the next
+            // window's loads into the decode: N = 8 lists 0.213 -> 0.254 ms,
+            // profiles/r04/rank_sim_C0_uncond_decode.log)
             float smp = 0.0f;
             if (vc && alive) smp = decode8<B, M>(P, rc, fc);
             const uint64_t vm = __ballot(vc);
@@ -189,6 +211,107 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVE
     }
 }
 
+// A tile list whose longest tiles set the launch time (a rank's list at 4-8
+// GPUs): those tiles take SH lanes per ray, the rest ST, in ONE launch -- two
+// kernels' worth of workgroups, the head's dispatched first.  Both bodies
+// have about the same register need (one window of 8 corner records per lane),
+// so sharing a kernel costs no occupancy.  Slots [0, head_slots) are the
+// first entries of every XCD sublist (entry s runs on XCD s % 8 and each
+// sublist is longest first, tiles.py / frame_order); head_slots is a multiple
+// of 8, so the tail's workgroup b keeps b % 8 = its slot % 8.
+template <int B, int M, int SH, int ST, int GM = kGatherMode<M>>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVES, 8))) void k_march_seg_head(const float *__restrict__ vol, Params P) {
+    const uint32_t hw = P.head_slots * (uint32_t)SH;  // head workgroups
+    uint32_t b = blockIdx.x, slot, part;
+    unsigned long long t0 = 0;
+    if (P.wave_clock) t0 = wall_clock64();
+    if (b < hw) {
+        slot = (b & 7u) + 8u * (b / (8u * SH));
+        part = (b >> 3) % SH;
+        march_seg_part<B, M, SH, true, GM>(vol, P, slot, part);
+    } else {
+        b -= hw;
+        slot = P.head_slots + (b & 7u) + 8u * (b / (8u * ST));
+        part = (b >> 3) % ST;
+        march_seg_part<B, M, ST, true, GM>(vol, P, slot, part);
+    }
+    if (P.wave_clock && (threadIdx.x & 63u) == 0 && slot < P.n_tiles && part < 4) {  // tooling
+        unsigned long long *w = P.wave_clock + ((uint64_t)slot * 16u + part * 4u + threadIdx.x / 64u) * 3u;
+        w[0] = t0;
+        w[1] = wall_clock64();
+        w[2] = __smid();
+    }
+}
+
+// The same split with the one-lane pipelined march (march_pipe_tile, one
+// 256-ray tile per workgroup) for the tail: the tail's rays are short enough
+// that one lane per ray is the cheaper issue, the head's long chains take SH
+// lanes.  Tail workgroup b' = b - head workgroups renders slot head_slots + b'
+// (b' % 8 = b % 8: the tile list's XCD interleave holds).
+template <int B, int M, int SH, int GM = kGatherMode<M>>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVES, 8))) void k_march_pipe_head(const float *__restrict__ vol, Params P) {
+    const uint32_t hw = P.head_slots * (uint32_t)SH;
+    const uint32_t b = blockIdx.x;
+    if (b < hw) {
+        march_seg_part<B, M, SH, true, GM>(vol, P, (b & 7u) + 8u * (b / (8u * SH)), (b >> 3) % SH);
+        return;
+    }
+    const uint32_t slot = P.head_slots + (b - hw);
+    if (slot >= P.n_tiles) return;
+    const uint32_t tile = P.tile_list[slot];
+    if (tile == kPad) return;
+    march_pipe_tile<B, M, GM>(vol, P, slot, tile, threadIdx.x);
+}
+
+template <int B, int SH>
+static hipError_t pipe_head_launch(int method, const float *vol, const Params &P, uint32_t nslots,
+                                   hipStream_t s) {
+    const dim3 grid(P.head_slots * (uint32_t)SH + (nslots - P.head_slots)), block(256);
+    if (P.avol) {
+        Params Q = P;
+        Q.sx = P.asx;
+        Q.sy = P.asy;
+        Q.sz = P.asz;
+        switch (method) {
+        case 1: hipLaunchKernelGGL((k_march_pipe_head<B, 1, SH, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+        case 2: hipLaunchKernelGGL((k_march_pipe_head<B, 2, SH, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (method) {
+        case 1: hipLaunchKernelGGL((k_march_pipe_head<B, 1, SH>), grid, block, occupancy_lds(P), s, vol, P); break;
+        case 2: hipLaunchKernelGGL((k_march_pipe_head<B, 2, SH>), grid, block, occupancy_lds(P), s, vol, P); break;
+        default: return hipErrorInvalidValue;
+        }
+    }
+    return hipGetLastError();
+}
+
+template <int B, int SH>
+static hipError_t seg_head_launch(int method, const float *vol, const Params &P, uint32_t nslots,
+                                  hipStream_t s) {
+    const uint32_t tail = nslots - P.head_slots;
+    const dim3 grid(P.head_slots * (uint32_t)SH + ((tail + 7u) / 8u) * 8u * 2u), block(256);
+    if (P.avol) {
+        Params Q = P;
+        Q.sx = P.asx;
+        Q.sy = P.asy;
+        Q.sz = P.asz;
+        switch (method) {
+        case 1: hipLaunchKernelGGL((k_march_seg_head<B, 1, SH, 2, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+        case 2: hipLaunchKernelGGL((k_march_seg_head<B, 2, SH, 2, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (method) {
+        case 1: hipLaunchKernelGGL((k_march_seg_head<B, 1, SH, 2>), grid, block, occupancy_lds(P), s, vol, P); break;
+        case 2: hipLaunchKernelGGL((k_march_seg_head<B, 2, SH, 2>), grid, block, occupancy_lds(P), s, vol, P); break;
+        default: return hipErrorInvalidValue;
+        }
+    }
+    return hipGetLastError();
+}
+
 template <int B, int S, bool PIPE>
 static hipError_t seg_launch(int method, const float *vol, const Params &P, uint32_t nslots,
                              hipStream_t s) {
@@ -196,7 +319,13 @@ static hipError_t seg_launch(int method, const float *vol, const Params &P, uint
     switch (method) {
     case 0:  // baked statistics, one float per voxel (vr_stats.hip), 32-bit offsets
         if constexpr (B == 1) {
-            hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P);
+            // a plane's y- / z-rows copy (gather8 MODE 4 / 5)
+            if (P.plane_axis == 1)
+                hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE, 4>), grid, block, occupancy_lds(P), s, vol, P);
+            else if (P.plane_axis == 2)
+                hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE, 5>), grid, block, occupancy_lds(P), s, vol, P);
+            else
+                hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P);
             break;
         }
         return hipErrorInvalidValue;
@@ -257,6 +386,24 @@ bool launch_march_seg(int nb, int method, int S, const float *vol, const Params 
                       uint32_t nslots, hipStream_t s, hipError_t &err) {
     if (method < (nb == 1 ? -1 : 1) || method > 3) return false;
     bool ok = false;
+    if (nb == 8 && S == -2 && (method == 1 || method == 2) && P.head_slots > 0 &&
+        P.head_slots < nslots && (P.head_slots & 7u) == 0 &&
+        (P.head_lanes == -2 || P.head_lanes == -4 || P.head_lanes == -8)) {
+        if (P.head_tail == 1)
+            err = P.head_lanes == -2 ? pipe_head_launch<8, 2>(method, vol, P, nslots, s)
+                : P.head_lanes == -4 ? pipe_head_launch<8, 4>(method, vol, P, nslots, s)
+                                     : pipe_head_launch<8, 8>(method, vol, P, nslots, s);
+        else
+            err = P.head_lanes == -2 ? seg_head_launch<8, 2>(method, vol, P, nslots, s)
+                : P.head_lanes == -4 ? seg_head_launch<8, 4>(method, vol, P, nslots, s)
+                                     : seg_head_launch<8, 8>(method, vol, P, nslots, s);
+        char kind[48];
+        snprintf(kind, sizeof kind, "k_march_segp%d_head_%s%s", -P.head_lanes,
+                 P.head_tail == 1 ? "pipe" : "segp2",
+                 P.avol ? (P.asy == 1 ? "_yrows" : "_zrows") : "");
+        note_kernel(kind, nb, method);
+        return true;
+    }
     switch (nb) {
     case 1: ok = seg_b<1>(method, S, vol, P, nslots, s, err); break;
     case 2: ok = seg_b<2>(method, S, vol, P, nslots, s, err); break;
@@ -265,9 +412,11 @@ bool launch_march_seg(int nb, int method, int S, const float *vol, const Params 
     default: return false;
     }
     if (ok) {
-        char kind[32];
+        char kind[40];
         snprintf(kind, sizeof kind, S < 0 ? "k_march_segp%d%s" : "k_march_seg%d%s", S < 0 ? -S : S,
-                 (P.avol && method >= 1 && method <= 3) ? (P.asy == 1 ? "_yrows" : "_zrows") : "");
+                 (P.avol && method >= 1 && method <= 3) ? (P.asy == 1 ? "_yrows" : "_zrows")
+                 : (nb == 1 && method == 0 && P.plane_axis) ? (P.plane_axis == 1 ? "_plane_yrows" : "_plane_zrows")
+                 : "");
         note_kernel(kind, nb, method);
     }
     return ok;

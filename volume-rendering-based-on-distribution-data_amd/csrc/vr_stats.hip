@@ -169,6 +169,32 @@ hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint6
     return hipGetLastError();
 }
 
+// Axis copy of one baked plane (views whose screen x runs along the volume's y
+// or z): the plane's 16 x 2 x 1 bricks with that axis in the
+// brick rows -- axis 1: y rows (y fast, x pairs, z slices), axis 2: z rows (z
+// fast, y pairs, x slices); gather8 MODE 4 / 5 reads it.  One thread per
+// voxel, grid over (fast, pair, slow) of the copy so its writes are coalesced.
+__global__ __launch_bounds__(256) void k_plane_axis(const float *__restrict__ src, uint64_t ssy,
+                                                    uint64_t ssz, float *__restrict__ out,
+                                                    uint64_t dsy, uint64_t dsz, uint32_t nfast,
+                                                    int axis) {
+    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
+    if (f >= nfast) return;
+    const uint32_t p = blockIdx.y, s = blockIdx.z;
+    const uint32_t x = axis == 2 ? s : p, y = axis == 2 ? p : f, z = axis == 2 ? f : s;
+    put_plane(out, f, p, s, dsy, dsz, src[plane_index(x, y, z, ssy, ssz)]);
+}
+
+hipError_t launch_plane_axis(const float *src, uint64_t ssy, uint64_t ssz, float *out,
+                             uint64_t dsy, uint64_t dsz, int nx, int ny, int nz, int axis,
+                             hipStream_t s) {
+    const uint32_t nf = axis == 2 ? nz : ny, np = axis == 2 ? ny : nx, ns = axis == 2 ? nx : nz;
+    if (nf == 0 || np == 0 || ns == 0 || np > 65535 || ns > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_plane_axis, dim3((nf + 255) / 256, np, ns), dim3(256), 0, s, src, ssy,
+                       ssz, out, dsy, dsz, nf, axis);
+    return hipGetLastError();
+}
+
 hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t bsy,
                          uint64_t bsz, hipStream_t s) {
     dim3 grid;
