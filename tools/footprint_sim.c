@@ -21,6 +21,9 @@ static float M[12];
 static int PF = 0;
 static int ALIGN = 0; /* 1: per-step scopes count a ray's sample s at iteration s + its depth
                          offset round((tnear - tnear_min of the tile) / 0.01) */
+static int RING = 0;  /* > 1: per-tile ring of the last RING steps' lines (an LDS cache of
+                         recent steps): a tile-step counts only lines not in the previous
+                         RING - 1 steps of the same tile */
 static int LAYOUT = 0; /* 0: x-rows (4 records along x per line), 1: 2x2 (x,y) micro-bricks,
                           2: 2x1x2 (x,z) micro-bricks, 3: 1x2x2 (y,z) micro-bricks */
 
@@ -123,9 +126,11 @@ int main(int argc, char **argv) {
     const size_t nlines = (size_t)N * N * N * 32 / 128;
     uint8_t *bits = calloc(nlines / 8 + 1, 1);
     uint64_t samples = 0, per_tile = 0, per_wave_step = 0, per_tile_step = 0, per_wave = 0;
+    uint64_t per_ring = 0, max_ring = 0, max_tile_step = 0;
+    if (getenv("RING")) RING = atoi(getenv("RING"));
     uint64_t per_block4 = 0;
     const int TX = 120, TY = 68;
-#pragma omp parallel for schedule(dynamic) reduction(+ : samples, per_tile, per_wave_step, per_tile_step, per_wave)
+#pragma omp parallel for schedule(dynamic) reduction(+ : samples, per_tile, per_wave_step, per_tile_step, per_wave, per_ring) reduction(max : max_ring, max_tile_step)
     for (int t = 0; t < (argc >= 5 ? 0 : TX * TY); t++) {
         int tx = t % TX, ty = t / TX;
         uint32_t *buf = malloc(sizeof(uint32_t) * 256 * 500 * 8);
@@ -179,7 +184,33 @@ int main(int argc, char **argv) {
                 if (s >= 0 && lens[i] / 8 > s)
                     for (int c = 0; c < 8; c++) tmp[nt++] = rl[i][s * 8 + c];
             }
-            per_tile_step += uniq(tmp, nt);
+            const uint64_t u = uniq(tmp, nt);
+            per_tile_step += u;
+            if (u > max_tile_step) max_tile_step = u;
+            if (RING > 1) {
+                /* lines of steps k - RING + 1 .. k - 1 of this tile, sorted */
+                size_t np = 0;
+                uint32_t *prev = malloc(sizeof(uint32_t) * 256 * 8 * RING + 4);
+                for (int j = k - RING + 1; j < k; j++)
+                    for (int i = 0; i < 256; i++) {
+                        const int s = j - off[i];
+                        if (j >= 0 && s >= 0 && lens[i] / 8 > s)
+                            for (int c = 0; c < 8; c++) prev[np++] = rl[i][s * 8 + c];
+                    }
+                qsort(prev, np, 4, cmp_u32);
+                /* tmp holds step k's lines sorted (uniq sorted it): count the new ones */
+                uint64_t fresh = 0, ring = 0;
+                for (size_t a = 0; a < nt; a++) {
+                    if (a > 0 && tmp[a] == tmp[a - 1]) continue;
+                    size_t lo = 0, hi = np;
+                    while (lo < hi) { size_t mid = (lo + hi) / 2; if (prev[mid] < tmp[a]) lo = mid + 1; else hi = mid; }
+                    if (lo == np || prev[lo] != tmp[a]) fresh++;
+                }
+                for (size_t a = 0; a < np; a++) ring += (a == 0 || prev[a] != prev[a - 1]);
+                per_ring += fresh;
+                if (ring + fresh > max_ring) max_ring = ring + fresh;
+                free(prev);
+            }
         }
         for (int w = 0; w < 4; w++) {
             size_t nw = 0;
@@ -246,5 +277,9 @@ scope:
     printf("  sum per wave            %12llu  (%.3f GB)\n", (unsigned long long)per_wave, per_wave * 128e-9);
     printf("  sum per tile-step       %12llu  (%.3f GB)\n", (unsigned long long)per_tile_step, per_tile_step * 128e-9);
     printf("  sum per wave-step       %12llu  (%.3f GB)\n", (unsigned long long)per_wave_step, per_wave_step * 128e-9);
+    printf("  max lines per tile-step %12llu\n", (unsigned long long)max_tile_step);
+    if (RING > 1)
+        printf("  sum per tile-step ring%d %12llu  (%.3f GB), max ring lines %llu\n", RING,
+               (unsigned long long)per_ring, per_ring * 128e-9, (unsigned long long)max_ring);
     return 0;
 }

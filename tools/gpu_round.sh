@@ -5,7 +5,8 @@
 # issue -- run one per process (MI355X_MICROARCH.md PMC slot limits) and folded
 # into traffic.json (tools/pmc_traffic.py, keyed by workload and by the sha256
 # of this libvr.so).  Then the steady-state rank simulation.
-# usage: bash tools/gpu_round.sh TAG [workload ...]   (workload = config:camera[:baked])
+# usage: bash tools/gpu_round.sh TAG [workload ...]   (workload = config:camera[:baked[:method]],
+#   e.g. 1024x32:C0::3 for method 3 per-step, 1024x8:S:baked)
 #   PMC=0: bench lines and kernel traces only (profiles/traffic.json already holds
 #   this build's passes); RANKSIM=0: no rank simulation.  Run the PMC passes of one
 #   build in ONE call, or merge their traffic.json files: each call starts from a
@@ -16,8 +17,10 @@ O=gpurun_out/$TAG; mkdir -p $O
 WL=${@:-"1024x8:C0 1024x8:C1 1024x8:S 1024x8:C0:baked 1024x8:C1:baked 512x8:C0 256x4:C0 128x1:C0 gmm1024:C0"}
 guard() { rc=$1; if [ $rc -ne 0 ]; then echo "$2 failed rc=$rc"; tail -20 $3; exit $rc; fi; }
 for W in $WL; do
-  IFS=: read CFG CAM BK <<< "$W"
-  ARGS="--config $CFG --camera $CAM"; KEY="$CFG|$CAM|m1"; N="${CFG}_$CAM"
+  IFS=: read CFG CAM BK MTH <<< "$W"
+  MTH=${MTH:-1}
+  ARGS="--config $CFG --camera $CAM --method $MTH"; KEY="$CFG|$CAM|m$MTH"; N="${CFG}_$CAM"
+  [ "$MTH" != 1 ] && N="${N}_m$MTH"
   if [ "$BK" = baked ]; then ARGS="$ARGS --baked"; KEY="$KEY|baked"; N="${N}_baked"; fi
   timeout -k 10 600 python -u bench.py $ARGS > $O/bench_$N.log 2>&1; guard $? bench-$N $O/bench_$N.log
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o $N -- python bench.py $ARGS --no-cpu-baseline --no-issue-bounds > $O/ktrace_$N.log 2>&1; guard $? ktrace-$N $O/ktrace_$N.log

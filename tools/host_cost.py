@@ -83,7 +83,10 @@ def main():
     works, assembled, ev = [None] * 4, [None] * 4, []
     nframe = [0]
 
-    def step(events=False, gather=True, unscatter=True, ring=4):  # bench.py step(), N > 1, rank 0
+    def step(events=False, gather=True, unscatter=True, ring=4, mode="nccl", on_render=False):
+        # bench.py step(), N > 1, rank 0.  mode: "nccl" the gather on the one-rank
+        # group, "copy" a device copy on the assembly stream instead; on_render: the
+        # unscatter of the previous frame on the render stream after this render
         b = nframe[0] % ring
         nframe[0] += 1
         with torch.cuda.stream(stream):
@@ -100,8 +103,16 @@ def main():
                 e1.record(stream)
                 ev.append((e0, e1))
             works[b] = (dist.gather(packed[b], gather_list=list(recv1[b].unbind(0)), dst=0,
-                                    async_op=True) if gather else None)
-        if unscatter:
+                                    async_op=True) if gather and mode == "nccl" else None)
+            if on_render and unscatter:
+                pkg.unscatter_tiles(recvN, all_lists, N, slots, frame, W, H)
+        if gather and mode == "copy":
+            ev_r = torch.cuda.Event()
+            ev_r.record(stream)
+            with torch.cuda.stream(assemble):
+                assemble.wait_event(ev_r)
+                recv1[b][0].copy_(packed[b])
+        if unscatter and not on_render:
             with torch.cuda.stream(assemble):
                 if works[b] is not None:
                     works[b].wait()
@@ -150,7 +161,8 @@ def main():
     print(f"  host calls alone: vr_render {t_render:.4f} ms (no launch), dist.gather {t_gather:.4f} ms, "
           f"unscatter {t_unsc:.4f} ms", flush=True)
     pkg.set_tuning("VR_DRY", "0")
-    for kw in ({}, {"ring": 2}, {"events": True, "ring": 2}, {"events": True},
+    for kw in ({}, {"mode": "copy"}, {"unscatter": False}, {"gather": False},
+               {"on_render": True}, {"mode": "copy", "unscatter": False},
                {"gather": False, "unscatter": False},
                {"events": True, "gather": False, "unscatter": False}):
         works[:] = [None] * 4

@@ -82,6 +82,39 @@ __device__ __forceinline__ void quad_transpose(float4 (&M)[4], uint32_t g) {
 
 
 
+// Entropy (K:761-769) of a 16 / 32-bin record with few registers: the lane parks
+// its record in its own bin-major LDS column (st[i * 64 + lane]: conflict-free)
+// and runs the per-bin sum as a rolled loop over it, the exact logarithm from
+// the LDS table -- the same operations in the same order as entropy_p, so the
+// same float.  Unrolled over 32 bins the decode held ~430 registers (1 wave per
+// SIMD); rolled, the march keeps several waves per SIMD to hide its loads.
+template <int B>
+__device__ __forceinline__ float entropy_stash(const float (&p)[B], float *st, uint32_t lane,
+                                               float enorm, const LogEnt *tab) {
+#pragma unroll
+    for (int i = 0; i < B; i++) st[i * 64 + lane] = p[i];
+    float ent = 0.0f;
+#pragma unroll 2
+    for (int i = 0; i < B; i++) {
+        const float pr = st[i * 64 + lane];  // written by this lane: program order suffices
+        const double t =
+            pr <= 0 ? 0.0 : div_const((double)logf_canon_p(pr, tab), VR_LN2_D, kLn2R);
+        ent = (float)((double)ent + (double)pr * t);
+    }
+    ent = -ent;
+    return ent / enorm;
+}
+
+// the statistic of a record in the box / direct paths of k_march: wide entropy
+// through the LDS column (st: this wave's, 64 * B floats), everything else as
+// record_stat
+template <int B, int M>
+__device__ __forceinline__ float box_stat(const float (&p)[B], const Params &P, float *st,
+                                          uint32_t lane, const LogEnt *tab) {
+    if constexpr (M == 3 && B >= 16) return entropy_stash<B>(p, st, lane, P.enorm, tab);
+    else return record_stat<B, M>(p, P.enorm);
+}
+
 // Compile-time tuning knobs (tools/build_variants.sh builds sweeps of them).
 #ifndef VR_DIRECT_CG
 #define VR_DIRECT_CG 8      // corners gathered before decoding, direct path
@@ -94,7 +127,8 @@ __device__ __forceinline__ void quad_transpose(float4 (&M)[4], uint32_t g) {
 // corners in flight.
 template <int B, int M, int CGMAX = VR_DIRECT_CG>
 __device__ __forceinline__ float sample_direct_cg(const float *__restrict__ vol, const Params &P,
-                                                  const Foot &f) {
+                                                  const Foot &f, const LogEnt *tab = nullptr,
+                                                  float *st = nullptr) {
     const uint64_t r00 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y0 * P.sy;
     const uint64_t r10 = (uint64_t)f.z0 * P.sz + (uint64_t)f.y1 * P.sy;
     const uint64_t r01 = (uint64_t)f.z1 * P.sz + (uint64_t)f.y0 * P.sy;
@@ -111,7 +145,7 @@ __device__ __forceinline__ float sample_direct_cg(const float *__restrict__ vol,
 #pragma unroll
             for (int j = 0; j < CG; j++) load_rec<B>(vol, vidx[g + j], rec[j]);
 #pragma unroll
-            for (int j = 0; j < CG; j++) s[g + j] = record_stat<B, M>(rec[j], P.enorm);
+            for (int j = 0; j < CG; j++) s[g + j] = box_stat<B, M>(rec[j], P, st, threadIdx.x & 63u, tab);
         }
     } else {
 #pragma unroll
@@ -123,8 +157,9 @@ __device__ __forceinline__ float sample_direct_cg(const float *__restrict__ vol,
 
 template <int B, int M>
 __device__ __forceinline__ float sample_direct(const float *__restrict__ vol, const Params &P,
-                                               const Foot &f) {
-    return sample_direct_cg<B, M, VR_DIRECT_CG>(vol, P, f);
+                                               const Foot &f, const LogEnt *tab = nullptr,
+                                               float *st = nullptr) {
+    return sample_direct_cg<B, M, VR_DIRECT_CG>(vol, P, f, tab, st);
 }
 
 __device__ __forceinline__ void mark_foot(const Params &P, const Foot &f) {
@@ -142,7 +177,8 @@ __device__ __forceinline__ void mark_foot(const Params &P, const Foot &f) {
 template <int B, int M, int NG>
 __device__ __forceinline__ void box_chunk(const float *__restrict__ vbase, const Params &P,
                                           float *box, int dx, int dxy, int V, uint32_t lane,
-                                          int p0, float rdx, float rdxy) {
+                                          int p0, float rdx, float rdxy, const LogEnt *tab,
+                                          float *st) {
     const uint32_t sy = (uint32_t)P.sy;
     float rec[NG][B];
 #pragma unroll
@@ -190,7 +226,7 @@ __device__ __forceinline__ void box_chunk(const float *__restrict__ vbase, const
 #pragma unroll
     for (int g = 0; g < NG; g++) {
         const int p = p0 + g * 64 + (int)lane;
-        if (p < V) box[p] = record_stat<B, M>(rec[g], P.enorm);
+        if (p < V) box[p] = box_stat<B, M>(rec[g], P, st, lane, tab);
     }
 }
 
@@ -206,29 +242,50 @@ __device__ __forceinline__ void box_chunk(const float *__restrict__ vbase, const
 // 192 slots, not 256 (512^3 x 8 at 1080p: boxes of ~130-210 voxels).
 template <int B, int M>
 __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, const Params &P,
-                                           float *box, int dx, int dxy, int V, uint32_t lane) {
+                                           float *box, int dx, int dxy, int V, uint32_t lane,
+                                           const LogEnt *tab, float *st) {
     constexpr int G0 = B >= 32 ? 1 : (B >= 16 ? 2 : 4);
     constexpr int G = G0 < VR_BOX_G ? G0 : VR_BOX_G;  // voxels per lane in flight
-    const float rdx = 1.0f / (float)dx, rdxy = 1.0f / (float)dxy;
+    // hardware reciprocals (1 ulp) instead of two IEEE divisions per wave-step:
+    // (p + 0.5) / d lies at least 0.5 / d from an integer, a relative gap of
+    // >= 2^-12 for p < 2^11, far above the reciprocal's 2^-22 error, so the
+    // truncations below give the same box coordinates
+    const float rdx = __builtin_amdgcn_rcpf((float)dx), rdxy = __builtin_amdgcn_rcpf((float)dxy);
     for (int p0 = 0; p0 < V; p0 += 64 * G) {
         const int left = V - p0;  // wave-uniform
         if (G >= 4 && left > 192)
-            box_chunk<B, M, (G >= 4 ? 4 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
+            box_chunk<B, M, (G >= 4 ? 4 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
         else if (G >= 3 && left > 128)
-            box_chunk<B, M, (G >= 3 ? 3 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
+            box_chunk<B, M, (G >= 3 ? 3 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
         else if (G >= 2 && left > 64)
-            box_chunk<B, M, (G >= 2 ? 2 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
+            box_chunk<B, M, (G >= 2 ? 2 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
         else
-            box_chunk<B, M, 1>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy);
+            box_chunk<B, M, 1>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
     }
 }
 
+#ifndef VR_MARCH_MINW
+#define VR_MARCH_MINW 1   // minimum waves per SIMD the register allocation must allow
+#endif
 template <int B, int M, bool COUNT>
-__global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MINW, 8))) void k_march(const float *__restrict__ vol, Params P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // whole workgroup uniform
+    // entropy (method 3) of 16 / 32-bin records: the exact logarithm through the
+    // LDS table (logf_fast_tabp: no f64 division), which the decode-bound wide
+    // entropy needs (copied behind the box slices)
+    const LogEnt *tab = nullptr;
+    float *st = nullptr;
+    if constexpr (M == 3 && B >= 16) {
+        LogEnt *t = reinterpret_cast<LogEnt *>(lds + 4u * (uint32_t)P.box_max);
+        copy_logtab(t);
+        __syncthreads();
+        tab = t;
+        // this wave's bin-major record column (entropy_stash) behind the table
+        st = lds + 4u * (uint32_t)P.box_max + 65u * (sizeof(LogEnt) / 4u) + (threadIdx.x >> 6) * 64u * B;
+    }
     const uint32_t lane = threadIdx.x & 63u;
     float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
     uint32_t lx, ly;
@@ -276,7 +333,7 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
                     const float *vbase =
                         vol + ((uint64_t)bz0 * P.sz + (uint64_t)by0 * P.sy + (uint64_t)bx0) *
                                   (uint64_t)B;
-                    decode_box<B, M>(vbase, P, box, dx, dxy, dxy * dz, lane);
+                    decode_box<B, M>(vbase, P, box, dx, dxy, dxy * dz, lane, tab, st);
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -303,7 +360,7 @@ __global__ __launch_bounds__(256) void k_march(const float *__restrict__ vol, Pa
             }
         }
         if (alive) {
-            if (!staged) sample = sample_direct<B, M>(vol, P, f);
+            if (!staged) sample = sample_direct<B, M>(vol, P, f, tab, st);
             n = i + 1;
             if (composite(P, sample, sx, sy, sz, sw)) {
                 alive = false;
@@ -768,7 +825,7 @@ __device__ __forceinline__ void wq_gather(const float *__restrict__ vol, const P
 // transpose a gathered corner and decode this lane's record
 template <int B, int M>
 __device__ __forceinline__ float wq_decode(float4 (&Mc)[B / 16][4], uint32_t g, bool alive,
-                                           float enorm, const LogEnt *lt) {
+                                           float enorm, const LogEnt *lt, float *col) {
 #pragma unroll
     for (int s = 0; s < B / 16; s++) quad_transpose(Mc[s], g);
     float st = 0.0f;
@@ -783,7 +840,9 @@ __device__ __forceinline__ float wq_decode(float4 (&Mc)[B / 16][4], uint32_t g, 
                 p[16 * s + 4 * c + 2] = Mc[s][c].z;
                 p[16 * s + 4 * c + 3] = Mc[s][c].w;
             }
-        st = record_stat_p<B, M>(p, enorm, lt);
+        // entropy: the rolled per-bin sum over this lane's LDS column (entropy_stash)
+        if constexpr (M == 3) st = entropy_stash<B>(p, col, threadIdx.x & 63u, enorm, lt);
+        else st = record_stat_p<B, M>(p, enorm, lt);
     }
     return st;
 }
@@ -797,12 +856,12 @@ __device__ __forceinline__ void wq_pair(const float *__restrict__ vol, const Par
                                         const QuadFeet &qc, const QuadFeet &qn, uint32_t g,
                                         bool alive, float4 (&A)[64 / B][B / 16][4],
                                         float4 (&Bf)[64 / B][B / 16][4], float (&sv)[8],
-                                        const LogEnt *lt) {
+                                        const LogEnt *lt, float *col) {
     constexpr int CG = 64 / B, NB = 8 / CG;
 #pragma unroll
     for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qc, (K + 1) * CG + c, g, Bf[c]);
 #pragma unroll
-    for (int c = 0; c < CG; c++) sv[K * CG + c] = wq_decode<B, M>(A[c], g, alive, P.enorm, lt);
+    for (int c = 0; c < CG; c++) sv[K * CG + c] = wq_decode<B, M>(A[c], g, alive, P.enorm, lt, col);
     if constexpr (K + 2 < NB) {
 #pragma unroll
         for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qc, (K + 2) * CG + c, g, A[c]);
@@ -811,13 +870,13 @@ __device__ __forceinline__ void wq_pair(const float *__restrict__ vol, const Par
         for (int c = 0; c < CG; c++) wq_gather<B>(vol, P, qn, c, g, A[c]);
     }
 #pragma unroll
-    for (int c = 0; c < CG; c++) sv[(K + 1) * CG + c] = wq_decode<B, M>(Bf[c], g, alive, P.enorm, lt);
+    for (int c = 0; c < CG; c++) sv[(K + 1) * CG + c] = wq_decode<B, M>(Bf[c], g, alive, P.enorm, lt, col);
 }
 
 template <int B, int M>
 __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, const Params &P,
                                              uint32_t slot, uint32_t tile, uint32_t tid,
-                                             const LogEnt *lt) {
+                                             const LogEnt *lt, float *col) {
     constexpr int S = B / 16;        // 16-byte chunks per lane per record
     constexpr int CG = 64 / B;       // corners per batch (64 VGPRs)
     constexpr int NB = 8 / CG;       // batches per step
@@ -857,8 +916,8 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
         const Foot fn = footprint(P, nx, ny, nz);
         const QuadFeet qn = quad_feet(fn, cont);
         float sv[8];
-        wq_pair<B, M, 0>(vol, P, qc, qn, g, alive, A, Bf, sv, lt);
-        if constexpr (NB == 4) wq_pair<B, M, 2>(vol, P, qc, qn, g, alive, A, Bf, sv, lt);
+        wq_pair<B, M, 0>(vol, P, qc, qn, g, alive, A, Bf, sv, lt, col);
+        if constexpr (NB == 4) wq_pair<B, M, 2>(vol, P, qc, qn, g, alive, A, Bf, sv, lt, col);
         if (alive) {
             n = i + 1;
             if (composite(P, blend8(sv, fc), sx, sy, sz, sw) || !cont) {
@@ -884,8 +943,10 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
 }
 
 template <int B, int M>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, M == 3 ? 8 : VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
     __shared__ LogEnt s_lt[M == 3 ? 65 : 1];  // entropy: the exact-log table (copy_logtab)
+    // entropy: each wave's bin-major record columns (entropy_stash)
+    __shared__ float s_col[M == 3 ? 4 * 64 * B : 1];
     if constexpr (M == 3) {
         copy_logtab(s_lt);
         __syncthreads();
@@ -893,7 +954,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MIN
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
-    const int n = march_wq_tile<B, M>(vol, P, slot, tile, threadIdx.x, s_lt);
+    const int n = march_wq_tile<B, M>(vol, P, slot, tile, threadIdx.x, s_lt,
+                                      s_col + (threadIdx.x >> 6) * 64u * B);
     if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
 }
 
@@ -2321,7 +2383,9 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     const dim3 grid(nslots), block(256);
     // one f32 box slice of box_max voxels per wave (4 waves); a larger request
     // caps the workgroups resident per CU (160 KiB of LDS per CU)
-    const size_t lds = cap_lds(P, P.wg_per_cu, B > 0 ? (size_t)P.box_max * 4u * sizeof(float) : 0);
+    // (+ the log table and the record columns of the wide entropy march, k_march)
+    const size_t lds = cap_lds(P, P.wg_per_cu, B > 0 ? (size_t)P.box_max * 4u * sizeof(float) +
+                                                   (B >= 16 && method == 3 ? 65 * sizeof(LogEnt) + 4u * 64u * B * sizeof(float) : 0) : 0);
     if constexpr (!COUNT && B > 0 && B <= 8) {
         if (P.path == 7) {
             hipError_t err = hipSuccess;
