@@ -129,3 +129,13 @@ def test_tuning_knobs_are_explicit(pkg):
     for f in ("vr_kernels.hip", "vr_seg.hip", "vr_gmm.hip", "vr_stats.hip", "vr_flex.hip"):
         assert "getenv(" not in open(os.path.join(ROOT, "volume-rendering-based-on-"
                                                   "distribution-data_amd", "csrc", f)).read()
+
+
+def test_init_gmm_validates_array_likes_without_gpu(pkg):
+    """init_gmm takes lists like numpy arrays (converted before the shape checks) and
+    rejects mismatched shapes with ValueError before any device call"""
+    wm = np.zeros((2, 3, 4, 8, 2), np.float32).tolist()
+    with pytest.raises(ValueError, match="sigma must have shape"):
+        pkg.init_gmm(wm, np.zeros((2, 3, 4, 7), np.float32).tolist())
+    with pytest.raises(ValueError, match="wm must have shape"):
+        pkg.init_gmm(np.zeros((2, 3, 4, 8), np.float32).tolist(), [[0.0]])

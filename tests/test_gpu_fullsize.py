@@ -133,10 +133,11 @@ def test_footprint_count_at_size(pkg, orc, gpu, name, cam):
             assert u == 399031053
 
 
-@pytest.mark.parametrize("cam", ["C0", "C1"])
+@pytest.mark.parametrize("cam", ["C0", "C1", "S"])
 def test_full_frame_baked(pkg, orc, gpu, cam):
     """config 4 after basicDataProcessing (the reference's own order, C:1200-1221):
-    frames filter the baked statistics planes"""
+    frames filter the baked statistics planes (the side view S: the method's
+    plane's z-rows copy, round 4)"""
     import torch
     n, nb, W, H = CONFIGS["1024x8"]
     vol = scene(pkg, orc, "1024x8")
@@ -147,11 +148,13 @@ def test_full_frame_baked(pkg, orc, gpu, cam):
             ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
             got = render_frames(pkg, torch, W, H, m, method, n_frames=1)[0]
             assert_parity(got[:3], ref, f"baked 1024x8 {cam} m{method} ({got[3]})")
+            if cam == "S":
+                assert "plane_zrows" in got[3], got[3]
     finally:
         pkg.release_stats()
 
 
-@pytest.mark.parametrize("cam", ["C0", "C1"])
+@pytest.mark.parametrize("cam", ["C0", "C1", "S"])
 def test_rank_lists_of_eight_gpus(pkg, orc, gpu, cam):
     """config 4 split over 8 ranks as bench.py deals it (estimate lists, then the
     measured-cost re-deal): each rank's packed tiles through the kernel the rank
@@ -217,3 +220,29 @@ def test_render_kernel_grid_covers_the_frame(pkg, orc, gpu):
         torch.cuda.synchronize()
         assert int(torch.count_nonzero(out)) == 0
     assert TOL == 1e-4
+
+
+@pytest.mark.parametrize("cam", ["C0", "C1"])
+def test_wide_entropy_at_size(pkg, orc, gpu, cam):
+    """32-bin records (the reference's width, C:86-87) at 1080p, entropy (method 3):
+    the LDS-box march (C0) and the quad march (C1) with the rolled per-bin sums
+    over LDS record columns (round 4), every 8th row against the oracle"""
+    import torch
+    n, nb, W, H = 512, 32, 1920, 1080
+    _scene.vol = None
+    _scene.name = None
+    pkg.freeCudaBuffers()
+    pkg.synthesize((n, n, n), nb, SEED)
+    vol = orc.synth_volume(n, n, n, nb, SEED)
+    try:
+        m = camera(pkg, cam)
+        got = render_frames(pkg, torch, W, H, m, 3, n_frames=1)[0]
+        want = "k_march<B=32,M=3>" if cam == "C0" else "k_march_wq<B=32,M=3>"
+        assert got[3] == want, got[3]
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=3), row_stride=8)[:3]
+        rows = slice(0, None, 8)
+        assert_parity(tuple(a[rows] for a in got[:3]), tuple(a[rows] for a in ref),
+                      f"512x32 {cam} m3")
+    finally:
+        del vol
+        pkg.freeCudaBuffers()

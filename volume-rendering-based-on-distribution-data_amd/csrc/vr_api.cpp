@@ -26,6 +26,10 @@ struct State {
     uint64_t sy = 0, sz = 0;        // record pitch of a voxel row / slice in HBM
     float inv_view[12] = {0};       // __constant__ c_invViewMatrix starts zeroed (K:116)
     hipStream_t stream = nullptr;   // legacy default stream, like the reference
+    // a second, library-owned stream and two events for the split launch of a
+    // tile list (head and tail on two hardware queues, split_launch); made lazily
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool linear_filter = false;     // tex.filterMode = point after initCuda (K:2163)
     std::string err;
     int status = VR_OK;
@@ -1558,6 +1562,45 @@ int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins) {
 
 namespace {
 
+// Tooling (VR_HEAD_STREAM=1): a tile list's head (its first head_slots slots,
+// head_lanes lanes per ray) and tail (the rest: VR_HEAD_TAILPATH 2 = one lane
+// per ray, k_march_pipe; 7 = 2-lane windows) as two launches on two hardware
+// queues, each kernel at its own occupancy: the library's aux stream forks off
+// g.stream and joins it again, so the caller's stream sees one frame.
+hipError_t split_launch(int method, const vr::Params &P, uint32_t nslots) {
+    hipError_t e = hipSuccess;
+    if (!g.aux) {
+        e = hipStreamCreateWithFlags(&g.aux, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g.ev_fork, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g.ev_join, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t head = P.head_slots;
+    vr::Params Ph = P;
+    Ph.head_slots = 0;
+    Ph.n_tiles = head;
+    Ph.seg_lanes = P.head_lanes;
+    Ph.path = 7;
+    vr::Params Pt = P;
+    Pt.head_slots = 0;
+    Pt.n_tiles = nslots - head;
+    Pt.tile_list = P.tile_list + head;
+    Pt.out = P.out + (uint64_t)head * 256u;
+    if (P.out_f) Pt.out_f = P.out_f + (uint64_t)head * 256u * 4u;
+    if (P.out_n) Pt.out_n = P.out_n + (uint64_t)head * 256u;
+    Pt.wave_clock = nullptr;
+    Ph.wave_clock = nullptr;
+    const char *tp = vr::tuning("VR_HEAD_TAILPATH");
+    Pt.path = tp ? std::atoi(tp) : 2;
+    if ((e = hipEventRecord(g.ev_fork, g.stream)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(g.aux, g.ev_fork, 0)) != hipSuccess) return e;
+    if ((e = vr::launch_march(g.nb, method, g.vol, Ph, head, false, g.aux)) != hipSuccess) return e;
+    if ((e = vr::launch_march(g.nb, method, g.vol, Pt, nslots - head, false, g.stream)) != hipSuccess)
+        return e;
+    if ((e = hipEventRecord(g.ev_join, g.aux)) != hipSuccess) return e;
+    return hipStreamWaitEvent(g.stream, g.ev_join, 0);
+}
+
 // One frame of vr_render / render_kernel; clip_w x clip_h is the top-left
 // rectangle of pixels the launch covers (render_kernel's gridSize x blockSize,
 // K:2397 + K:282-286; the whole image otherwise).
@@ -1647,7 +1690,10 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
             P.bsy = g.bsy;
             P.bsz = g.bsz;
         }
-        e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
+        if (P.head_slots && vr::tuning("VR_HEAD_STREAM") && std::atoi(vr::tuning("VR_HEAD_STREAM")))
+            e = split_launch(desc->query_method, P, nslots);
+        else
+            e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
     }
     if (e != hipSuccess) return hip_fail(e, "launch(k_march)");
     if (P.tile_cost) g.cost_recorded = true;

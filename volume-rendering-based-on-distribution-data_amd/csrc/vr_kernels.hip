@@ -82,36 +82,13 @@ __device__ __forceinline__ void quad_transpose(float4 (&M)[4], uint32_t g) {
 
 
 
-// Entropy (K:761-769) of a 16 / 32-bin record with few registers: the lane parks
-// its record in its own bin-major LDS column (st[i * 64 + lane]: conflict-free)
-// and runs the per-bin sum as a rolled loop over it, the exact logarithm from
-// the LDS table -- the same operations in the same order as entropy_p, so the
-// same float.  Unrolled over 32 bins the decode held ~430 registers (1 wave per
-// SIMD); rolled, the march keeps several waves per SIMD to hide its loads.
-template <int B>
-__device__ __forceinline__ float entropy_stash(const float (&p)[B], float *st, uint32_t lane,
-                                               float enorm, const LogEnt *tab) {
-#pragma unroll
-    for (int i = 0; i < B; i++) st[i * 64 + lane] = p[i];
-    float ent = 0.0f;
-#pragma unroll 2
-    for (int i = 0; i < B; i++) {
-        const float pr = st[i * 64 + lane];  // written by this lane: program order suffices
-        const double t =
-            pr <= 0 ? 0.0 : div_const((double)logf_canon_p(pr, tab), VR_LN2_D, kLn2R);
-        ent = (float)((double)ent + (double)pr * t);
-    }
-    ent = -ent;
-    return ent / enorm;
-}
-
 // the statistic of a record in the box / direct paths of k_march: wide entropy
 // through the LDS column (st: this wave's, 64 * B floats), everything else as
 // record_stat
 template <int B, int M>
 __device__ __forceinline__ float box_stat(const float (&p)[B], const Params &P, float *st,
                                           uint32_t lane, const LogEnt *tab) {
-    if constexpr (M == 3 && B >= 16) return entropy_stash<B>(p, st, lane, P.enorm, tab);
+    if constexpr (M == 3 && B >= 8) return entropy_stash<B>(p, st, lane, P.enorm, tab);
     else return record_stat<B, M>(p, P.enorm);
 }
 
@@ -273,12 +250,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // whole workgroup uniform
-    // entropy (method 3) of 16 / 32-bin records: the exact logarithm through the
-    // LDS table (logf_fast_tabp: no f64 division), which the decode-bound wide
-    // entropy needs (copied behind the box slices)
+    // entropy (method 3) of 8 / 16 / 32-bin records: the exact logarithm through
+    // the LDS table (logf_fast_tabp: no f64 division) and the rolled per-bin sum
+    // over the lane's record column (entropy_stash), behind the box slices
     const LogEnt *tab = nullptr;
     float *st = nullptr;
-    if constexpr (M == 3 && B >= 16) {
+    if constexpr (M == 3 && B >= 8) {
         LogEnt *t = reinterpret_cast<LogEnt *>(lds + 4u * (uint32_t)P.box_max);
         copy_logtab(t);
         __syncthreads();
@@ -437,6 +414,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
     __shared__ uint2 s_rows[4][kWsRows];  // x: ry | rz << 10 | loff << 20,  y: xmin
     __shared__ int s_mark[4][kWsRec];
     __shared__ float s_stat[4][kWsRec];
+    __shared__ float s_col[4][M == 3 ? 64 * B : 1];  // entropy: per-wave record columns (entropy_stash)
     extern __shared__ __attribute__((aligned(32))) LogEnt s_lt[];  // entropy's log table (M == 3)
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
@@ -561,7 +539,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
                     }
 #pragma unroll
                     for (int u = 0; u < U; u++)
-                        if (li[u] >= 0) stat[li[u]] = record_stat_p<B, M>(rr[u], P.enorm, s_lt);
+                        if (li[u] >= 0)
+                            stat[li[u]] = M == 3 ? entropy_stash<B>(rr[u], s_col[threadIdx.x >> 6], lane, P.enorm, s_lt)
+                                                 : record_stat_p<B, M>(rr[u], P.enorm, s_lt);
                 }
                 wave_sync();
                 if (alive) {
@@ -621,7 +601,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_PIPE_WAV
     if (tile == kPad) return;
     unsigned long long t0 = 0;
     if (P.wave_clock) t0 = wall_clock64();
-    const int n = march_pipe_tile<B, M, GM>(vol, P, slot, tile, threadIdx.x);
+    float *st = nullptr;
+    const LogEnt *tab = nullptr;
+    if constexpr (M == 3) {  // entropy: rolled per-bin sums over LDS record columns
+        __shared__ EntropyLds<B> el;
+        copy_logtab(el.tab);
+        __syncthreads();
+        st = el.col + (threadIdx.x >> 6) * 64u * B;
+        tab = el.tab;
+    }
+    const int n = march_pipe_tile<B, M, GM>(vol, P, slot, tile, threadIdx.x, st, tab);
     if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
     if (P.wave_clock && (threadIdx.x & 63) == 0) {
         unsigned long long *w = P.wave_clock + ((uint64_t)slot * 4u + threadIdx.x / 64u) * 3u;
@@ -1044,8 +1033,15 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
     ln = qc_gather<G, BR>(vol, P, fn, g, L);
     float s0 = 0.0f, s1 = 0.0f;
     if (lc) {
-        s0 = record_stat_p<8, M>(r0, P.enorm, lt);
-        s1 = record_stat_p<8, M>(r1, P.enorm, lt);
+        if constexpr (M == 3) {  // rolled per-bin sums over this lane's LDS column
+            float *col = reinterpret_cast<float *>(const_cast<LogEnt *>(lt) + 65) +
+                         (threadIdx.x >> 6) * 64u * 8u;
+            s0 = entropy_stash<8>(r0, col, threadIdx.x & 63u, P.enorm, lt);
+            s1 = entropy_stash<8>(r1, col, threadIdx.x & 63u, P.enorm, lt);
+        } else {
+            s0 = record_stat_p<8, M>(r0, P.enorm, lt);
+            s1 = record_stat_p<8, M>(r1, P.enorm, lt);
+        }
     }
     return qc_blend<G>(fc, s0, s1);
 }
@@ -1738,7 +1734,8 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
             float dec[B];
             codec_decode_scr<B, TL>(P, s_lds, scr, c[j], pre[j],
                                     P.err + v[j] * (uint64_t)P.err_slots, dec);
-            sv[j] = C == 2 ? entropy_p<B>(dec, P.enorm, lt) : codec_stat_of<B, C>(dec, P.enorm);
+            // entropy: rolled per-bin sum over the thread's LDS scratch column
+            sv[j] = C == 2 ? entropy_col<B, 256>(dec, scr, P.enorm, lt) : codec_stat_of<B, C>(dec, P.enorm);
         }
         n = i + 1;
         if (composite(P, blend8(sv, f), sx, sy, sz, sw)) break;
@@ -1803,7 +1800,7 @@ __device__ __forceinline__ float cq_stat(const Params &P, const float *s_tpl, fl
                                          uint64_t vox) {
     float dec[8];
     codec_decode_scr<8, TL>(P, s_tpl, scr, c, pre, P.err + vox * (uint64_t)P.err_slots, dec);
-    if constexpr (C == 2) return entropy_p<8>(dec, P.enorm, lt);
+    if constexpr (C == 2) return entropy_col<8, 256>(dec, scr, P.enorm, lt);  // rolled, LDS column
     else return codec_stat_of<8, C>(dec, P.enorm);
 }
 
@@ -2385,7 +2382,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     // caps the workgroups resident per CU (160 KiB of LDS per CU)
     // (+ the log table and the record columns of the wide entropy march, k_march)
     const size_t lds = cap_lds(P, P.wg_per_cu, B > 0 ? (size_t)P.box_max * 4u * sizeof(float) +
-                                                   (B >= 16 && method == 3 ? 65 * sizeof(LogEnt) + 4u * 64u * B * sizeof(float) : 0) : 0);
+                                                   (B >= 8 && method == 3 ? 65 * sizeof(LogEnt) + 4u * 64u * B * sizeof(float) : 0) : 0);
     if constexpr (!COUNT && B > 0 && B <= 8) {
         if (P.path == 7) {
             hipError_t err = hipSuccess;
@@ -2404,7 +2401,8 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // 0.59 ms; 3 per CU 0.68; tools/rank_sim.py)
             const int qcap = P.wg_per_cu > 0 ? P.wg_per_cu
                              : (P.tile_list && (uint64_t)nslots * 256u <= 400000u) ? 1 : 2;
-            const size_t qlds = cap_lds(P, qcap);
+            // entropy: the log table + 4 waves' record columns (qc_group) at the front
+            const size_t qlds = cap_lds(P, qcap, method == 3 ? 65 * sizeof(LogEnt) + 4 * 64 * 8 * sizeof(float) : 0);
             if (P.quad2) {  // two lanes per ray, two workgroups per tile
                 note_kernel(P.bvol ? "k_march_quad2_brick" : "k_march_quad2", B, method);
                 const dim3 grid2(((nslots + 7u) / 8u) * 16u);

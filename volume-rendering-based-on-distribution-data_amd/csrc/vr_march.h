@@ -262,10 +262,58 @@ __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Par
 template <int M>
 constexpr int kGatherMode = M == 0 ? 1 : (M == -1 ? 2 : 0);
 
+// Entropy (K:761-769) of a record with few registers: the lane parks
+// its record in its own bin-major LDS column (st[i * 64 + lane]: conflict-free)
+// and runs the per-bin sum as a rolled loop over it, the exact logarithm from
+// the LDS table -- the same operations in the same order as entropy_p, so the
+// same float.  Unrolled over 32 bins the decode held ~430 registers (1 wave per
+// SIMD); rolled, the march keeps several waves per SIMD to hide its loads.  The
+// 8-bin marches use it too (their unrolled 8 x 8 logarithms per step held
+// 360-470 registers, or spilled).
+template <int B, int STRIDE = 64>
+__device__ __forceinline__ float entropy_col(const float (&p)[B], float *col, float enorm,
+                                             const LogEnt *tab) {
+#pragma unroll
+    for (int i = 0; i < B; i++) col[i * STRIDE] = p[i];
+    float ent = 0.0f;
+#pragma unroll 2
+    for (int i = 0; i < B; i++) {
+        const float pr = col[i * STRIDE];  // written by this lane: program order suffices
+        const double t =
+            pr <= 0 ? 0.0 : div_const((double)logf_canon_p(pr, tab), VR_LN2_D, kLn2R);
+        ent = (float)((double)ent + (double)pr * t);
+    }
+    ent = -ent;
+    return ent / enorm;
+}
+// st: the wave's 64 * B-float region, bin-major (st[i * 64 + lane])
+template <int B>
+__device__ __forceinline__ float entropy_stash(const float (&p)[B], float *st, uint32_t lane,
+                                               float enorm, const LogEnt *tab) {
+    return entropy_col<B, 64>(p, st + lane, enorm, tab);
+}
+
+// an entropy march's LDS: the log table (65 entries) + 4 waves' record columns
+template <int B>
+struct EntropyLds {
+    LogEnt tab[65];
+    float col[4 * 64 * B];
+};
+
+// (st, tab): this wave's record column and the LDS log table of an entropy
+// march (EntropyLds), nullptr for the other methods
 template <int B, int M>
 __device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][B],
-                                         const Foot &f) {
+                                         const Foot &f, float *st = nullptr,
+                                         const LogEnt *tab = nullptr) {
     float s[8];
+    if constexpr (M == 3) {
+        if (st) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) s[j] = entropy_stash<B>(rec[j], st, threadIdx.x & 63u, P.enorm, tab);
+            return blend8(s, f);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 8; j++) s[j] = record_stat<B, M>(rec[j], P.enorm);
     return blend8(s, f);
@@ -280,7 +328,8 @@ __device__ __forceinline__ float decode8(const Params &P, const float (&rec)[8][
 // the 256-thread tile; slot: the tile's launch slot (packed output position).
 template <int B, int M, int GM = kGatherMode<M>>
 __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, const Params &P,
-                                               uint32_t slot, uint32_t tile, uint32_t tid) {
+                                               uint32_t slot, uint32_t tile, uint32_t tid,
+                                               float *st = nullptr, const LogEnt *tab = nullptr) {
     uint32_t lx, ly;
     tile_pixel(tid, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
@@ -318,7 +367,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
         // the select changed the schedule again.)
         fn = footprint(P, nx, ny, nz);
         gather8<B, GM>(vol, P, fn, rn);
-        const float sample = decode8<B, M>(P, rc, fc);
+        const float sample = decode8<B, M>(P, rc, fc, st, tab);
         n = i + 1;
         if (composite(P, sample, sx, sy, sz, sw) || !cont) {
             alive = false;
