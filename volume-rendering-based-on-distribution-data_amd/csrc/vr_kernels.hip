@@ -88,8 +88,10 @@ __device__ __forceinline__ void quad_transpose(float4 (&M)[4], uint32_t g) {
 template <int B, int M>
 __device__ __forceinline__ float box_stat(const float (&p)[B], const Params &P, float *st,
                                           uint32_t lane, const LogEnt *tab) {
-    if constexpr (M == 3 && B >= 8) return entropy_stash<B>(p, st, lane, P.enorm, tab);
-    else return record_stat<B, M>(p, P.enorm);
+    if constexpr (M == 3 && B >= 8) {
+        if (st) return entropy_stash<B>(p, st, lane, P.enorm, tab);
+    }
+    return record_stat<B, M>(p, P.enorm);  // (callers without an LDS column: k_march_ws's direct path)
 }
 
 // Compile-time tuning knobs (tools/build_variants.sh builds sweeps of them).
@@ -414,7 +416,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
     __shared__ uint2 s_rows[4][kWsRows];  // x: ry | rz << 10 | loff << 20,  y: xmin
     __shared__ int s_mark[4][kWsRec];
     __shared__ float s_stat[4][kWsRec];
-    __shared__ float s_col[4][M == 3 ? 64 * B : 1];  // entropy: per-wave record columns (entropy_stash)
     extern __shared__ __attribute__((aligned(32))) LogEnt s_lt[];  // entropy's log table (M == 3)
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
@@ -540,8 +541,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WS_WAVES
 #pragma unroll
                     for (int u = 0; u < U; u++)
                         if (li[u] >= 0)
-                            stat[li[u]] = M == 3 ? entropy_stash<B>(rr[u], s_col[threadIdx.x >> 6], lane, P.enorm, s_lt)
-                                                 : record_stat_p<B, M>(rr[u], P.enorm, s_lt);
+                            stat[li[u]] = record_stat_p<B, M>(rr[u], P.enorm, s_lt);
                 }
                 wave_sync();
                 if (alive) {
@@ -604,11 +604,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_PIPE_WAV
     float *st = nullptr;
     const LogEnt *tab = nullptr;
     if constexpr (M == 3) {  // entropy: rolled per-bin sums over LDS record columns
-        __shared__ EntropyLds<B> el;
-        copy_logtab(el.tab);
+        // (in the dynamic LDS, the launch requests sizeof(EntropyLds<B>) at least)
+        extern __shared__ __attribute__((aligned(32))) float s_dyn[];
+        EntropyLds<B> *el = reinterpret_cast<EntropyLds<B> *>(s_dyn);
+        copy_logtab(el->tab);
         __syncthreads();
-        st = el.col + (threadIdx.x >> 6) * 64u * B;
-        tab = el.tab;
+        st = el->col + (threadIdx.x >> 6) * 64u * B;
+        tab = el->tab;
     }
     const int n = march_pipe_tile<B, M, GM>(vol, P, slot, tile, threadIdx.x, st, tab);
     if (P.tile_cost) record_tile_cost(P, tile, n);  // all lanes have reconverged here
@@ -2464,7 +2466,8 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             switch (method) {
             case 1: hipLaunchKernelGGL((k_march_pipe<B, 1, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
             case 2: hipLaunchKernelGGL((k_march_pipe<B, 2, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
-            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3, 3>), grid, block, occupancy_lds(P), s, P.avol, Q); break;
+            // (the entropy march's LDS columns and table are part of the request)
+            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3, 3>), grid, block, cap_lds(P, P.wg_per_cu, sizeof(EntropyLds<B>)), s, P.avol, Q); break;
             }
             return hipGetLastError();
         }
@@ -2494,7 +2497,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
                 return hipErrorInvalidValue;
             case 1: hipLaunchKernelGGL((k_march_pipe<B, 1>), grid, block, occupancy_lds(P), s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_pipe<B, 2>), grid, block, occupancy_lds(P), s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3>), grid, block, occupancy_lds(P), s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_pipe<B, 3>), grid, block, cap_lds(P, P.wg_per_cu, sizeof(EntropyLds<B>)), s, vol, P); break;
             }
             return hipGetLastError();
         }
@@ -2508,7 +2511,10 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         // stays on k_march: unrolled over a batch its per-bin logarithms need more
         // than 256 VGPRs (B = 16: 512 + spills).
         if (P.path != 1 && (method == 1 || method == 2 || (method == 3 && WQ3))) {
-            const size_t wl = occupancy_lds(P);
+            // an occupancy cap's LDS request leaves room for the kernel's static LDS
+            // (the entropy march's log table and record columns)
+            const size_t wl = cap_lds(P, P.wg_per_cu, 0,
+                                      method == 3 ? 65 * sizeof(LogEnt) + 4 * 64 * B * sizeof(float) : 64);
             int kind = (B == 16 && !P.oblique && method != 3) ? 1 : 2;
             if (const char *ew = tuning("VR_WIDE")) {
                 const int v = std::atoi(ew);
