@@ -207,14 +207,14 @@ def test_oblique_coarse_volume_takes_segmented_march(pkg, orc, gpu):
 def test_row_aligned_coarse_volume_takes_box_march(pkg, orc, gpu, tune):
     """row-aligned full frame, >= 4 pixels per voxel, more rays than the segmented
     threshold: methods 1/2 stage the wave's footprint box in LDS (path 1),
-    bit-identical; entropy keeps the wave-staged march; a frame below the threshold takes
-    the ray-segmented march"""
+    bit-identical; 8-bin entropy takes it too (round 4: the rolled LDS-column entropy);
+    a frame below the threshold takes the ray-segmented march"""
     import torch
     tune.set("VR_SEG_RAYS", "1000")
     vol = orc.synth_volume(20, 18, 16, 8)
     m = pkg.camera.display_inv_view((0.0, 0.0), translation=(0.05, -0.1, 0.0))
     for method, W, H, kern in ((1, 96, 64, "k_march<"), (2, 96, 64, "k_march<"),
-                               (3, 96, 64, "k_march_ws"), (1, 32, 24, "k_march_segp4")):
+                               (3, 96, 64, "k_march<"), (1, 32, 24, "k_march_segp4")):
         got = gpu_render(pkg, vol, W, H, m, method, torch)
         ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
         assert_parity(got, ref, f"coarse rows m{method} {W}x{H}")

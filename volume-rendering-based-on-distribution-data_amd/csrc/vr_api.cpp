@@ -595,6 +595,11 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // (VR_SEG lanes per ray).
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
     P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
+    // 8-bin entropy of row-aligned views: the LDS-box march with the rolled
+    // LDS-column entropy (k_march<8,3>, 128 VGPRs) beats the wave-staged march:
+    // 1024^3 C0 4.31 -> 3.52 ms, 512^3 3.10 -> 1.63 (round 4,
+    // profiles/r04/variants_1024x8_m3.log, variants_512x8_m3.log)
+    if (along_rows && d->query_method == 3 && g.nb == 8) P.path = 1;
     P.oblique = along_rows ? 0 : 1;
     device_lds(P.lds_cu, P.lds_wg);
     // Views whose screen x runs along the volume's z or y (|M[8]| / |M[4]| >=

@@ -831,8 +831,10 @@ __device__ __forceinline__ float wq_decode(float4 (&Mc)[B / 16][4], uint32_t g, 
                 p[16 * s + 4 * c + 2] = Mc[s][c].z;
                 p[16 * s + 4 * c + 3] = Mc[s][c].w;
             }
-        // entropy: the rolled per-bin sum over this lane's LDS column (entropy_stash)
-        if constexpr (M == 3) st = entropy_stash<B>(p, col, threadIdx.x & 63u, enorm, lt);
+        // 32-bin entropy: the rolled per-bin sum over this lane's LDS column
+        // (entropy_stash; 1024^3 x 32 C1 m3 ~51 -> 26.8 ms); 16 bins keep the
+        // unrolled sum (13.4 ms rolled vs 12.5)
+        if constexpr (M == 3 && B >= 32) st = entropy_stash<B>(p, col, threadIdx.x & 63u, enorm, lt);
         else st = record_stat_p<B, M>(p, enorm, lt);
     }
     return st;
@@ -934,10 +936,10 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
 }
 
 template <int B, int M>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, M == 3 ? 8 : VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, M == 3 && B >= 32 ? 8 : VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
     __shared__ LogEnt s_lt[M == 3 ? 65 : 1];  // entropy: the exact-log table (copy_logtab)
     // entropy: each wave's bin-major record columns (entropy_stash)
-    __shared__ float s_col[M == 3 ? 4 * 64 * B : 1];
+    __shared__ float s_col[M == 3 && B >= 32 ? 4 * 64 * B : 1];
     if constexpr (M == 3) {
         copy_logtab(s_lt);
         __syncthreads();
@@ -1035,15 +1037,10 @@ __device__ __forceinline__ float qc_group(const float *__restrict__ vol, const P
     ln = qc_gather<G, BR>(vol, P, fn, g, L);
     float s0 = 0.0f, s1 = 0.0f;
     if (lc) {
-        if constexpr (M == 3) {  // rolled per-bin sums over this lane's LDS column
-            float *col = reinterpret_cast<float *>(const_cast<LogEnt *>(lt) + 65) +
-                         (threadIdx.x >> 6) * 64u * 8u;
-            s0 = entropy_stash<8>(r0, col, threadIdx.x & 63u, P.enorm, lt);
-            s1 = entropy_stash<8>(r1, col, threadIdx.x & 63u, P.enorm, lt);
-        } else {
-            s0 = record_stat_p<8, M>(r0, P.enorm, lt);
-            s1 = record_stat_p<8, M>(r1, P.enorm, lt);
-        }
+        // (the rolled LDS-column entropy measured slower here: 1024^3 x 8 C1 m3
+        // 8.37 -> 9.44 ms, profiles/r04/variants_1024x8_m3.log)
+        s0 = record_stat_p<8, M>(r0, P.enorm, lt);
+        s1 = record_stat_p<8, M>(r1, P.enorm, lt);
     }
     return qc_blend<G>(fc, s0, s1);
 }
@@ -2403,8 +2400,8 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // 0.59 ms; 3 per CU 0.68; tools/rank_sim.py)
             const int qcap = P.wg_per_cu > 0 ? P.wg_per_cu
                              : (P.tile_list && (uint64_t)nslots * 256u <= 400000u) ? 1 : 2;
-            // entropy: the log table + 4 waves' record columns (qc_group) at the front
-            const size_t qlds = cap_lds(P, qcap, method == 3 ? 65 * sizeof(LogEnt) + 4 * 64 * 8 * sizeof(float) : 0);
+            // entropy: the log table (qc_group) at the front
+            const size_t qlds = cap_lds(P, qcap, method == 3 ? 65 * sizeof(LogEnt) : 0);
             if (P.quad2) {  // two lanes per ray, two workgroups per tile
                 note_kernel(P.bvol ? "k_march_quad2_brick" : "k_march_quad2", B, method);
                 const dim3 grid2(((nslots + 7u) / 8u) * 16u);
@@ -2514,7 +2511,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // an occupancy cap's LDS request leaves room for the kernel's static LDS
             // (the entropy march's log table and record columns)
             const size_t wl = cap_lds(P, P.wg_per_cu, 0,
-                                      method == 3 ? 65 * sizeof(LogEnt) + 4 * 64 * B * sizeof(float) : 64);
+                                      method == 3 ? 65 * sizeof(LogEnt) + (B >= 32 ? 4 * 64 * B * sizeof(float) : 4) : 64);
             int kind = (B == 16 && !P.oblique && method != 3) ? 1 : 2;
             if (const char *ew = tuning("VR_WIDE")) {
                 const int v = std::atoi(ew);
