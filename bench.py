@@ -620,11 +620,17 @@ def main():
         with torch.cuda.stream(stream):
             if world == 1:
                 frame.zero_()  # C:208 (tile slots need none: misses are written as 0)
-            else:
-                if works[b] is not None:
-                    works[b].wait()           # the gather of frame f - RING has read packed[b]
-                if assembled[b] is not None:
-                    stream.wait_event(assembled[b])  # rank 0 has unscattered recv[b]
+            elif (nframe[0] - 1) % RING == 0 and nframe[0] > 1:
+                # once per RING frames, on the newest gather and assembly (their
+                # streams run in order, so this covers the older ones): the next
+                # RING frames reuse buffers whose gathers and assemblies (frames
+                # f - RING .. f - 1) are then done.  One wait per frame cost the
+                # loop more (tools/host_cost.py)
+                w = (nframe[0] - 2) % RING
+                if works[w] is not None:
+                    works[w].wait()
+                if assembled[w] is not None:
+                    stream.wait_event(assembled[w])
             # per-frame timing events only at N = 1: between the render, the gather
             # and the assembly streams of N > 1 they cost the frame loop ~0.1 ms per
             # frame (tools/host_cost.py); N > 1 times its renders after the loop

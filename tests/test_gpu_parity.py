@@ -903,8 +903,8 @@ def test_quad_march_brick_layout(pkg, orc, gpu, dims, brick, tune):
     ((40, 36, 32), 8, 256, 200, "k_march_segp4<")])
 def test_small_frames_take_segmented_march(pkg, orc, gpu, dims, nb, W, H, want):
     """small full frames run the pipelined ray-segmented march: 4 lanes per ray up to
-    128 K rays; oblique views (B < 8) 2 lanes up to 700 K, row-aligned ones one lane
-    above 128 K; bit-identical"""
+    128 K rays; oblique views (B < 8) 4 lanes up to 400 K (round 4), 2 up to 700 K,
+    row-aligned ones one lane above 128 K; bit-identical"""
     import torch
     vol = orc.synth_volume(*dims, nb)
     pkg.init_distribution(vol)
@@ -914,7 +914,8 @@ def test_small_frames_take_segmented_march(pkg, orc, gpu, dims, nb, W, H, want):
             ref = orc.render(vol, orc.make_params(W, H, cam, query_method=method))[:3]
             assert_parity(got, ref, f"{dims}x{nb} {W}x{H} m{method}")
             rows = abs(float(cam[0])) >= 0.95
-            k = want or ("k_march_pipe<" if rows else "k_march_segp2<")
+            k = want or ("k_march_pipe<" if rows else
+                         "k_march_segp4<" if W * H <= 400000 else "k_march_segp2<")
             if nb < 8 or rows:
                 assert pkg.last_kernel().startswith(k), pkg.last_kernel()
 

@@ -72,28 +72,34 @@ def main():
     pkg.set_stream(stream)
     frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
     with torch.cuda.stream(stream):
-        packed = [torch.zeros(slots * 256, dtype=torch.int32, device=dev) for _ in range(4)]
-        recv1 = [torch.empty((1, slots * 256), dtype=torch.int32, device=dev) for _ in range(4)]
+        packed = [torch.zeros(slots * 256, dtype=torch.int32, device=dev) for _ in range(8)]
+        recv1 = [torch.empty((1, slots * 256), dtype=torch.int32, device=dev) for _ in range(8)]
         recvN = torch.zeros((N, slots * 256), dtype=torch.int32, device=dev)
         my_list = torch.from_numpy(lists[0].view(np.int32).copy()).to(dev)
         all_lists = torch.from_numpy(lists.view(np.int32).copy()).to(dev)
         descs = [pkg.make_desc(packed[b], W, H, m, query_method=args.method,
-                               d_tile_list=my_list, n_tiles=slots) for b in range(4)]
+                               d_tile_list=my_list, n_tiles=slots) for b in range(8)]
     torch.cuda.synchronize()
-    works, assembled, ev = [None] * 4, [None] * 4, []
+    works, assembled, ev = [None] * 8, [None] * 8, []
     nframe = [0]
 
-    def step(events=False, gather=True, unscatter=True, ring=4, mode="nccl", on_render=False):
+    def step(events=False, gather=True, unscatter=True, ring=4, mode="nccl", on_render=False,
+             every=1):
         # bench.py step(), N > 1, rank 0.  mode: "nccl" the gather on the one-rank
         # group, "copy" a device copy on the assembly stream instead; on_render: the
         # unscatter of the previous frame on the render stream after this render
-        b = nframe[0] % ring
+        f = nframe[0]
+        b = f % ring
         nframe[0] += 1
         with torch.cuda.stream(stream):
-            if works[b] is not None:
-                works[b].wait()
-            if assembled[b] is not None:
-                stream.wait_event(assembled[b])
+            # every: wait once per `every` frames, on the newest gather / assembly
+            # (the NCCL and assembly streams are in order, so that covers the
+            # older ones; needs ring >= every)
+            w = b if every == 1 else ((f - 1) % ring if f % every == 0 else None)
+            if w is not None and works[w] is not None:
+                works[w].wait()
+            if w is not None and assembled[w] is not None:
+                stream.wait_event(assembled[w])
             if events:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
@@ -161,12 +167,11 @@ def main():
     print(f"  host calls alone: vr_render {t_render:.4f} ms (no launch), dist.gather {t_gather:.4f} ms, "
           f"unscatter {t_unsc:.4f} ms", flush=True)
     pkg.set_tuning("VR_DRY", "0")
-    for kw in ({}, {"mode": "copy"}, {"unscatter": False}, {"gather": False},
-               {"on_render": True}, {"mode": "copy", "unscatter": False},
-               {"gather": False, "unscatter": False},
+    for kw in ({}, {"every": 4}, {"every": 8, "ring": 8}, {"mode": "copy"}, {"unscatter": False},
+               {"gather": False}, {"gather": False, "unscatter": False},
                {"events": True, "gather": False, "unscatter": False}):
-        works[:] = [None] * 4
-        assembled[:] = [None] * 4
+        works[:] = [None] * 8
+        assembled[:] = [None] * 8
         ev.clear()
         loop(50, **kw)
         ev.clear()

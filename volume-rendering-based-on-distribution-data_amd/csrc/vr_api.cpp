@@ -26,10 +26,6 @@ struct State {
     uint64_t sy = 0, sz = 0;        // record pitch of a voxel row / slice in HBM
     float inv_view[12] = {0};       // __constant__ c_invViewMatrix starts zeroed (K:116)
     hipStream_t stream = nullptr;   // legacy default stream, like the reference
-    // a second, library-owned stream and two events for the split launch of a
-    // tile list (head and tail on two hardware queues, split_launch); made lazily
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool linear_filter = false;     // tex.filterMode = point after initCuda (K:2163)
     std::string err;
     int status = VR_OK;
@@ -600,6 +596,12 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // 1024^3 C0 4.31 -> 3.52 ms, 512^3 3.10 -> 1.63 (round 4,
     // profiles/r04/variants_1024x8_m3.log, variants_512x8_m3.log)
     if (along_rows && d->query_method == 3 && g.nb == 8) P.path = 1;
+    // ... and of oblique views of a volume coarse for the frame (>= 4 pixels per
+    // voxel of the x-y face): 512^3 C1 m3 8.32 -> 5.11 ms; at 1024^3 the quad
+    // march stays ahead (8.42 vs 8.61; profiles/r04/variants_*_m3_r4g.log)
+    if (!along_rows && d->query_method == 3 && g.nb == 8 && !d->d_tile_list &&
+        (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
+        P.path = 1;
     P.oblique = along_rows ? 0 : 1;
     device_lds(P.lds_cu, P.lds_wg);
     // Views whose screen x runs along the volume's z or y (|M[8]| / |M[4]| >=
@@ -668,6 +670,13 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     if (along_rows && !d->d_tile_list && g.nb == 32 && d->query_method >= 1 &&
         d->query_method <= 3 && (uint64_t)d->width * d->height > seg_rays)
         P.path = 1;
+    // 16-bin entropy of row-aligned full frames: the box decodes each record
+    // once per wave-step with the rolled LDS-column entropy (round 4): 1024^3 x
+    // 16 C0 m3 12.3 -> 5.6 ms; oblique views keep the quad march (13.7 vs 14.0)
+    // (profiles/r04/variants_1024x16_m3_r4g.log)
+    if (along_rows && !d->d_tile_list && g.nb == 16 && d->query_method == 3 &&
+        (uint64_t)d->width * d->height > seg_rays)
+        P.path = 1;
     // Small full frames (BASELINE configs 1 and 2: 128^3 x 1 at 256^2, 256^3 x 4
     // at 512^2) cannot fill the GPU with one ray per lane, so the per-ray step
     // chain sets the time, as for a rank's tile list: the pipelined
@@ -684,7 +693,10 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         if (!d->d_tile_list && !codec && !flex && rays <= limit && nb_ok &&
             (d->query_method == 1 || d->query_method == 2)) {
             P.path = 7;
-            small_seg = rays <= 131072 ? -4 : -2;
+            // oblique frames up to 400 K rays on 4-lane windows too (round 4, after
+            // the unconditional gathers): 256^3 x 4 C1 at 512^2 0.161 -> 0.135 ms
+            // (profiles/r04/variants_256x4_r4g.log)
+            small_seg = (rays <= 131072 || (!row_like && rays <= 400000)) ? -4 : -2;
         }
     }
     if (P.path != 2 && P.path != 7) P.axis_view = 0;  // 7: the segmented march reads the copy too
@@ -1567,45 +1579,6 @@ int vr_volume_info(vr_extent *dims, int *nbins, const float **d_bins) {
 
 namespace {
 
-// Tooling (VR_HEAD_STREAM=1): a tile list's head (its first head_slots slots,
-// head_lanes lanes per ray) and tail (the rest: VR_HEAD_TAILPATH 2 = one lane
-// per ray, k_march_pipe; 7 = 2-lane windows) as two launches on two hardware
-// queues, each kernel at its own occupancy: the library's aux stream forks off
-// g.stream and joins it again, so the caller's stream sees one frame.
-hipError_t split_launch(int method, const vr::Params &P, uint32_t nslots) {
-    hipError_t e = hipSuccess;
-    if (!g.aux) {
-        e = hipStreamCreateWithFlags(&g.aux, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&g.ev_fork, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&g.ev_join, hipEventDisableTiming);
-        if (e != hipSuccess) return e;
-    }
-    const uint32_t head = P.head_slots;
-    vr::Params Ph = P;
-    Ph.head_slots = 0;
-    Ph.n_tiles = head;
-    Ph.seg_lanes = P.head_lanes;
-    Ph.path = 7;
-    vr::Params Pt = P;
-    Pt.head_slots = 0;
-    Pt.n_tiles = nslots - head;
-    Pt.tile_list = P.tile_list + head;
-    Pt.out = P.out + (uint64_t)head * 256u;
-    if (P.out_f) Pt.out_f = P.out_f + (uint64_t)head * 256u * 4u;
-    if (P.out_n) Pt.out_n = P.out_n + (uint64_t)head * 256u;
-    Pt.wave_clock = nullptr;
-    Ph.wave_clock = nullptr;
-    const char *tp = vr::tuning("VR_HEAD_TAILPATH");
-    Pt.path = tp ? std::atoi(tp) : 2;
-    if ((e = hipEventRecord(g.ev_fork, g.stream)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(g.aux, g.ev_fork, 0)) != hipSuccess) return e;
-    if ((e = vr::launch_march(g.nb, method, g.vol, Ph, head, false, g.aux)) != hipSuccess) return e;
-    if ((e = vr::launch_march(g.nb, method, g.vol, Pt, nslots - head, false, g.stream)) != hipSuccess)
-        return e;
-    if ((e = hipEventRecord(g.ev_join, g.aux)) != hipSuccess) return e;
-    return hipStreamWaitEvent(g.stream, g.ev_join, 0);
-}
-
 // One frame of vr_render / render_kernel; clip_w x clip_h is the top-left
 // rectangle of pixels the launch covers (render_kernel's gridSize x blockSize,
 // K:2397 + K:282-286; the whole image otherwise).
@@ -1695,10 +1668,7 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
             P.bsy = g.bsy;
             P.bsz = g.bsz;
         }
-        if (P.head_slots && vr::tuning("VR_HEAD_STREAM") && std::atoi(vr::tuning("VR_HEAD_STREAM")))
-            e = split_launch(desc->query_method, P, nslots);
-        else
-            e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
+        e = vr::launch_march(g.nb, desc->query_method, g.vol, P, nslots, false, g.stream);
     }
     if (e != hipSuccess) return hip_fail(e, "launch(k_march)");
     if (P.tile_cost) g.cost_recorded = true;
