@@ -559,12 +559,13 @@ def main():
     n_slots = lists.shape[1]
     frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
     # N > 1: a ring of RING packed buffers (and gather targets on rank 0): frame f
-    # renders into buffer f % RING, so it waits only for the gather and the
-    # assembly of frame f - RING, which had RING - 1 frames to finish.  With two
-    # buffers the next-but-one render waited for the gather of the frame just
-    # before it, which gets its CUs only as that frame's waves drain
-    # (tools/host_cost.py, profiles/r04/host_cost_*.log).
-    RING = 4 if world > 1 else 1
+    # renders into buffer f % RING; the render stream waits for the gathers and
+    # assemblies once per RING frames (below), so each buffer's gather had up to
+    # RING - 1 frames to finish.  Rank 0's frame loop with an 8-rank split, on one
+    # GPU: 0.2199 ms per frame waiting every frame (ring 4), 0.2179 every 4th,
+    # 0.2150 every 8th (ring 8), against 0.1984 without gather and assembly
+    # (tools/host_cost.py, profiles/r04/host_cost_N8_r4h.log).
+    RING = 8 if world > 1 else 1
     with torch.cuda.stream(stream):
         if world > 1:
             packed = [torch.zeros(n_slots * 256, dtype=torch.int32, device=dev) for _ in range(RING)]
