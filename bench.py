@@ -182,6 +182,7 @@ def cpu_baseline(pkg, cfg_name, m, method, row_stride):
         cb, tp, er = orc.synth_codec_field(n, n, n, nb, CODEC_TEMPLATES, CODEC_SLOTS, SEED)
     else:
         vol = orc.synth_volume(n, n, n, nb, SEED, threads)
+    print(f"cpu baseline: {n}^3 x {nb} volume in host RAM", file=sys.stderr, flush=True)
     p = orc.make_params(W, H, m, query_method=method, m7_dims=(n, n, n))
 
     def frame(want):
@@ -199,6 +200,7 @@ def cpu_baseline(pkg, cfg_name, m, method, row_stride):
         dt += time.perf_counter() - t0
         samples += smp
         frames += 1
+        print(f"cpu baseline: frame {frames} ({dt:.1f} s)", file=sys.stderr, flush=True)
     rows = len(range(0, H, row_stride))
     rays = rows * W * frames
     omp = orc.max_threads()

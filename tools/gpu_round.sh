@@ -1,10 +1,11 @@
 #!/bin/bash
-# Round measurement: for every workload a bench line (with the CPU baseline and
-# parity check), the rocprofv3 --kernel-trace --stats summary of the same bench
-# command, and the PMC passes -- FETCH_SIZE, WRITE_SIZE, TCC_EA0 requests, VALU
-# issue -- run one per process (MI355X_MICROARCH.md PMC slot limits) and folded
-# into traffic.json (tools/pmc_traffic.py, keyed by workload and by the sha256
-# of this libvr.so).  Then the steady-state rank simulation.
+# Round measurement: for every workload the PMC passes -- FETCH_SIZE, WRITE_SIZE,
+# TCC_EA0 requests, VALU issue -- run one per process (MI355X_MICROARCH.md PMC
+# slot limits) and folded into traffic.json (tools/pmc_traffic.py, keyed by
+# workload and by the sha256 of this libvr.so), then the bench line (with the CPU
+# baseline and parity check) reading that traffic.json, so the line carries its
+# own build's traffic, then the rocprofv3 --kernel-trace --stats summary of the
+# same bench command.  Then the steady-state rank simulation.
 # usage: bash tools/gpu_round.sh TAG [workload ...]   (workload = config:camera[:baked[:method]],
 #   e.g. 1024x32:C0::3 for method 3 per-step, 1024x8:S:baked)
 #   PMC=0: bench lines and kernel traces only (profiles/traffic.json already holds
@@ -22,8 +23,7 @@ for W in $WL; do
   ARGS="--config $CFG --camera $CAM --method $MTH"; KEY="$CFG|$CAM|m$MTH"; N="${CFG}_$CAM"
   [ "$MTH" != 1 ] && N="${N}_m$MTH"
   if [ "$BK" = baked ]; then ARGS="$ARGS --baked"; KEY="$KEY|baked"; N="${N}_baked"; fi
-  timeout -k 10 600 python -u bench.py $ARGS > $O/bench_$N.log 2>&1; guard $? bench-$N $O/bench_$N.log
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o $N -- python bench.py $ARGS --no-cpu-baseline --no-issue-bounds > $O/ktrace_$N.log 2>&1; guard $? ktrace-$N $O/ktrace_$N.log
+  # PMC passes first, so the bench line of this same build carries their traffic
   if [ "${PMC:-1}" = 1 ]; then
   i=0
   for CTRS in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
@@ -31,7 +31,10 @@ for W in $WL; do
     timeout -s KILL 300 rocprofv3 --pmc $CTRS --output-format csv -d $O/pmc_$N/p$i -o p$i -- python bench.py $ARGS --no-cpu-baseline --no-issue-bounds --steps 3 --warmup 1 > $O/pmc_${N}_p$i.log 2>&1; guard $? pmc-$N-$i $O/pmc_${N}_p$i.log
   done
   PMC_TAG=$TAG python tools/pmc_traffic.py $O/traffic.json "$KEY" $O/pmc_${N}_p1.log $O/pmc_$N/p1 $O/pmc_$N/p2 $O/pmc_$N/p3 $O/pmc_$N/p4 > /dev/null || exit 1
+  TJ="--traffic-json $O/traffic.json"
   fi
+  timeout -k 10 900 python -u bench.py $ARGS ${TJ:-} > $O/bench_$N.log 2>&1; guard $? bench-$N $O/bench_$N.log
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o $N -- python bench.py $ARGS --no-cpu-baseline --no-issue-bounds > $O/ktrace_$N.log 2>&1; guard $? ktrace-$N $O/ktrace_$N.log
   echo "$N $(grep -o '"kernel": "[^"]*", "kernel_ms": [0-9.]*' $O/bench_$N.log)"
 done
 if [ "${RANKSIM:-1}" = 1 ]; then
