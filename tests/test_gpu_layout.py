@@ -177,3 +177,23 @@ def test_baked_axis_views_take_a_plane_copy(pkg, orc, gpu, tune, nb):
     assert pkg.layout_info()["resident_bytes"] == 0
     got = gpu_render(pkg, None, W, H, pkg.camera.display_inv_view((0.0, 90.0)), 1, torch)
     assert "plane" not in pkg.last_kernel()
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4, 8])
+def test_axis_copy_tiles_pitched_and_ragged(pkg, orc, gpu, tune, nb):
+    """the LDS-tiled axis copy (k_axis_copy, 32 x 32 record tiles): volumes whose x,
+    y, z are not multiples of the tile, pitched rows / slices (VR_PAD), records of
+    1-8 bins; side and top views through both copies bit-identical to the oracle"""
+    import torch
+    vol = orc.synth_volume(45, 33, 70, nb)
+    W, H = 72, 56
+    tune.set("VR_SEG_RAYS", "0")  # the one-lane march, which reads the copies
+    for pad in ("", "3,77"):
+        if pad:
+            tune.set("VR_PAD", pad)
+        for rot, kern in (((0.0, 90.0), "zrows"), ((90.0, 90.0), "yrows")):
+            m = pkg.camera.display_inv_view(rot)
+            got = gpu_render(pkg, vol, W, H, m, 1, torch)
+            assert kern in pkg.last_kernel(), (pad, rot, pkg.last_kernel())
+            assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=1))[:3],
+                          f"nb={nb} pad={pad!r} {rot}")

@@ -925,10 +925,11 @@ bool ensure_brick() {
 // that axis contiguous (axis_copy_strides) gives them what x rows give the
 // runSingleTest view -- consecutive lanes on consecutive records -- and the
 // per-ray pipelined march reads it (1024^3 x 8, yaw 90: 3.01 -> 1.63 ms,
-// DESIGN.md 4.7).  One axis copy is resident at a time (a view along the other
-// axis replaces it).  Made on the first such frame of an owned volume with
-// B <= 8 (as ensure_brick: synchronous, only with max(4 GiB, 5 %) of HBM left
-// free); VR_ZROWS=0 (vr_set_tuning) disables it.
+// DESIGN.md 4.7).  Both axis copies stay resident when the layout budget holds
+// them (vr_set_layout_budget); otherwise a view along the other axis replaces
+// the copy.  Made on the first such frame of an owned volume with B <= 8 (as
+// ensure_brick: synchronous, timed into vr_layout_info) by k_axis_copy, an
+// LDS-tiled transpose; VR_ZROWS=0 (vr_set_tuning) disables it.
 bool ensure_axis_copy(int axis) {
     if (const char *e = vr::tuning("VR_ZROWS"))
         if (std::atoi(e) == 0) return false;

@@ -15,6 +15,8 @@
 
 #include "vr_internal.h"
 
+#include <type_traits>
+
 namespace vr {
 
 // a voxel's statistic at its home position and, for x = 15 k (k > 0), in the
@@ -124,13 +126,18 @@ hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, uint64
 // an even (x, y): record (x, y, z) sits at z*bsz + (y>>1)*bsy + (x>>1)*4 +
 // (y&1)*2 + (x&1) (brick_index).  Like a cudaArray, the copy is the
 // library's own layout of the uploaded records (K:1913-1918); the quad march
-// of oblique views reads it.  One thread per record.
+// of oblique views reads it.  One thread per record, a
+// workgroup per 128 x 2 records (y pair 2 by): lanes 4q .. 4q+3 write the
+// whole line of x pair q, and each row's 128 records are read as 4 KB runs.
+// (One row per workgroup wrote every line in two halves from two workgroups:
+// 1024^3 x 8, 17.4 ms; profiles/r04/final/kernel_stats_1024x8_C1.csv.)
 __global__ __launch_bounds__(256) void k_brick8(const float *__restrict__ vol, Params P,
                                                 float *__restrict__ out, uint64_t bsy,
                                                 uint64_t bsz) {
-    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
-    if (x >= (uint32_t)P.nx) return;
-    const uint32_t y = blockIdx.y, z = blockIdx.z;
+    const uint32_t t = threadIdx.x;
+    const uint32_t x = blockIdx.x * 128u + (t >> 2) * 2u + (t & 1u);
+    const uint32_t y = blockIdx.y * 2u + ((t >> 1) & 1u), z = blockIdx.z;
+    if (x >= (uint32_t)P.nx || y >= (uint32_t)P.ny) return;
     const uint64_t src = (uint64_t)z * P.sz + (uint64_t)y * P.sy + x;
     const uint64_t dst = brick_index(x, y, z, bsy, bsz);
     const float4 *s4 = reinterpret_cast<const float4 *>(vol + src * 8);
@@ -140,32 +147,74 @@ __global__ __launch_bounds__(256) void k_brick8(const float *__restrict__ vol, P
     d4[1] = b;
 }
 
-// axis-rows copy (views along y / z): one thread per record, x-row reads coalesced
+// Axis-rows copy (views along y / z, axis_copy_strides): a transpose of x with
+// the copy's fast axis f (y or z) in every slice s of the third axis.  One
+// workgroup moves a 32 (x) x 32 (f) tile through LDS: it reads 32 x rows of 32
+// records (32*B floats contiguous each) and writes 32 f runs of 32 records, so
+// both sides are whole lines.  A record-per-thread copy wrote each record to
+// its own line (1024^3 x 8 z rows: 60.3 ms, ~1.1 TB/s of the 64 GiB moved;
+// profiles/r04/final/kernel_stats_1024x8_S.csv).  Element granularity is a
+// float4 for B >= 4, a float below; LDS rows are padded by one float4.
+constexpr int AXT = 32;
 template <int B>
-__global__ __launch_bounds__(256) void k_axis_copy(const float *__restrict__ vol, Params P,
-                                                   float *__restrict__ out, uint64_t asx,
-                                                   uint64_t asy, uint64_t asz) {
-    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
-    if (x >= (uint32_t)P.nx) return;
-    const uint32_t y = blockIdx.y, z = blockIdx.z;
-    float r[B];
-    load_rec<B>(vol, (uint64_t)z * P.sz + (uint64_t)y * P.sy + x, r);
-    float *d = out + (x * asx + y * asy + z * asz) * B;
-#pragma unroll
-    for (int i = 0; i < B; i++) d[i] = r[i];
+__global__ __launch_bounds__(256) void k_axis_copy(const float *__restrict__ vol,
+                                                   float *__restrict__ out, uint32_t nx,
+                                                   uint32_t nf, uint64_t ssf, uint64_t sss,
+                                                   uint64_t dsx, uint64_t dss, uint32_t tiles_x) {
+    using V = typename std::conditional<(B >= 4), float4, float>::type;
+    constexpr int RS = B >= 4 ? B / 4 : B;             // V slots per record
+    constexpr int PER_ROW = AXT * RS;                  // V slots of one 32-record row
+    constexpr int ROW = PER_ROW + 1;
+    __shared__ V tile[AXT * ROW];
+    const uint32_t tx = blockIdx.x % tiles_x, tf = blockIdx.x / tiles_x, s = blockIdx.y;
+    const uint32_t x0 = tx * AXT, f0 = tf * AXT;
+    const uint32_t wx = min((uint32_t)AXT, nx - x0), wf = min((uint32_t)AXT, nf - f0);
+    const V *src = reinterpret_cast<const V *>(vol);
+    V *dst = reinterpret_cast<V *>(out);
+    // read: row f of the tile = records (x0 .. x0+31, f0 + f, s), contiguous in x
+    for (int e = threadIdx.x; e < AXT * PER_ROW; e += 256) {
+        const int f = e / PER_ROW, c = e % PER_ROW;    // c = x * RS + slot
+        const uint32_t x = c / RS;
+        if ((uint32_t)f < wf && x < wx) {
+            const uint64_t rec = (uint64_t)s * sss + (uint64_t)(f0 + f) * ssf + x0;
+            tile[f * ROW + c] = src[rec * RS + c];
+        }
+    }
+    __syncthreads();
+    // write: run x of the copy = records (x0 + x, f0 .. f0+31, s), contiguous in f
+    for (int e = threadIdx.x; e < AXT * PER_ROW; e += 256) {
+        const int x = e / PER_ROW, c = e % PER_ROW;    // c = f * RS + slot
+        const uint32_t f = c / RS, k = c % RS;
+        if ((uint32_t)x < wx && f < wf) {
+            const uint64_t rec = (uint64_t)s * dss + (uint64_t)(x0 + x) * dsx + f0;
+            dst[rec * RS + c] = tile[f * ROW + x * RS + k];
+        }
+    }
 }
 
 hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint64_t asx,
                             uint64_t asy, uint64_t asz, hipStream_t s) {
-    dim3 grid;
-    if (!bake_grid(P, grid)) return hipErrorInvalidValue;
+    if (P.nx <= 0 || P.ny <= 0 || P.nz <= 0) return hipErrorInvalidValue;
+    // fast axis of the copy: stride 1 (axis_copy_strides); s = the remaining one
+    const bool zrows = asz == 1;
+    if (!(zrows || asy == 1)) return hipErrorInvalidValue;
+    const uint32_t nf = zrows ? P.nz : P.ny, ns = zrows ? P.ny : P.nz;
+    const uint64_t ssf = zrows ? P.sz : P.sy, sss = zrows ? P.sy : P.sz;
+    const uint64_t dss = zrows ? asy : asz;
+    const uint32_t tiles_x = (P.nx + AXT - 1) / AXT, tiles_f = (nf + AXT - 1) / AXT;
+    if (ns > 65535 || (uint64_t)tiles_x * tiles_f > 0x7fffffffull) return hipErrorInvalidValue;
+    const dim3 grid(tiles_x * tiles_f, ns);
+#define VR_AXC(BB)                                                                                 \
+    hipLaunchKernelGGL(k_axis_copy<BB>, grid, dim3(256), 0, s, vol, out, (uint32_t)P.nx, nf, ssf, \
+                       sss, asx, dss, tiles_x)
     switch (P.nb) {
-    case 1: hipLaunchKernelGGL(k_axis_copy<1>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
-    case 2: hipLaunchKernelGGL(k_axis_copy<2>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
-    case 4: hipLaunchKernelGGL(k_axis_copy<4>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
-    case 8: hipLaunchKernelGGL(k_axis_copy<8>, grid, dim3(256), 0, s, vol, P, out, asx, asy, asz); break;
+    case 1: VR_AXC(1); break;
+    case 2: VR_AXC(2); break;
+    case 4: VR_AXC(4); break;
+    case 8: VR_AXC(8); break;
     default: return hipErrorInvalidValue;
     }
+#undef VR_AXC
     return hipGetLastError();
 }
 
@@ -197,8 +246,8 @@ hipError_t launch_plane_axis(const float *src, uint64_t ssy, uint64_t ssz, float
 
 hipError_t launch_brick8(const float *vol, const Params &P, float *out, uint64_t bsy,
                          uint64_t bsz, hipStream_t s) {
-    dim3 grid;
-    if (!bake_grid(P, grid)) return hipErrorInvalidValue;
+    if (P.nx <= 0 || P.ny <= 0 || P.nz <= 0 || P.nz > 65535) return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)(P.nx + 127) / 128u, (uint32_t)(P.ny + 1) / 2u, (uint32_t)P.nz);
     hipLaunchKernelGGL(k_brick8, grid, dim3(256), 0, s, vol, P, out, bsy, bsz);
     return hipGetLastError();
 }
