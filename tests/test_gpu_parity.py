@@ -213,7 +213,8 @@ def test_row_aligned_coarse_volume_takes_box_march(pkg, orc, gpu, tune):
     tune.set("VR_SEG_RAYS", "1000")
     vol = orc.synth_volume(20, 18, 16, 8)
     m = pkg.camera.display_inv_view((0.0, 0.0), translation=(0.05, -0.1, 0.0))
-    for method, W, H, kern in ((1, 96, 64, "k_march<"), (2, 96, 64, "k_march<"),
+    # (8-bin mean / variance: two samples per box, k_march_duo)
+    for method, W, H, kern in ((1, 96, 64, "k_march_duo<"), (2, 96, 64, "k_march_duo<"),
                                (3, 96, 64, "k_march<"), (1, 32, 24, "k_march_segp4")):
         got = gpu_render(pkg, vol, W, H, m, method, torch)
         ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
@@ -424,6 +425,9 @@ def test_errors_do_not_exit(pkg, gpu):
     ("7", {"VR_SEG": "-2", "VR_WG_PER_CU": "3"}), ("1", {"VR_BOX_MAX": "64", "VR_WG_PER_CU": "3"}),
     ("2", {"VR_WG_PER_CU": "2"}), ("0", {"VR_WG_PER_CU": "3"}),
     ("0", {"VR_QUAD2": "1"}), ("0", {"VR_QUAD2": "1", "VR_WG_PER_CU": "1"}),
+    # K samples per footprint box (k_march_duo, m1/m2), with direct-path fallbacks
+    ("1", {"VR_DUO": "2"}), ("1", {"VR_DUO": "2", "VR_BOX_MAX": "64"}),
+    ("1", {"VR_DUO": "3"}), ("1", {"VR_DUO": "4", "VR_BOX_MAX": "64"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
@@ -441,6 +445,48 @@ def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
             got = gpu_render(pkg, None, 80, 64, cam, method, torch)
             ref = orc.render(vol, orc.make_params(80, 64, cam, query_method=method))[:3]
             assert_parity(got, ref, f"path {path} {env} nb={nb} m{method}")
+
+
+@pytest.mark.parametrize("k", ["2", "3", "4"])
+@pytest.mark.parametrize("nb", [1, 2, 8])
+def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune):
+    """k_march_duo (two samples per footprint box, mean and variance): rays ending on
+    the first or the second sample of a pair (opacity, tfar), full frames and tile
+    lists, bit-identical to the oracle (entropy: k_march)"""
+    import torch
+    tune.set("VR_PATH", "1")
+    tune.set("VR_DUO", k)
+    vol = orc.synth_volume(30, 26, 22, nb)
+    pkg.init_distribution(vol)
+    cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),
+            pkg.camera.display_inv_view((0.0, 90.0))]
+    for cam in cams:
+        for density, bright in ((0.05, 1.0), (0.6, 1.3), (3.0, 0.7)):
+            for method in (1, 2, 3):
+                got = gpu_render(pkg, None, 72, 40, cam, method, torch, density=density,
+                                 brightness=bright)
+                want = ("k_march<" if method == 3  # k_march_duo: m1 / m2
+                        else "k_march_duo<" if k == "2" else f"k_march_duo{k}<")
+                assert pkg.last_kernel().startswith(want), pkg.last_kernel()
+                ref = orc.render(vol, orc.make_params(72, 40, cam, query_method=method,
+                                                      density=density, brightness=bright))[:3]
+                assert_parity(got, ref, f"duo nb={nb} m{method} d={density}")
+    W, H, m = 72, 40, cams[0]
+    lists = pkg.tiles.tile_lists(W, H, 3, m)
+    n_slots = lists.shape[1]
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    packed = torch.full((3, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    for r in range(3):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+        assert pkg.last_kernel().startswith("k_march_duo"), pkg.last_kernel()
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, 3, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    got = frame.cpu().numpy().view(np.uint32).reshape(H, W)
+    ref8 = orc.render(vol, orc.make_params(72, 40, cams[0], query_method=1), want_float=False,
+                      want_steps=False)[0]
+    assert np.array_equal(got, ref8)
 
 
 @pytest.mark.parametrize("seg", ["2", "4", "-2", "-4"])

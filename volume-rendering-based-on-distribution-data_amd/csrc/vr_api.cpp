@@ -657,11 +657,17 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // once per wave is what the log-heavy wide decode needs (VR_BOX3=0: quad march).
     const bool wide3 = (g.nb == 16 || g.nb == 32) && d->query_method == 3 &&
                        !(vr::tuning("VR_BOX3") && std::atoi(vr::tuning("VR_BOX3")) == 0);
+    // 8-bin mean and variance there take two samples per footprint box
+    // (k_march_duo): 512^3 x 8 C0 m1 0.694 -> 0.623 ms, m2 0.571 -> 0.496; three
+    // or four per box 0.655 / 0.707; at 1024^3 (VR_PATH=1) the doubled boxes lose,
+    // 1.69 -> 2.26 (profiles/r04/variants_*_duo_r4l.log)
     if (along_rows && !d->d_tile_list && (g.nb == 8 || g.nb == 16 || g.nb == 32) &&
         (d->query_method == 1 || d->query_method == 2 || wide3) &&
         (uint64_t)d->width * d->height > seg_rays &&
-        (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
+        (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny) {
         P.path = 1;
+        P.duo = 2;
+    }
     // 32-bin records (the reference's own width) are decode-bound at any volume
     // size, and with a 16x4-pixel block per wave the box decodes each record
     // once per wave-step instead of once per touching ray: row-aligned full
@@ -700,6 +706,10 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         }
     }
     if (P.path != 2 && P.path != 7) P.axis_view = 0;  // 7: the segmented march reads the copy too
+    if (const char *e = vr::tuning("VR_DUO")) {  // 0 / 1: one sample per box, 2-4: that many
+        const int v = std::atoi(e);
+        if (v >= 0 && v <= 4) P.duo = v;
+    }
     if (const char *e = vr::tuning("VR_PATH")) {
         const int v = std::atoi(e);
         if (v == 0 || v == 1 || v == 2 || v == 4 || v == 7) {

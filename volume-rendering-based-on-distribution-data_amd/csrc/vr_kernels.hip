@@ -364,6 +364,149 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                 sw * P.brightness);
 }
 
+// ---- the LDS-box march, two samples per box (k_march_duo) ----
+// k_march decodes a footprint box for every sample; on coarse volumes (512^3 x
+// 8 at 1080p: ~4 rays per voxel, ~70 box voxels per wave-step) most of a
+// wave-step is the box's fixed cost -- six wave reductions, the box set-up,
+// the barriers -- not the decode.  Here one box covers a sample and the next
+// one of every lane (the union of both footprints; the next one only where the
+// ray reaches it by tfar, K:700-705), so those costs are paid once per two
+// samples.  The samples and their compositing are those of k_march in the same
+// order (positions advanced by the same float adds; a ray that terminates on the
+// first sample leaves the second unread): the frame is bit-identical.  Mean and
+// variance only: the entropy instance needed 190 VGPRs and a private stack, and
+// faulted at 512^3 (HSA aperture violation, profiles/r04/variants_512x8_m3_duo_fault.log).
+template <int B, int M, int K>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MINW, 8))) void k_march_duo(const float *__restrict__ vol, Params P) {
+    static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
+    static_assert(K >= 2 && K <= 4, "samples per box");
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const uint32_t slot = launch_slot(P);
+    const uint32_t tile = tile_of(P, slot);
+    if (tile == kPad) return;  // whole workgroup uniform
+    const uint32_t lane = threadIdx.x & 63u;
+    float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
+    uint32_t lx, ly;
+    if (P.wq_map) {
+        lx = (threadIdx.x >> 6) * 16u + ((threadIdx.x & 63u) >> 2);
+        ly = threadIdx.x & 3u;
+    } else {
+        tile_pixel(threadIdx.x, lx, ly);
+    }
+    const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.CW && y < P.CH;
+    const uint64_t o = P.tile_list ? (uint64_t)slot * 256u + ly * kTileW + lx
+                                   : (uint64_t)y * P.W + x;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    for (int i = 0; i < kMaxSteps; i += K) {
+        if (!wave_any(alive)) break;
+        // this sample's footprint and those of the next K - 1 the one-sample loop
+        // would take if none ends the ray (same float adds; K:700-705)
+        Foot f[K];
+        f[0] = footprint(P, px, py, pz);
+        int lo_x = alive ? f[0].x0 : 0x7FFFFFFF, lo_y = alive ? f[0].y0 : 0x7FFFFFFF;
+        int lo_z = alive ? f[0].z0 : 0x7FFFFFFF;
+        int hi_x = alive ? -f[0].x0 : 0x7FFFFFFF, hi_y = alive ? -f[0].y0 : 0x7FFFFFFF;
+        int hi_z = alive ? -f[0].z0 : 0x7FFFFFFF;
+        {
+            bool reach = alive;
+            float tq = t, qx = px, qy = py, qz = pz;
+#pragma unroll
+            for (int k = 1; k < K; k++) {
+                tq = tq + kTStep;
+                reach = reach && !(tq > r.tfar) && i + k < kMaxSteps;
+                qx = qx + stx;
+                qy = qy + sty;
+                qz = qz + stz;
+                f[k] = footprint(P, qx, qy, qz);
+                if (reach) {
+                    lo_x = min(lo_x, f[k].x0);
+                    lo_y = min(lo_y, f[k].y0);
+                    lo_z = min(lo_z, f[k].z0);
+                    hi_x = min(hi_x, -f[k].x0);
+                    hi_y = min(hi_y, -f[k].y0);
+                    hi_z = min(hi_z, -f[k].z0);
+                }
+            }
+        }
+        dpp_min3(lo_x, lo_y, lo_z);
+        dpp_min3(hi_x, hi_y, hi_z);
+        const int bx0 = lo_x, by0 = lo_y, bz0 = lo_z;
+        // x1 = min(x0 + 1, n - 1) except at the low clamp: a superset of the upper corners
+        const int bx1 = min(-hi_x + 1, P.nx - 1);
+        const int by1 = min(-hi_y + 1, P.ny - 1);
+        const int bz1 = min(-hi_z + 1, P.nz - 1);
+        const int dx = bx1 - bx0 + 1, dy = by1 - by0 + 1, dz = bz1 - bz0 + 1;
+        const bool staged = dx * dy * dz <= P.box_max;  // wave-uniform
+        const int dxy = dx * dy;
+        if (staged) {
+            const float *vbase =
+                vol + ((uint64_t)bz0 * P.sz + (uint64_t)by0 * P.sy + (uint64_t)bx0) * (uint64_t)B;
+            decode_box<B, M>(vbase, P, box, dx, dxy, dxy * dz, lane, nullptr, nullptr);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            // alive here: the ray reached this sample (t <= tfar), so f[k] is in the box
+            if (alive) {
+                const Foot &fk = f[k];
+                float sample;
+                if (staged) {
+                    const int b0 = ((fk.z0 - bz0) * dy + (fk.y0 - by0)) * dx + (fk.x0 - bx0);
+                    const int ox = fk.x1 - fk.x0, oy = (fk.y1 - fk.y0) * dx;
+                    const int oz = (fk.z1 - fk.z0) * dxy;
+                    float sv[8];
+                    sv[0] = box[b0];
+                    sv[1] = box[b0 + ox];
+                    sv[2] = box[b0 + oy];
+                    sv[3] = box[b0 + oy + ox];
+                    sv[4] = box[b0 + oz];
+                    sv[5] = box[b0 + oz + ox];
+                    sv[6] = box[b0 + oz + oy];
+                    sv[7] = box[b0 + oz + oy + ox];
+                    sample = blend8(sv, fk);
+                } else {
+                    sample = sample_direct<B, M>(vol, P, fk);
+                }
+                n = i + k + 1;
+                if (composite(P, sample, sx, sy, sz, sw)) {
+                    alive = false;
+                } else {
+                    t = t + kTStep;
+                    if (t > r.tfar || i + k + 1 >= kMaxSteps) {
+                        alive = false;
+                    } else {
+                        px = px + stx;
+                        py = py + sty;
+                        pz = pz + stz;
+                    }
+                }
+            }
+        }
+        if (staged) {  // the slice is rewritten next step: keep these reads ahead of it
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    if (!valid) return;
+    if (n == 0) {  // miss (K:302-303): nothing written
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 __device__ __forceinline__ int wave_incl_scan(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
@@ -2549,6 +2692,25 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         // (profiles/r03/box_map.log); VR_BOX_MAP=0 keeps the rows
         P.wq_map = 1;
         if (const char *em = tuning("VR_BOX_MAP")) P.wq_map = std::atoi(em) != 0;
+    }
+    if constexpr (!COUNT && B > 0 && B <= 8) {
+        // mean and variance: P.duo samples per footprint box (k_march_duo;
+        // fill_params: coarse row-aligned 8-bin full frames, VR_DUO)
+        const int k = P.duo;
+        if (k >= 2 && k <= 4 && (method == 1 || method == 2) && P.box_max > 0) {
+            note_kernel(k == 2 ? "k_march_duo" : k == 3 ? "k_march_duo3" : "k_march_duo4", B, method);
+#define VR_DUO_L(MM, KK) hipLaunchKernelGGL((k_march_duo<B, MM, KK>), grid, block, lds, s, vol, P)
+            switch (k * 4 + method) {
+            case 9: VR_DUO_L(1, 2); break;
+            case 10: VR_DUO_L(2, 2); break;
+            case 13: VR_DUO_L(1, 3); break;
+            case 14: VR_DUO_L(2, 3); break;
+            case 17: VR_DUO_L(1, 4); break;
+            case 18: VR_DUO_L(2, 4); break;
+            }
+#undef VR_DUO_L
+            return hipGetLastError();
+        }
     }
     switch (method) {
     case 0:

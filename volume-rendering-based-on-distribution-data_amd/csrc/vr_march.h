@@ -124,6 +124,27 @@ __device__ __forceinline__ int dpp_min(int v, int ident) {
 __device__ __forceinline__ int wave_min(int v) { return dpp_min(v, 0x7FFFFFFF); }
 __device__ __forceinline__ int wave_max(int v) { return -dpp_min(-v, 0x7FFFFFFF); }
 
+// three wave minima at once: each DPP level is issued for the three values back
+// to back, so the DPP read-after-write hazard of one chain is covered by the
+// other two instead of by s_nop wait states
+__device__ __forceinline__ void dpp_min3(int &a, int &b, int &c) {
+    constexpr int I = 0x7FFFFFFF;
+#define VR_DPP3(CTRL, ROWM)                                                  \
+    a = min(a, __builtin_amdgcn_update_dpp(I, a, CTRL, ROWM, 0xF, false));   \
+    b = min(b, __builtin_amdgcn_update_dpp(I, b, CTRL, ROWM, 0xF, false));   \
+    c = min(c, __builtin_amdgcn_update_dpp(I, c, CTRL, ROWM, 0xF, false));
+    VR_DPP3(0x111, 0xF)
+    VR_DPP3(0x112, 0xF)
+    VR_DPP3(0x114, 0xF)
+    VR_DPP3(0x118, 0xF)
+    VR_DPP3(0x142, 0xA)
+    VR_DPP3(0x143, 0xC)
+#undef VR_DPP3
+    a = __builtin_amdgcn_readlane(a, 63);
+    b = __builtin_amdgcn_readlane(b, 63);
+    c = __builtin_amdgcn_readlane(c, 63);
+}
+
 __device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0; }
 
 // Corners of one sample (K:601 texture footprint): texel indices + 8-bit weights.
