@@ -221,26 +221,58 @@ hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint6
 // Axis copy of one baked plane (views whose screen x runs along the volume's y
 // or z): the plane's 16 x 2 x 1 bricks with that axis in the
 // brick rows -- axis 1: y rows (y fast, x pairs, z slices), axis 2: z rows (z
-// fast, y pairs, x slices); gather8 MODE 4 / 5 reads it.  One thread per
-// voxel, grid over (fast, pair, slow) of the copy so its writes are coalesced.
+// fast, y pairs, x slices); gather8 MODE 4 / 5 reads it.  A workgroup moves a
+// tile of 30 x by 30 f (the copy's fast axis; 30 = two bricks' home runs) --
+// for axis 2 by a y pair, for axis 1 in one z slice -- through LDS: it reads
+// whole source bricks (x runs) and writes whole copy bricks (f runs), the
+// apron voxel of each copy brick included (put_plane).  One voxel per thread
+// with the grid over the copy's order read the source across its lines
+// (1024^3 z rows: 20.6 ms for 8 GiB moved; profiles/r04/final/bench_1024x8_S_baked.json).
+constexpr int PLT = 30;
 __global__ __launch_bounds__(256) void k_plane_axis(const float *__restrict__ src, uint64_t ssy,
                                                     uint64_t ssz, float *__restrict__ out,
-                                                    uint64_t dsy, uint64_t dsz, uint32_t nfast,
-                                                    int axis) {
-    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
-    if (f >= nfast) return;
-    const uint32_t p = blockIdx.y, s = blockIdx.z;
-    const uint32_t x = axis == 2 ? s : p, y = axis == 2 ? p : f, z = axis == 2 ? f : s;
-    put_plane(out, f, p, s, dsy, dsz, src[plane_index(x, y, z, ssy, ssz)]);
+                                                    uint64_t dsy, uint64_t dsz, uint32_t nx,
+                                                    uint32_t ny, uint32_t nz, int axis,
+                                                    uint32_t tiles_x) {
+    constexpr int XP = PLT + 1;                           // padded x extent in LDS
+    __shared__ float tile[2 * PLT * XP];                  // [o][f][x], o: the y pair (axis 2)
+    const uint32_t nf = axis == 2 ? nz : ny;
+    const uint32_t x0 = (blockIdx.x % tiles_x) * PLT, f0 = (blockIdx.x / tiles_x) * PLT;
+    const uint32_t no = axis == 2 ? 2u : 1u;              // y rows (axis 2) / z slices (axis 1)
+    const uint32_t o0 = blockIdx.y * no;                  // first y (axis 2) / the z (axis 1)
+    const uint32_t wx = min((uint32_t)PLT, nx - x0), wf = min((uint32_t)PLT, nf - f0);
+    const uint32_t wo = min(no, (axis == 2 ? ny : nz) - o0);
+    for (uint32_t e = threadIdx.x; e < no * PLT * PLT; e += 256) {
+        const uint32_t xi = e % PLT, fi = (e / PLT) % PLT, oi = e / (PLT * PLT);
+        if (xi < wx && fi < wf && oi < wo) {
+            const uint32_t x = x0 + xi, f = f0 + fi, o = o0 + oi;
+            const uint32_t y = axis == 2 ? o : f, z = axis == 2 ? f : o;
+            tile[(oi * PLT + fi) * XP + xi] = src[plane_index(x, y, z, ssy, ssz)];
+        }
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < no * PLT * PLT; e += 256) {
+        const uint32_t fi = e % PLT, xi = (e / PLT) % PLT, oi = e / (PLT * PLT);
+        if (xi < wx && fi < wf && oi < wo) {
+            const uint32_t x = x0 + xi, f = f0 + fi, o = o0 + oi;
+            // copy coordinates (fast, pair, slow): axis 2 (z, y, x), axis 1 (y, x, z)
+            const uint32_t pp = axis == 2 ? o : x, ss = axis == 2 ? x : o;
+            put_plane(out, f, pp, ss, dsy, dsz, tile[(oi * PLT + fi) * XP + xi]);
+        }
+    }
 }
 
 hipError_t launch_plane_axis(const float *src, uint64_t ssy, uint64_t ssz, float *out,
                              uint64_t dsy, uint64_t dsz, int nx, int ny, int nz, int axis,
                              hipStream_t s) {
-    const uint32_t nf = axis == 2 ? nz : ny, np = axis == 2 ? ny : nx, ns = axis == 2 ? nx : nz;
-    if (nf == 0 || np == 0 || ns == 0 || np > 65535 || ns > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_plane_axis, dim3((nf + 255) / 256, np, ns), dim3(256), 0, s, src, ssy,
-                       ssz, out, dsy, dsz, nf, axis);
+    if (nx <= 0 || ny <= 0 || nz <= 0 || (axis != 1 && axis != 2) || nx >= 65536 ||
+        ny >= 65536 || nz >= 65536)
+        return hipErrorInvalidValue;
+    const uint32_t nf = axis == 2 ? nz : ny;
+    const uint32_t tiles_x = (nx + PLT - 1) / PLT, tiles_f = (nf + PLT - 1) / PLT;
+    const uint32_t gy = axis == 2 ? (uint32_t)(ny + 1) / 2u : (uint32_t)nz;
+    hipLaunchKernelGGL(k_plane_axis, dim3(tiles_x * tiles_f, gy), dim3(256), 0, s, src, ssy, ssz,
+                       out, dsy, dsz, (uint32_t)nx, (uint32_t)ny, (uint32_t)nz, axis, tiles_x);
     return hipGetLastError();
 }
 
