@@ -31,6 +31,8 @@ def main():
                          "on the same lists, so variants share one process and one GPU state")
     ap.add_argument("--worlds", default="2,4,8")
     ap.add_argument("--modes", default="est,cost")
+    ap.add_argument("--blocks", default="1x4",
+                    help="cost-dealing block shapes (tiles, WxH) to compare, e.g. 1x4,2x4,4x4")
     ap.add_argument("--host-ms", type=float, default=0.0,
                     help="per-frame host issue cost of the N > 1 frame loop (tools/host_cost.py); "
                          "reported as a second, conservative speed-up with it added")
@@ -84,13 +86,15 @@ def main():
     pkg.render(pkg.make_desc(full, W, H, m, query_method=args.method, d_steps=steps))
     cost = pkg.tiles.tile_costs_from_frame(steps.cpu().numpy(), W, H)
     worlds = [int(w) for w in args.worlds.split(",")]
-    modes = [(md, w) for md in args.modes.split(",") for w in worlds]
+    blocks = [tuple(int(v) for v in b.split("x")) for b in args.blocks.split(",")]
+    modes = [(md, w, bl) for md in args.modes.split(",") for w in worlds
+             for bl in (blocks if md == "cost" else [None])]
     envs = args.envs if args.envs is not None else [args.env]
-    for mode, world in modes:
+    for mode, world, bl in modes:
         if mode == "est":
             lists = pkg.tiles.tile_lists(W, H, world, None if args.no_lpt else m)
         else:
-            lists = pkg.tiles.tile_lists_by_cost(W, H, world, cost)
+            lists = pkg.tiles.tile_lists_by_cost(W, H, world, cost, block=bl)
         slots = lists.shape[1]
         packed = torch.zeros((world, slots * 256), dtype=torch.int32, device="cuda")
         dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
@@ -110,7 +114,8 @@ def main():
             ok = torch.equal(frame, full)
             host = (f"  + host {args.host_ms:.3f} -> {t1 / (max(per) + tu + args.host_ms):.2f}x"
                     if args.host_ms > 0 else "")
-            print(f"  {mode:4s} N={world} [{spec or 'defaults'}] {kern}: per-rank ms "
+            tag = mode if bl is None or bl == (1, 4) else f"{mode} {bl[0]}x{bl[1]}"
+            print(f"  {tag:4s} N={world} [{spec or 'defaults'}] {kern}: per-rank ms "
                   f"{' '.join(f'{x:.3f}' for x in per)}  max {max(per):.3f}"
                   f"  unscatter {tu:.3f}  -> est. speedup {t1 / (max(per) + tu):.2f}x{host}"
                   f"  frame {'identical' if ok else 'DIFFERS'}", flush=True)

@@ -154,7 +154,8 @@ def tile_costs_from_frame(steps, width: int, height: int) -> np.ndarray:
     return tile_costs_from_steps(packed, np.arange(tx * ty, dtype=np.uint32), tx * ty)
 
 
-def tile_lists_by_cost(width: int, height: int, world_size: int, cost) -> np.ndarray:
+def tile_lists_by_cost(width: int, height: int, world_size: int, cost,
+                       block=(BLOCK_X, BLOCK_Y)) -> np.ndarray:
     """Like tile_lists, but dealt by measured per-tile costs (tile_costs_from_steps
     summed over the ranks of a previous frame of the same view).
 
@@ -166,11 +167,12 @@ def tile_lists_by_cost(width: int, height: int, world_size: int, cost) -> np.nda
     Each rank's 8 XCD sublists are PAD-padded to one length before they are
     interleaved, so list entry 8*k + g is always the k-th tile of XCD g."""
     tx, ty = tiles_x(width), tiles_y(height)
+    BX, BY = int(block[0]), int(block[1])  # tiles per block (tooling sweeps other shapes)
     cost = np.asarray(cost, dtype=np.int64).reshape(ty, tx)
-    nbx, nby = (tx + BLOCK_X - 1) // BLOCK_X, (ty + BLOCK_Y - 1) // BLOCK_Y
-    pad = np.zeros((nby * BLOCK_Y, nbx * BLOCK_X), dtype=np.int64)
+    nbx, nby = (tx + BX - 1) // BX, (ty + BY - 1) // BY
+    pad = np.zeros((nby * BY, nbx * BX), dtype=np.int64)
     pad[:ty, :tx] = cost
-    bcost = pad.reshape(nby, BLOCK_Y, nbx, BLOCK_X).sum(axis=(1, 3)).reshape(-1)
+    bcost = pad.reshape(nby, BY, nbx, BX).sum(axis=(1, 3)).reshape(-1)
     nbins = XCDS * world_size
     # every bin ends with lo or lo + 1 blocks, exactly `extra` of them with lo + 1
     lo, extra = divmod(len(bcost), nbins)
@@ -194,8 +196,8 @@ def tile_lists_by_cost(width: int, height: int, world_size: int, cost) -> np.nda
             lst = []
             for b in members[g * world_size + r]:
                 by, bx = divmod(b, nbx)
-                for y in range(by * BLOCK_Y, min(ty, by * BLOCK_Y + BLOCK_Y)):
-                    for x in range(bx * BLOCK_X, min(tx, bx * BLOCK_X + BLOCK_X)):
+                for y in range(by * BY, min(ty, by * BY + BY)):
+                    for x in range(bx * BX, min(tx, bx * BX + BX)):
                         lst.append(y * tx + x)
             lists.append(lst)
         longest = max(len(l) for l in lists)
