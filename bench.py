@@ -68,6 +68,9 @@ def parse():
                     help="skip the untimed one-tile latency probe (roofline.compute): "
                          "profiling runs use it so a kernel's rocprofv3 average holds only "
                          "whole-frame launches")
+    ap.add_argument("--render-streams", type=int, default=0, choices=[0, 1, 2],
+                    help="N > 1: render streams consecutive frames alternate over "
+                         "(0 = default: 2 at N > 1; N = 1 always 1)")
     ap.add_argument("--no-balance", action="store_true",
                     help="N > 1: keep the estimate-dealt tile lists (no measured-cost re-deal)")
     ap.add_argument("--dump-frame", default="",
@@ -568,6 +571,17 @@ def main():
     # 0.2150 every 8th (ring 8), against 0.1984 without gather and assembly
     # (tools/host_cost.py, profiles/r04/host_cost_N8_r4h.log).
     RING = 8 if world > 1 else 1
+    # N > 1: consecutive frames alternate over two render streams, so a frame's
+    # launch can start while the previous one drains its last waves (the frames
+    # are independent: their own ring buffers; the gathers wait on their frame's
+    # stream).  Rank lists are short launches whose ramp and tail are a larger
+    # share: one rank's frame period at N = 8, C0 0.196 -> 0.186 ms, C1 0.449 ->
+    # 0.412, side view 0.242 -> 0.219 (tools/overlap_sim.py,
+    # profiles/r04/overlap_*_r4u.log).  N = 1 keeps one stream: its per-frame
+    # HIP events time each launch alone for the roofline.
+    NSTREAMS = args.render_streams if args.render_streams else (2 if world > 1 else 1)
+    if world == 1:
+        NSTREAMS = 1
     with torch.cuda.stream(stream):
         if world > 1:
             packed = [torch.zeros(n_slots * 256, dtype=torch.int32, device=dev) for _ in range(RING)]
@@ -582,6 +596,7 @@ def main():
     desc = descs[0]
     torch.cuda.synchronize()
     assemble = torch.cuda.Stream(device=dev) if world > 1 else None
+    render_streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(NSTREAMS - 1)]
     works, assembled = [None] * RING, [None] * RING
 
     # algorithmic bytes of one launch on this rank: the volume bytes
@@ -619,21 +634,27 @@ def main():
 
     def step(timed):
         b = nframe[0] % RING
+        rs = render_streams[nframe[0] % NSTREAMS]
         nframe[0] += 1
-        with torch.cuda.stream(stream):
+        if NSTREAMS > 1:
+            pkg.set_stream(rs)  # the library launches this frame on its stream
+        if world > 1 and (nframe[0] - 1) % RING == 0 and nframe[0] > 1:
+            # once per RING frames, on the newest gather and assembly (their
+            # streams run in order, so this covers the older ones): the next
+            # RING frames reuse buffers whose gathers and assemblies (frames
+            # f - RING .. f - 1) are then done.  One wait per frame cost the
+            # loop more (tools/host_cost.py).  Every render stream
+            # waits: the next RING frames use all of them.
+            w = (nframe[0] - 2) % RING
+            for s_ in render_streams:
+                with torch.cuda.stream(s_):
+                    if works[w] is not None:
+                        works[w].wait()
+                    if assembled[w] is not None:
+                        s_.wait_event(assembled[w])
+        with torch.cuda.stream(rs):
             if world == 1:
                 frame.zero_()  # C:208 (tile slots need none: misses are written as 0)
-            elif (nframe[0] - 1) % RING == 0 and nframe[0] > 1:
-                # once per RING frames, on the newest gather and assembly (their
-                # streams run in order, so this covers the older ones): the next
-                # RING frames reuse buffers whose gathers and assemblies (frames
-                # f - RING .. f - 1) are then done.  One wait per frame cost the
-                # loop more (tools/host_cost.py)
-                w = (nframe[0] - 2) % RING
-                if works[w] is not None:
-                    works[w].wait()
-                if assembled[w] is not None:
-                    stream.wait_event(assembled[w])
             # per-frame timing events only at N = 1: between the render, the gather
             # and the assembly streams of N > 1 they cost the frame loop ~0.1 ms per
             # frame (tools/host_cost.py); N > 1 times its renders after the loop
@@ -641,10 +662,10 @@ def main():
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
+                e0.record(rs)
             pkg.render(descs[b])
             if timed:
-                e1.record(stream)
+                e1.record(rs)
                 ev.append((e0, e1))
             if world > 1:
                 works[b] = pkg.tiles.gather_packed_into(packed[b], recv[b], world, rank)
@@ -653,7 +674,7 @@ def main():
                 works[b].wait()
                 pkg.set_stream(assemble)
                 pkg.unscatter_tiles(recv[b], all_lists, world, n_slots, frame, W, H)
-                pkg.set_stream(stream)
+                pkg.set_stream(rs)
                 done = torch.cuda.Event()
                 done.record(assemble)
                 assembled[b] = done
@@ -681,6 +702,7 @@ def main():
                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    pkg.set_stream(stream)  # (N > 1: the loop left the library on the last frame's stream)
     if world > 1:
         # this rank's render alone (untimed, after the loop): HIP events around 5
         # renders of its list; the line reports the max over ranks
@@ -779,6 +801,7 @@ def main():
                                if args.baked else "decoded from the records at every step"),
                 "bake_ms": round(bake_ms, 3) if bake_ms is not None else None,
                 "layout_copies": layout,
+                "render_streams": NSTREAMS,
                 "tile_deal": (None if world == 1 else "estimate" if args.no_balance
                               else "measured cost (one untimed frame)"),
                 "parallelism": f"image tiles x{world}" + (

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--port", default="29533")
     ap.add_argument("--env", default="", help="tuning knobs NAME=VALUE[,...] for the live loop")
+    ap.add_argument("--streams-only", action="store_true",
+                    help="only the ring-8 loop on one vs two alternating render streams")
     ap.add_argument("--priority", type=int, default=0,
                     help="torch stream priority of the render stream (-1 = high)")
     args = ap.parse_args()
@@ -83,30 +85,37 @@ def main():
     works, assembled, ev = [None] * 8, [None] * 8, []
     nframe = [0]
 
+    render_streams = [stream, torch.cuda.Stream(device=dev, priority=args.priority)]
+
     def step(events=False, gather=True, unscatter=True, ring=4, mode="nccl", on_render=False,
-             every=1):
+             every=1, streams=1):
         # bench.py step(), N > 1, rank 0.  mode: "nccl" the gather on the one-rank
         # group, "copy" a device copy on the assembly stream instead; on_render: the
-        # unscatter of the previous frame on the render stream after this render
+        # unscatter of the previous frame on the render stream after this render;
+        # streams: consecutive frames alternate over that many render streams
         f = nframe[0]
         b = f % ring
         nframe[0] += 1
-        with torch.cuda.stream(stream):
-            # every: wait once per `every` frames, on the newest gather / assembly
-            # (the NCCL and assembly streams are in order, so that covers the
-            # older ones; needs ring >= every)
-            w = b if every == 1 else ((f - 1) % ring if f % every == 0 else None)
-            if w is not None and works[w] is not None:
-                works[w].wait()
-            if w is not None and assembled[w] is not None:
-                stream.wait_event(assembled[w])
+        rs = render_streams[f % streams]
+        pkg.set_stream(rs)
+        # every: wait once per `every` frames, on the newest gather / assembly
+        # (the NCCL and assembly streams are in order, so that covers the
+        # older ones; needs ring >= every), on every render stream
+        w = b if every == 1 else ((f - 1) % ring if f % every == 0 else None)
+        for s in (render_streams[:streams] if every > 1 else [rs]):
+            with torch.cuda.stream(s):
+                if w is not None and works[w] is not None:
+                    works[w].wait()
+                if w is not None and assembled[w] is not None:
+                    s.wait_event(assembled[w])
+        with torch.cuda.stream(rs):
             if events:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
+                e0.record(rs)
             pkg.render(descs[b])
             if events:
-                e1.record(stream)
+                e1.record(rs)
                 ev.append((e0, e1))
             works[b] = (dist.gather(packed[b], gather_list=list(recv1[b].unbind(0)), dst=0,
                                     async_op=True) if gather and mode == "nccl" else None)
@@ -114,7 +123,7 @@ def main():
                 pkg.unscatter_tiles(recvN, all_lists, N, slots, frame, W, H)
         if gather and mode == "copy":
             ev_r = torch.cuda.Event()
-            ev_r.record(stream)
+            ev_r.record(rs)
             with torch.cuda.stream(assemble):
                 assemble.wait_event(ev_r)
                 recv1[b][0].copy_(packed[b])
@@ -124,7 +133,7 @@ def main():
                     works[b].wait()
                 pkg.set_stream(assemble)
                 pkg.unscatter_tiles(recvN, all_lists, N, slots, frame, W, H)
-                pkg.set_stream(stream)
+                pkg.set_stream(rs)
                 done = torch.cuda.Event()
                 done.record(assemble)
                 assembled[b] = done
@@ -167,9 +176,34 @@ def main():
     print(f"  host calls alone: vr_render {t_render:.4f} ms (no launch), dist.gather {t_gather:.4f} ms, "
           f"unscatter {t_unsc:.4f} ms", flush=True)
     pkg.set_tuning("VR_DRY", "0")
-    for kw in ({}, {"every": 4}, {"every": 8, "ring": 8}, {"mode": "copy"}, {"unscatter": False},
-               {"gather": False}, {"gather": False, "unscatter": False},
-               {"events": True, "gather": False, "unscatter": False}):
+    variants = ({}, {"every": 4}, {"every": 8, "ring": 8}, {"mode": "copy"}, {"unscatter": False},
+                {"gather": False}, {"gather": False, "unscatter": False},
+                {"events": True, "gather": False, "unscatter": False})
+    if args.streams_only:
+        variants = ()
+    variants += ({"every": 8, "ring": 8}, {"every": 8, "ring": 8, "streams": 2},
+                 {"every": 8, "ring": 8, "gather": False, "unscatter": False},
+                 {"every": 8, "ring": 8, "streams": 2, "gather": False, "unscatter": False})
+    # the steady full frame (one GPU, one stream, zeroed output as bench.py N = 1)
+    # in the same process, for loop speed-ups full frame / frame period
+    fdesc = pkg.make_desc(frame, W, H, m, query_method=args.method)
+
+    def full_frame():
+        with torch.cuda.stream(stream):
+            frame.zero_()
+            pkg.render(fdesc)
+    pkg.set_stream(stream)
+    for _ in range(40):
+        full_frame()
+    t_full = each(full_frame, 100)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(100):
+        full_frame()
+    torch.cuda.synchronize()
+    t_full = (time.perf_counter() - t0) * 10.0
+    print(f"  full frame (N = 1 loop, {pkg.last_kernel()}): period {t_full:.4f} ms", flush=True)
+    for kw in variants:
         works[:] = [None] * 8
         assembled[:] = [None] * 8
         ev.clear()
@@ -184,8 +218,8 @@ def main():
                   f"{period:.4f} ms, render (HIP events) {kern:.4f} ms, median gap between renders "
                   f"{gap:.4f} ms", flush=True)
         else:
-            print(f"  live [{what}]: host issue {issue:.4f} ms/frame, frame period {period:.4f} ms",
-                  flush=True)
+            print(f"  live [{what}]: host issue {issue:.4f} ms/frame, frame period {period:.4f} ms"
+                  f"  (full frame / period = {t_full / period:.2f}x)", flush=True)
     dist.destroy_process_group()
 
 
