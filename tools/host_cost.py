@@ -85,7 +85,8 @@ def main():
     works, assembled, ev = [None] * 8, [None] * 8, []
     nframe = [0]
 
-    render_streams = [stream, torch.cuda.Stream(device=dev, priority=args.priority)]
+    render_streams = [stream] + [torch.cuda.Stream(device=dev, priority=args.priority)
+                                 for _ in range(3)]
 
     def step(events=False, gather=True, unscatter=True, ring=4, mode="nccl", on_render=False,
              every=1, streams=1):
@@ -182,6 +183,7 @@ def main():
     if args.streams_only:
         variants = ()
     variants += ({"every": 8, "ring": 8}, {"every": 8, "ring": 8, "streams": 2},
+                 {"every": 8, "ring": 8, "streams": 3}, {"every": 8, "ring": 8, "streams": 4},
                  {"every": 8, "ring": 8, "gather": False, "unscatter": False},
                  {"every": 8, "ring": 8, "streams": 2, "gather": False, "unscatter": False})
     # the steady full frame (one GPU, one stream, zeroed output as bench.py N = 1)
