@@ -949,8 +949,9 @@ def test_quad_march_brick_layout(pkg, orc, gpu, dims, brick, tune):
     ((40, 36, 32), 8, 256, 200, "k_march_segp4<")])
 def test_small_frames_take_segmented_march(pkg, orc, gpu, dims, nb, W, H, want):
     """small full frames run the pipelined ray-segmented march: 4 lanes per ray up to
-    128 K rays; oblique views (B < 8) 4 lanes up to 400 K (round 4), 2 up to 700 K,
-    row-aligned ones one lane above 128 K; bit-identical"""
+    128 K rays; oblique views (B < 8) 4 lanes up to 400 K (round 4), 2 up to 700 K;
+    row-aligned 4- and 8-bin frames above 128 K rays of a coarse volume take the box
+    march with four samples per box (k_march_duo4, round 4); bit-identical"""
     import torch
     vol = orc.synth_volume(*dims, nb)
     pkg.init_distribution(vol)
@@ -960,10 +961,31 @@ def test_small_frames_take_segmented_march(pkg, orc, gpu, dims, nb, W, H, want):
             ref = orc.render(vol, orc.make_params(W, H, cam, query_method=method))[:3]
             assert_parity(got, ref, f"{dims}x{nb} {W}x{H} m{method}")
             rows = abs(float(cam[0])) >= 0.95
-            k = want or ("k_march_pipe<" if rows else
+            k = want or ("k_march_duo4<" if rows else
                          "k_march_segp4<" if W * H <= 400000 else "k_march_segp2<")
             if nb < 8 or rows:
                 assert pkg.last_kernel().startswith(k), pkg.last_kernel()
+
+
+@pytest.mark.parametrize("nb,want", [(2, "k_march_pipe<"), (4, "k_march_duo4<"),
+                                     (8, "k_march_duo4<")])
+def test_midsize_rows_take_box_march_with_four_samples(pkg, orc, gpu, nb, want):
+    """row-aligned full frames between 128 K and 700 K rays of a volume with >= 4
+    pixels per voxel face (BASELINE config 2's shape): 4 and 8 bins, methods 1/2, on
+    k_march_duo with four samples per box, 2 bins on the one-lane march; entropy on
+    k_march; rays ending on any sample of a box; bit-identical"""
+    import torch
+    vol = orc.synth_volume(44, 38, 30, nb)
+    pkg.init_distribution(vol)
+    W, H = 400, 360
+    m = pkg.camera.single_test_inv_view()
+    for method, density in ((1, 0.05), (2, 0.05), (1, 2.5), (2, 0.8), (3, 0.05)):
+        got = gpu_render(pkg, None, W, H, m, method, torch, density=density)
+        ref = orc.render(vol, orc.make_params(W, H, m, query_method=method, density=density))[:3]
+        assert_parity(got, ref, f"nb={nb} m{method} d={density}")
+        k = want if method != 3 else ("k_march<" if nb == 8 else "k_march_ws<")
+        if method != 3 or nb == 8:
+            assert pkg.last_kernel().startswith(k), (method, pkg.last_kernel())
 
 
 def test_environment_does_not_change_the_kernel(pkg, orc, gpu, monkeypatch):

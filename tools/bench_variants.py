@@ -40,7 +40,12 @@ def main():
     import __graft_entry__ as g
     import bench
     pkg = g.load_package()
-    n, nb, W, H = bench.CONFIGS[args.config]
+    if args.config in bench.CONFIGS:
+        n, nb, W, H = bench.CONFIGS[args.config]
+    else:  # ad-hoc shape for sweeps: N x B @ W x H, e.g. 256x8@512x512
+        vol, img = args.config.split("@")
+        n, nb = (int(v) for v in vol.split("x"))
+        W, H = (int(v) for v in img.split("x"))
     paths = {"main": pkg.LIB_PATH}
     for p in sorted(glob.glob(os.path.join(ROOT, "tools/build/variants/*/libvr.so"))):
         paths[os.path.basename(os.path.dirname(p))] = p

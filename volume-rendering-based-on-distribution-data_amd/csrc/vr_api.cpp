@@ -683,13 +683,30 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     if (along_rows && !d->d_tile_list && g.nb == 16 && d->query_method == 3 &&
         (uint64_t)d->width * d->height > seg_rays)
         P.path = 1;
+    // Mid-size row-aligned full frames of such a coarse volume (more rays than the
+    // small-frame threshold below, fewer than the segmented one: BASELINE config 2,
+    // 256^3 x 4 at 512^2): a round of 4 waves per SIMD whose per-step overheads
+    // dominate, so the box march with four samples per box (k_march_duo) beats the
+    // one-lane march for 4 and 8 bins: 256^3 x 4 C0 m1 0.129 -> 0.105 ms, m2 0.104
+    // -> 0.076; 256^3 x 8 at 512^2 m1 0.271 -> 0.245, m2 0.240 -> 0.144; 384^3 x 4 at
+    // 768^2 m1 0.197 -> 0.198, m2 0.176 -> 0.137; 2 bins lose (m2 0.188 -> 0.213)
+    // (profiles/r04/variants_midsize_duo_r4ad.log)
+    {
+        const uint64_t rays = (uint64_t)d->width * d->height;
+        if (along_rows && !d->d_tile_list && !codec && !flex && (g.nb == 4 || g.nb == 8) &&
+            (d->query_method == 1 || d->query_method == 2) && rays > 131072 &&
+            rays <= seg_rays && rays >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny) {
+            P.path = 1;
+            P.duo = 4;
+        }
+    }
     // Small full frames (BASELINE configs 1 and 2: 128^3 x 1 at 256^2, 256^3 x 4
     // at 512^2) cannot fill the GPU with one ray per lane, so the per-ray step
     // chain sets the time, as for a rank's tile list: the pipelined
     // ray-segmented march, 4 lanes per ray up to 128 K rays, else 2.  Measured
     // (profiles/r02/small_frames.log): 128^3 x 1 C0 0.136 -> 0.082 ms, C1
-    // 0.180 -> 0.093; 256^3 x 4 C1 0.224 -> 0.147, while its row-aligned view
-    // (262 K rays) stays on the one-lane march (0.136 vs 0.139).  Oblique views
+    // 0.180 -> 0.093; 256^3 x 4 C1 0.224 -> 0.147 (its row-aligned view, 262 K
+    // rays, takes the box march above).  Oblique views
     // of 8-bin volumes keep the quad march (as for oblique rank lists).
     int small_seg = 0;
     {
