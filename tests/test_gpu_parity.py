@@ -973,7 +973,8 @@ def test_midsize_rows_take_box_march_with_four_samples(pkg, orc, gpu, nb, want):
     """row-aligned full frames between 128 K and 700 K rays of a volume with >= 4
     pixels per voxel face (BASELINE config 2's shape): 4 and 8 bins, methods 1/2, on
     k_march_duo with four samples per box, 2 bins on the one-lane march; entropy on
-    k_march; rays ending on any sample of a box; bit-identical"""
+    k_march (the 2-bin frame too, round 4's small-frame entropy rule); rays ending on
+    any sample of a box; bit-identical"""
     import torch
     vol = orc.synth_volume(44, 38, 30, nb)
     pkg.init_distribution(vol)
@@ -983,9 +984,27 @@ def test_midsize_rows_take_box_march_with_four_samples(pkg, orc, gpu, nb, want):
         got = gpu_render(pkg, None, W, H, m, method, torch, density=density)
         ref = orc.render(vol, orc.make_params(W, H, m, query_method=method, density=density))[:3]
         assert_parity(got, ref, f"nb={nb} m{method} d={density}")
-        k = want if method != 3 else ("k_march<" if nb == 8 else "k_march_ws<")
-        if method != 3 or nb == 8:
-            assert pkg.last_kernel().startswith(k), (method, pkg.last_kernel())
+        k = want if method != 3 else "k_march<"  # entropy: the one-sample box
+        assert pkg.last_kernel().startswith(k), (method, pkg.last_kernel())
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_small_frame_entropy_dispatch(pkg, orc, gpu, nb):
+    """entropy of small and mid-size full frames with 1-4 bins (round 4): 2-lane
+    windows for frames up to 128 K rays and for oblique frames up to 700 K, the LDS
+    box for row-aligned frames of a coarse volume above 128 K rays; bit-identical,
+    dense and sparse (early exit) transfer"""
+    import torch
+    vol = orc.synth_volume(36, 30, 28, nb)
+    pkg.init_distribution(vol)
+    rows, obl = pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))
+    for m, W, H, want in ((rows, 200, 150, "k_march_segp2<"), (obl, 200, 150, "k_march_segp2<"),
+                          (rows, 400, 360, "k_march<"), (obl, 400, 360, "k_march_segp2<")):
+        for density in (0.05, 2.0):
+            got = gpu_render(pkg, None, W, H, m, 3, torch, density=density)
+            ref = orc.render(vol, orc.make_params(W, H, m, query_method=3, density=density))[:3]
+            assert_parity(got, ref, f"nb={nb} {W}x{H} d={density}")
+            assert pkg.last_kernel().startswith(want), (W, H, pkg.last_kernel())
 
 
 def test_environment_does_not_change_the_kernel(pkg, orc, gpu, monkeypatch):

@@ -721,6 +721,21 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
             // (profiles/r04/variants_256x4_r4g.log)
             small_seg = (rays <= 131072 || (!row_like && rays <= 400000)) ? -4 : -2;
         }
+        // Entropy of such frames with 1, 2 or 4 bins (round 4): the wave-staged
+        // march (row-aligned) and the one-lane march (oblique) lose to 2-lane
+        // windows, and row-aligned coarse frames above 128 K rays to the LDS box:
+        // 128^3 x 1 at 256^2 C0 1.066 -> 0.481 ms, C1 0.988 -> 0.514; 256^3 x 4 at
+        // 512^2 C0 1.600 -> 1.185 (box), C1 2.299 -> 1.707; 256^3 x 2 at 512^2 C0
+        // 1.343 -> 0.783 (box), C1 1.113 -> 1.064 (profiles/r04/variants_midsize_m3_r4ag.log)
+        if (!d->d_tile_list && !codec && !flex && d->query_method == 3 && !P.axis_view &&
+            (g.nb == 1 || g.nb == 2 || g.nb == 4) && rays <= seg_rays) {
+            if (along_rows && rays > 131072 && rays >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny) {
+                P.path = 1;
+            } else {
+                P.path = 7;
+                small_seg = -2;
+            }
+        }
     }
     if (P.path != 2 && P.path != 7) P.axis_view = 0;  // 7: the segmented march reads the copy too
     if (const char *e = vr::tuning("VR_DUO")) {  // 0 / 1: one sample per box, 2-4: that many
