@@ -11,8 +11,15 @@ before timing (synthetic, seeded) and replicated per GPU.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1024x8]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts
+its own N ranks: a child `python -m torch.distributed.run --nproc-per-node N
+bench.py ...` (a fresh process; this one never touches the GPU), whose rank-0
+JSON line it relays, exiting with the launcher's return code.  Under an external
+launcher WORLD_SIZE must equal --gpus (a mismatch exits non-zero).
+
 Prints ONE JSON line on rank 0 (contract in the task statement).  The metric
-formula is the reference's own benchmark line, 1e-6*W*H/t (C:1065-1067).
+formula is the reference's own benchmark line, 1e-6*W*H/t (C:1065-1067); one
+frame = one render_kernel (K:2387-2401), timed as runSingleTest does (C:1049-1067).
 """
 from __future__ import annotations
 
@@ -48,6 +55,53 @@ GMM_CPU_EDGE = 512  # CPU-baseline volume edge (a 1024^3 GMM exceeds the box's h
 SEED = 20261015
 CODEC_TEMPLATES, CODEC_SLOTS = 64, 4  # synthetic codec volume (methods 4/5/6)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
+
+
+LAUNCHED_ENV = "VR_BENCH_RANKS_LAUNCHED"  # set by the self-launch in the ranks' environment
+
+
+def launch_plan(gpus, argv, env):
+    """What `bench.py --gpus N` does before any GPU call: ("run", None) = this
+    process is the (only or one) rank; ("spawn", cmd) = start N ranks as fresh
+    child processes with cmd; ("error", why) = refuse.  Pure, so the CPU tests
+    cover every branch (tests/test_bench_launch.py)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", (f"--gpus {gpus} but WORLD_SIZE {ws}: the launcher started a "
+                             f"different number of ranks than asked for")
+        return "run", None
+    if gpus <= 1:
+        return "run", None
+    if env.get(LAUNCHED_ENV):
+        return "error", "self-launched rank without WORLD_SIZE (launcher did not set it)"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", os.path.abspath(__file__), *argv]
+    return "spawn", cmd
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relay_ranks(cmd, env=None):
+    """Run the rank launcher as a child process (never exec: this process may not
+    replace itself) and stream its output: JSON lines (rank 0's result) to stdout,
+    everything else to stderr, so the caller sees exactly one JSON line.  Returns
+    the launcher's return code (non-zero when any rank failed)."""
+    import subprocess
+    env = dict(os.environ if env is None else env)
+    env[LAUNCHED_ENV] = "1"
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def parse():
@@ -306,6 +360,7 @@ def main_gmm(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus, (world, args.gpus)  # launch_plan refused anything else
     ndev = torch.cuda.device_count()
     if args.dist_backend == "nccl" and world > ndev:
         raise SystemExit(f"{world} ranks need {world} GPUs, {ndev} visible")
@@ -469,12 +524,14 @@ def main_gmm(args):
             "value": round(W * H / (elapsed / args.steps) / 1e6, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
+            "physical_gpus": min(world, max(ndev, 1)),
+            "rehearsal_shared_gpus": world > max(ndev, 1),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(1e3 / ms_per_step, 2),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": None if world > max(ndev, 1) else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic seeded GMM volume (seed {SEED}, DESIGN.md s11.1)",
@@ -514,6 +571,14 @@ def main_gmm(args):
 
 def main():
     args = parse()
+    what, detail = launch_plan(args.gpus, sys.argv[1:], os.environ)
+    if what == "error":
+        print(f"bench.py: {detail}", file=sys.stderr)
+        sys.exit(2)
+    if what == "spawn":
+        print(f"bench.py: starting {args.gpus} ranks: {' '.join(detail)}", file=sys.stderr,
+              flush=True)
+        sys.exit(relay_ranks(detail))
     if args.config in GMM_CONFIGS:
         if args.baked:
             raise SystemExit("--baked applies to the histogram / codec volumes (DESIGN.md s12)")
@@ -525,10 +590,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if rank == 0:
-            print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
-                  file=sys.stderr)
+    assert world == args.gpus, (world, args.gpus)  # launch_plan refused anything else
     ndev = torch.cuda.device_count()
     if args.dist_backend == "nccl" and world > ndev:
         raise SystemExit(f"{world} ranks need {world} GPUs, {ndev} visible")

@@ -1,0 +1,77 @@
+"""bench.py's rank launcher (CPU): `python bench.py --gpus N` must start N ranks
+itself when no launcher did, refuse a WORLD_SIZE that differs from --gpus, and
+relay exactly rank 0's JSON line with the launcher's return code."""
+import importlib.util
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_plan_single_gpu_runs_in_process():
+    b = _bench()
+    assert b.launch_plan(1, ["--gpus", "1"], {}) == ("run", None)
+    assert b.launch_plan(1, [], {"WORLD_SIZE": "1"}) == ("run", None)
+
+
+def test_plan_external_launcher_must_match():
+    b = _bench()
+    assert b.launch_plan(8, [], {"WORLD_SIZE": "8"}) == ("run", None)
+    what, why = b.launch_plan(8, [], {"WORLD_SIZE": "1"})
+    assert what == "error" and "WORLD_SIZE 1" in why
+    assert b.launch_plan(1, [], {"WORLD_SIZE": "4"})[0] == "error"
+
+
+def test_plan_spawns_n_ranks_with_the_same_arguments():
+    b = _bench()
+    argv = ["--gpus", "4", "--config", "256x4", "--steps", "3"]
+    what, cmd = b.launch_plan(4, argv, {})
+    assert what == "spawn"
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    port = [c for c in cmd if c.startswith("--master-port=")]
+    assert len(port) == 1 and 0 < int(port[0].split("=")[1]) < 65536
+    assert cmd[-len(argv):] == argv and cmd[-len(argv) - 1].endswith("bench.py")
+    # a child that lost WORLD_SIZE must not launch again
+    assert b.launch_plan(4, argv, {b.LAUNCHED_ENV: "1"})[0] == "error"
+
+
+def test_relay_keeps_one_json_line_and_the_worst_rc(capfd):
+    b = _bench()
+    script = ("import sys, os; print('rank log'); print('{\"metric\": 1}'); "
+              "sys.stderr.write('err\\n'); sys.exit(int(os.environ['" + b.LAUNCHED_ENV + "']) * 3)")
+    rc = b.relay_ranks([sys.executable, "-c", script])
+    out, err = capfd.readouterr()
+    assert rc == 3
+    assert out.strip().splitlines() == ['{"metric": 1}']
+    assert "rank log" in err and "err" in err
+
+
+def test_bench_refuses_mismatched_world_size():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE 2" in r.stderr and not r.stdout.strip()
+
+
+def test_self_launch_starts_ranks_with_world_size(tmp_path, capfd):
+    """The spawned launcher really sets WORLD_SIZE/RANK in N fresh processes:
+    run it on a stand-in script that reports its environment (no GPU)."""
+    b = _bench()
+    probe = tmp_path / "probe.py"
+    probe.write_text("import os, json\n"
+                     "if os.environ['RANK'] == '0':\n"
+                     "    print(json.dumps({'ws': os.environ['WORLD_SIZE']}), flush=True)\n")
+    what, cmd = b.launch_plan(2, [], {})
+    cmd = [c if not c.endswith("bench.py") else str(probe) for c in cmd]
+    rc = b.relay_ranks(cmd)
+    out, _ = capfd.readouterr()
+    assert rc == 0 and out.strip().splitlines() == ['{"ws": "2"}']

@@ -39,11 +39,12 @@ def test_bench_single_and_two_rank_frames_agree(gpu, tmp_path):
     assert rc["bytes"] == 256 ** 3 * 4 * 4 and rc["GBps"] > 100 and rc["ms"] <= rc["mean_ms"]
     assert rf["frac_of_read_ceiling"] > 0 and rf["gather_bytes_per_launch"] > 0
     f2 = str(tmp_path / "f2.npy")
-    out2 = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                 "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", "29533",
-                 "bench.py", "--gpus", "2", *ARGS, "--dist-backend", "gloo",
+    # bench.py starts its own 2 ranks (no external launcher), as the driver's
+    # `python bench.py --gpus N` does
+    out2 = _run([sys.executable, "bench.py", "--gpus", "2", *ARGS, "--dist-backend", "gloo",
                  "--dump-frame", f2], tmp_path)
-    assert out2["n_gpus"] == 2
+    assert out2["n_gpus"] == 2 and out2["physical_gpus"] == 1
+    assert out2["rehearsal_shared_gpus"] is True and out2["scaling"] is None
     a, b = np.load(f1), np.load(f2)
     assert a.shape == (512, 512) and np.count_nonzero(a) > 0
     assert np.array_equal(a, b), f"{int(np.sum(a != b))} pixels differ between N=1 and N=2"
