@@ -179,6 +179,41 @@ def test_baked_axis_views_take_a_plane_copy(pkg, orc, gpu, tune, nb):
     assert "plane" not in pkg.last_kernel()
 
 
+@pytest.mark.parametrize("seg", ["0", ""])
+def test_baked_wide_planes_keep_plane_copies_on_their_modes(pkg, orc, gpu, tune, seg):
+    """x-row planes too large for 32-bit indices march with method -1 (64-bit plane
+    index); a plane's y- / z-rows copy must never go there (it is not an x-row
+    plane): VR_PLANE_WIDE=1 forces the wide branch at a small size, and every view
+    stays bit-identical to the oracle -- the row-aligned view on M=-1, the side and
+    top views on their plane copies (M=0, MODE 4 / 5), full frames and rank lists"""
+    import torch
+    vol = orc.synth_volume(52, 40, 47, 4)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    W, H = 120, 88
+    if seg:
+        tune.set("VR_SEG_RAYS", seg)
+    tune.set("VR_PLANE_WIDE", "1")
+    try:
+        for rot, kern in ((None, "M=-1"), ((0.0, 90.0), "plane_zrows"),
+                          ((90.0, 90.0), "plane_yrows")):
+            m = (pkg.camera.single_test_inv_view() if rot is None
+                 else pkg.camera.display_inv_view(rot))
+            for method in (1, 3):
+                got = gpu_render(pkg, None, W, H, m, method, torch)
+                assert kern in pkg.last_kernel(), (rot, pkg.last_kernel())
+                if rot is not None:
+                    assert "M=0" in pkg.last_kernel(), pkg.last_kernel()
+                ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+                assert_parity(got, ref, f"wide baked {rot} m{method}")
+            got, kernels = _split_frame(pkg, torch, W, H, m, 3, 2)
+            ref8 = orc.render(vol, orc.make_params(W, H, m, query_method=2), want_float=False,
+                              want_steps=False)[0]
+            assert np.array_equal(got, ref8), (rot, kernels)
+    finally:
+        pkg.release_stats()
+
+
 @pytest.mark.parametrize("nb", [1, 2, 4, 8])
 def test_axis_copy_tiles_pitched_and_ragged(pkg, orc, gpu, tune, nb):
     """the LDS-tiled axis copy (k_axis_copy, 32 x 32 record tiles): volumes whose x,

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-5 GPU jobs, one case per gpurun call: bash tools/jobs/r5.sh <job>
+# (each writes gpurun_out/<job>/; the committed logs under profiles/r05/ name
+# the job they came from).  Round 4's single-use scripts: profiles/r04/jobs/.
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
+J=${1:?job}; O=gpurun_out/$J; mkdir -p $O
+guard() { rc=$1; if [ $rc -ne 0 ]; then echo "$2 failed rc=$rc"; tail -30 $3; exit $rc; fi; }
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+case $J in
+launch)  # self-launched N = 2 bench, layout / wide-plane tests, m3 rank-list paths
+  timeout -k 10 600 $PYT tests/test_gpu_bench.py tests/test_gpu_layout.py > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -3 $O/pytest.log
+  timeout -k 10 300 python -u bench.py --gpus 2 --config 256x4 --dist-backend gloo --no-cpu-baseline --steps 5 --warmup 2 > $O/bench_n2.log 2>&1; guard $? n2 $O/bench_n2.log
+  grep '^{' $O/bench_n2.log | cut -c1-400
+  for CAM in C0; do
+    timeout -k 10 300 python -u tools/rank_sim.py --camera $CAM --method 3 --modes cost --envs "" "VR_PATH=4" > $O/rank_m3_$CAM.log 2>&1; guard $? rs-m3 $O/rank_m3_$CAM.log
+  done ;;
+*) echo "unknown job $J"; exit 2 ;;
+esac
+echo done

@@ -91,8 +91,9 @@ struct State {
         int plane = -1;
         uint64_t sy = 0, sz = 0, bytes = 0;
     } pcopy[2];
-    // layout copies (micro-bricks, axis rows): byte budget (vr_set_layout_budget)
-    // and the cost of the last one made (vr_layout_info)
+    // layout copies (micro-bricks, axis rows): byte budget (vr_set_layout_budget;
+    // UINT64_MAX = the default, layout_budget_bytes) and the cost of the last one
+    // made (vr_layout_info)
     uint64_t layout_budget = UINT64_MAX;
     float layout_last_ms = 0.0f;
     uint64_t layout_last_bytes = 0;
@@ -182,9 +183,21 @@ uint64_t layout_resident() {
 // Room for a layout copy of `bytes`: within the budget (vr_set_layout_budget)
 // next to the copies already resident (less `freed`, a copy the caller would
 // drop first), and HBM keeps max(4 GiB, 5 %) free after it for the caller.
+// The default budget: two copies of the resident record volume (a brick copy
+// and one axis copy, or both axis copies) plus two copies of one baked plane,
+// each with 1/8 for the copies' padding -- what one view class plus one change
+// of view needs, not every copy at once (a third record copy replaces one).
+uint64_t layout_budget_bytes() {
+    if (g.layout_budget != UINT64_MAX) return g.layout_budget;
+    const uint64_t rec = g.vol ? g.sz * (uint64_t)g.nz * g.nb * sizeof(float) : 0;
+    const uint64_t plane = g.stats ? g.stats_plane * sizeof(float) : 0;
+    return 2 * (rec + rec / 8) + 2 * (plane + plane / 8);
+}
+
 bool layout_room(uint64_t bytes, uint64_t freed = 0) {
     const uint64_t have = layout_resident() - freed;
-    if (g.layout_budget < have || g.layout_budget - have < bytes) return false;
+    const uint64_t budget = layout_budget_bytes();
+    if (budget < have || budget - have < bytes) return false;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
         (void)hipGetLastError();
@@ -1582,7 +1595,7 @@ int vr_set_layout_budget(uint64_t bytes) {
     g.layout_budget = bytes;
     // copies already resident beyond a lowered budget are dropped (the next
     // frame that wants one makes it again if it fits)
-    if (layout_resident() > bytes) {
+    if (layout_resident() > layout_budget_bytes()) {
         release_brick();
         release_axis_copy();
         release_plane_copies();
@@ -1677,7 +1690,14 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
             }
         }
         P.path = baked_path(desc, P);
-        const bool narrow = plane_narrow(P.sy, P.sz, (uint64_t)P.nz);
+        // method 0: the 32-bit plane index (MODE 1), or a plane copy's MODE 4 / 5
+        // (32-bit in-slice offsets, 64-bit slice offsets: ensure_plane_copy keeps
+        // a slice < 2^32 floats, so a copy never needs -1, which reads x rows);
+        // method -1: x-row planes too large for 32-bit indices (MODE 2).
+        // VR_PLANE_WIDE=1 (tests) sends every x-row plane to -1.
+        const char *ew = vr::tuning("VR_PLANE_WIDE");
+        const bool wide = ew && std::atoi(ew) != 0;
+        const bool narrow = P.plane_axis != 0 || (!wide && plane_narrow(P.sy, P.sz, (uint64_t)P.nz));
         e = vr::launch_march(1, narrow ? 0 : -1, baked, P, nslots, false, g.stream);
     } else if (is_flex_method(desc->query_method)) {
         e = vr::launch_march_flex(desc->query_method, P, nslots, g.stream);
