@@ -425,7 +425,7 @@ def test_errors_do_not_exit(pkg, gpu):
     ("7", {"VR_SEG": "-2", "VR_WG_PER_CU": "3"}), ("1", {"VR_BOX_MAX": "64", "VR_WG_PER_CU": "3"}),
     ("2", {"VR_WG_PER_CU": "2"}), ("0", {"VR_WG_PER_CU": "3"}),
     ("0", {"VR_QUAD2": "1"}), ("0", {"VR_QUAD2": "1", "VR_WG_PER_CU": "1"}),
-    # K samples per footprint box (k_march_duo, m1/m2), with direct-path fallbacks
+    # K samples per footprint box (k_march_duo, m1/m2/m3), with direct-path fallbacks
     ("1", {"VR_DUO": "2"}), ("1", {"VR_DUO": "2", "VR_BOX_MAX": "64"}),
     ("1", {"VR_DUO": "3"}), ("1", {"VR_DUO": "4", "VR_BOX_MAX": "64"}),
 ])
@@ -450,9 +450,10 @@ def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
 @pytest.mark.parametrize("k", ["2", "3", "4"])
 @pytest.mark.parametrize("nb", [1, 2, 8])
 def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune):
-    """k_march_duo (two samples per footprint box, mean and variance): rays ending on
-    the first or the second sample of a pair (opacity, tfar), full frames and tile
-    lists, bit-identical to the oracle (entropy: k_march)"""
+    """k_march_duo (K samples per footprint box; mean, variance and entropy -- the
+    entropy instance restored in round 5 with k_march's LDS log table and record
+    columns): rays ending on any sample of a box (opacity, tfar),
+    full frames and tile lists, bit-identical to the oracle"""
     import torch
     tune.set("VR_PATH", "1")
     tune.set("VR_DUO", k)
@@ -465,8 +466,7 @@ def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune):
             for method in (1, 2, 3):
                 got = gpu_render(pkg, None, 72, 40, cam, method, torch, density=density,
                                  brightness=bright)
-                want = ("k_march<" if method == 3  # k_march_duo: m1 / m2
-                        else "k_march_duo<" if k == "2" else f"k_march_duo{k}<")
+                want = "k_march_duo<" if k == "2" else f"k_march_duo{k}<"
                 assert pkg.last_kernel().startswith(want), pkg.last_kernel()
                 ref = orc.render(vol, orc.make_params(72, 40, cam, query_method=method,
                                                       density=density, brightness=bright))[:3]

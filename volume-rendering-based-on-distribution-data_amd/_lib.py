@@ -95,7 +95,7 @@ EXPORTS = [
     "vr_unscatter_tiles", "vr_tiles_x", "vr_tiles_y", "vr_version", "vr_last_kernel", "vr_selftest_logf", "vr_parse_codebook", "vr_parse_templates",
     "vr_load_reference_files", "vr_init_flex", "vr_flex_process", "vr_flex_info",
     "vr_parse_span_list", "vr_parse_fractal_histogram", "vr_parse_simple_histogram",
-    "vr_load_flex_files", "vr_debug_wave_clock",
+    "vr_load_flex_files", "vr_debug_wave_clock", "vr_debug_box_check",
     "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_render_gmm",
     "vr_gmm_count_footprint", "vr_bake_stats", "vr_release_stats", "vr_stats_info",
     "vr_set_tuning", "vr_clear_tuning", "vr_stream_read", "vr_set_layout_budget",
@@ -196,6 +196,8 @@ def load() -> ctypes.CDLL:
     L.vr_load_flex_files.restype = i32
     L.vr_debug_wave_clock.argtypes = [ctypes.c_void_p]
     L.vr_debug_wave_clock.restype = ctypes.c_int
+    L.vr_debug_box_check.argtypes = [ctypes.c_void_p]
+    L.vr_debug_box_check.restype = ctypes.c_int
     L.vr_last_kernel.argtypes = []
     L.vr_last_kernel.restype = ctypes.c_char_p
     L.vr_init_gmm.argtypes = [vp, vp, Extent, i32, i32, i32, i32]

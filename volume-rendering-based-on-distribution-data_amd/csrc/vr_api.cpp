@@ -57,6 +57,7 @@ struct State {
     uint32_t *tile_cost = nullptr;
     size_t tile_cost_cap = 0;
     unsigned long long *wave_clock = nullptr;  // vr_debug_wave_clock (tooling)
+    unsigned long long *box_check = nullptr;   // vr_debug_box_check (tooling, -DVR_BOX_CHECK builds)
     // GMM volume (config 5, vr_gmm.hip): planes (w, mu)[voxel][K][2] and
     // sigma[voxel][K] of the resident slices [z_base, z_base + nzs) of an
     // nx x ny x nz volume
@@ -772,6 +773,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     P.quad2 = d->d_tile_list && (uint64_t)d->n_tiles * vr::kTileW * vr::kTileH <= 700000u;
     if (const char *e = vr::tuning("VR_QUAD2")) P.quad2 = std::atoi(e) != 0;
     P.wave_clock = g.wave_clock;
+    P.box_check = g.box_check;
     P.tile_cost = record;
     P.seg_lanes = small_seg ? small_seg : -2;  // VR_SEG=S: S lanes per ray, negative = pipelined windows
     if (const char *e = vr::tuning("VR_SEG")) {
@@ -1747,6 +1749,18 @@ int vr_render(const vr_render_desc *desc) { return render_frame(desc, UINT32_MAX
 int vr_debug_wave_clock(uint64_t *d_buf) {
     g.wave_clock = reinterpret_cast<unsigned long long *>(d_buf);
     return VR_OK;
+}
+
+// tooling: 4 x u64 device counters of LDS-box bound violations (k_march /
+// k_march_duo staged reads); counted only by a -DVR_BOX_CHECK build, which
+// reports whether it was built so (return 1) -- the default build returns 0
+int vr_debug_box_check(uint64_t *d_buf) {
+    g.box_check = reinterpret_cast<unsigned long long *>(d_buf);
+#ifdef VR_BOX_CHECK
+    return 1;
+#else
+    return 0;
+#endif
 }
 
 int64_t vr_count_footprint(const vr_render_desc *desc) {

@@ -100,7 +100,10 @@ struct Params {
     int head_lanes;
     int head_tail;               // the rest of such a list: 0 seg_lanes windows, 1 one lane per ray (k_march_pipe_head)
     int plane_axis;              // baked frame on a plane's axis copy: 1 y rows, 2 z rows (gather8 MODE 3 + axis)
-    int duo;                     // LDS-box march (path 1, B <= 8, m1/m2): samples per box (k_march_duo), 0/1 = k_march
+    int duo;                     // LDS-box march (path 1, B <= 8, m1/m2/m3): samples per box (k_march_duo), 0/1 = k_march
+    // tooling (vr_debug_box_check; only a -DVR_BOX_CHECK build reads it): LDS-box
+    // bound violations {count, worst index - box size, box voxels, lane footprint}
+    unsigned long long *box_check;
 };
 
 // Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one

@@ -246,6 +246,37 @@ __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, cons
 #ifndef VR_MARCH_MINW
 #define VR_MARCH_MINW 1   // minimum waves per SIMD the register allocation must allow
 #endif
+
+#ifdef VR_BOX_CHECK
+// Tooling build (-DVR_BOX_CHECK, vr_debug_box_check): the staged reads' bounds.
+// A lane's 8 corners must lie inside the wave's box, the largest box index it
+// reads, ((z1 - bz0) dy + (y1 - by0)) dx + (x1 - bx0), below the box's dx dy dz
+// voxels (those the decode wrote this step), and the box inside the volume.  A
+// violating read is counted and skipped (its sample is 0), never performed.
+__device__ __forceinline__ bool box_ok(const Params &P, const Foot &f, int bx0, int by0, int bz0,
+                                       int dx, int dy, int dz) {
+    const int hi = ((f.z1 - bz0) * dy + (f.y1 - by0)) * dx + (f.x1 - bx0);
+    const bool ok = f.x0 >= bx0 && f.y0 >= by0 && f.z0 >= bz0 && f.x1 >= f.x0 &&
+                    f.y1 >= f.y0 && f.z1 >= f.z0 && f.x1 < bx0 + dx && f.y1 < by0 + dy &&
+                    f.z1 < bz0 + dz && hi < dx * dy * dz && dx * dy * dz <= P.box_max;
+    if (!ok && P.box_check) {
+        atomicAdd(P.box_check, 1ull);
+        const long long over = (long long)hi + 1 - (long long)dx * dy * dz;
+        if (over > 0) atomicMax(P.box_check + 1, (unsigned long long)over);
+    }
+    return ok;
+}
+// (wave-uniform) false = the box is not inside the volume: counted, and the
+// step takes the direct path instead, whose corners footprint() clamps
+__device__ __forceinline__ bool box_in_volume(const Params &P, int bx0, int by0, int bz0, int dx,
+                                              int dy, int dz, uint32_t lane) {
+    const bool in = bx0 >= 0 && by0 >= 0 && bz0 >= 0 && bx0 + dx <= P.nx &&
+                    by0 + dy <= P.ny && bz0 + dz <= P.nz;
+    if (!in && lane == 0 && P.box_check)
+        atomicAdd(P.box_check + 2, (unsigned long long)(dx * dy * dz));
+    return in;
+}
+#endif
 template <int B, int M, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MINW, 8))) void k_march(const float *__restrict__ vol, Params P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -306,7 +337,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                 const int by1 = min(wave_max(alive ? f.y0 : -1) + 1, P.ny - 1);
                 const int bz1 = min(wave_max(alive ? f.z0 : -1) + 1, P.nz - 1);
                 const int dx = bx1 - bx0 + 1, dy = by1 - by0 + 1, dz = bz1 - bz0 + 1;
+#ifdef VR_BOX_CHECK
+                if (dx * dy * dz <= P.box_max && box_in_volume(P, bx0, by0, bz0, dx, dy, dz, lane)) {
+#else
                 if (dx * dy * dz <= P.box_max) {  // wave-uniform
+#endif
                     staged = true;
                     const int dxy = dx * dy;
                     const float *vbase =
@@ -316,7 +351,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef VR_BOX_CHECK
+                    if (alive && box_ok(P, f, bx0, by0, bz0, dx, dy, dz)) {
+#else
                     if (alive) {
+#endif
                         const int b0 = ((f.z0 - bz0) * dy + (f.y0 - by0)) * dx + (f.x0 - bx0);
                         const int ox = f.x1 - f.x0, oy = (f.y1 - f.y0) * dx;
                         const int oz = (f.z1 - f.z0) * dxy;
@@ -373,17 +412,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
 // ray reaches it by tfar, K:700-705), so those costs are paid once per two
 // samples.  The samples and their compositing are those of k_march in the same
 // order (positions advanced by the same float adds; a ray that terminates on the
-// first sample leaves the second unread): the frame is bit-identical.  Mean and
-// variance only: the entropy instance needed 190 VGPRs and a private stack, and
-// faulted at 512^3 (HSA aperture violation, profiles/r04/variants_512x8_m3_duo_fault.log).
+// first sample leaves the second unread): the frame is bit-identical.  Entropy
+// (M = 3) decodes through the LDS log table and the rolled record columns of
+// k_march (same LDS request); its round-4 fault is DESIGN.md 4.2.1.
 template <int B, int M, int K>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MINW, 8))) void k_march_duo(const float *__restrict__ vol, Params P) {
-    static_assert(M == 1 || M == 2, "mean and variance (entropy: k_march)");
+    static_assert(M >= 1 && M <= 3, "mean, variance, entropy");
     static_assert(K >= 2 && K <= 4, "samples per box");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const uint32_t slot = launch_slot(P);
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;  // whole workgroup uniform
+    const LogEnt *tab = nullptr;
+    float *st = nullptr;
+    if constexpr (M == 3 && B >= 8) {  // k_march's entropy layout behind the box slices
+        LogEnt *tb = reinterpret_cast<LogEnt *>(lds + 4u * (uint32_t)P.box_max);
+        copy_logtab(tb);
+        __syncthreads();
+        tab = tb;
+        st = lds + 4u * (uint32_t)P.box_max + 65u * (sizeof(LogEnt) / 4u) + (threadIdx.x >> 6) * 64u * B;
+    }
     const uint32_t lane = threadIdx.x & 63u;
     float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
     uint32_t lx, ly;
@@ -444,12 +492,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
         const int by1 = min(-hi_y + 1, P.ny - 1);
         const int bz1 = min(-hi_z + 1, P.nz - 1);
         const int dx = bx1 - bx0 + 1, dy = by1 - by0 + 1, dz = bz1 - bz0 + 1;
+#ifdef VR_BOX_CHECK
+        const bool staged = dx * dy * dz <= P.box_max && box_in_volume(P, bx0, by0, bz0, dx, dy, dz, lane);
+#else
         const bool staged = dx * dy * dz <= P.box_max;  // wave-uniform
+#endif
         const int dxy = dx * dy;
         if (staged) {
             const float *vbase =
                 vol + ((uint64_t)bz0 * P.sz + (uint64_t)by0 * P.sy + (uint64_t)bx0) * (uint64_t)B;
-            decode_box<B, M>(vbase, P, box, dx, dxy, dxy * dz, lane, nullptr, nullptr);
+            decode_box<B, M>(vbase, P, box, dx, dxy, dxy * dz, lane, tab, st);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -459,7 +511,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
             // alive here: the ray reached this sample (t <= tfar), so f[k] is in the box
             if (alive) {
                 const Foot &fk = f[k];
-                float sample;
+                float sample = 0.0f;
+#ifdef VR_BOX_CHECK
+                if (staged && !box_ok(P, fk, bx0, by0, bz0, dx, dy, dz)) {
+                } else
+#endif
                 if (staged) {
                     const int b0 = ((fk.z0 - bz0) * dy + (fk.y0 - by0)) * dx + (fk.x0 - bx0);
                     const int ox = fk.x1 - fk.x0, oy = (fk.y1 - fk.y0) * dx;
@@ -475,7 +531,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                     sv[7] = box[b0 + oz + oy + ox];
                     sample = blend8(sv, fk);
                 } else {
-                    sample = sample_direct<B, M>(vol, P, fk);
+                    sample = sample_direct<B, M>(vol, P, fk, tab, st);
                 }
                 n = i + k + 1;
                 if (composite(P, sample, sx, sy, sz, sw)) {
@@ -2694,19 +2750,22 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         if (const char *em = tuning("VR_BOX_MAP")) P.wq_map = std::atoi(em) != 0;
     }
     if constexpr (!COUNT && B > 0 && B <= 8) {
-        // mean and variance: P.duo samples per footprint box (k_march_duo;
-        // fill_params: coarse row-aligned 8-bin full frames, VR_DUO)
+        // P.duo samples per footprint box (k_march_duo; fill_params: coarse
+        // row-aligned 8-bin full frames, VR_DUO)
         const int k = P.duo;
-        if (k >= 2 && k <= 4 && (method == 1 || method == 2) && P.box_max > 0) {
+        if (k >= 2 && k <= 4 && method >= 1 && method <= 3 && P.box_max > 0) {
             note_kernel(k == 2 ? "k_march_duo" : k == 3 ? "k_march_duo3" : "k_march_duo4", B, method);
 #define VR_DUO_L(MM, KK) hipLaunchKernelGGL((k_march_duo<B, MM, KK>), grid, block, lds, s, vol, P)
             switch (k * 4 + method) {
             case 9: VR_DUO_L(1, 2); break;
             case 10: VR_DUO_L(2, 2); break;
+            case 11: VR_DUO_L(3, 2); break;
             case 13: VR_DUO_L(1, 3); break;
             case 14: VR_DUO_L(2, 3); break;
+            case 15: VR_DUO_L(3, 3); break;
             case 17: VR_DUO_L(1, 4); break;
             case 18: VR_DUO_L(2, 4); break;
+            case 19: VR_DUO_L(3, 4); break;
             }
 #undef VR_DUO_L
             return hipGetLastError();
