@@ -132,6 +132,12 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages the tile gather through host memory (multi-rank "
                          "rehearsal on a single GPU; never for measurement)")
+    ap.add_argument("--slab-rehearsal", action="store_true",
+                    help="GMM volumes on ONE GPU: every rank's z-slab of the --rehearsal-ranks "
+                         "chain generated in turn (untimed) and its march timed with HIP "
+                         "events; reports per-slab ms and the pipeline-period estimate")
+    ap.add_argument("--rehearsal-ranks", type=int, default=8,
+                    help="--slab-rehearsal: slabs (ranks) of the chain (BASELINE config 5: 8)")
     ap.add_argument("--cpu-row-stride", type=int, default=0,
                     help="CPU baseline renders every k-th row (0 = auto)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -345,6 +351,130 @@ def gmm_cpu_baseline(m, method, W, H, K):
     }
 
 
+def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
+    """BASELINE config 5 rehearsed on one GPU.  The chain's R
+    slabs (march order) are generated in HBM one at a time, untimed, as rank r
+    holds slab r; each slab's march is timed with HIP events over --steps frames
+    of its real input (slab 0: the camera rays; slab r: the alive list slab r - 1
+    handed on, kept in HBM); its U is counted on the same input.  Two passes:
+    equal slabs, then the cost-balanced cut bench.py's N-rank run makes after
+    its untimed first frame (slabs.bounds_by_cost).  The pipeline period of the
+    R-GPU chain is at least its slowest slab's march (the RCCL hand-off of the
+    alive list and the frame reduce run beside it on other streams and are not
+    in this number): value = W*H / max over slabs.  Not an N-GPU measurement:
+    n_gpus 1, scaling null."""
+    R = args.rehearsal_ranks
+    direction = pkg.slabs.march_direction(m, W, H)
+    frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    desc = pkg.make_desc(frame, W, H, m, query_method=args.method, volume_size=(1, 1, 1))
+    bufs = [torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device=dev)
+            for _ in range(2)]
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    # the library launches on `stream` (pkg.set_stream): the alive-list counter
+    # is zeroed on the same stream, so every launch starts from an empty list
+    assert torch.cuda.current_stream(dev) == stream
+
+    def chain(bounds, label):
+        rows, n_in = [], 0
+        for i, (z_lo, z_hi) in enumerate(bounds):
+            if i and n_in == 0:  # no ray reaches this slab: nothing to march
+                rows.append({"slab": i, "z": [z_lo, z_hi], "rays_in": 0, "ms": 0.0,
+                             "rays_out": 0, "U_records": 0})
+                continue
+            zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
+            tg = time.perf_counter()
+            pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
+            torch.cuda.synchronize()
+            gen_s = time.perf_counter() - tg
+            out, inp = bufs[i % 2], bufs[(i + 1) % 2]
+            slab = pkg.gmm_slab(z_lo, z_hi, out, cnt, d_rays_in=inp if i else None, n_rays_in=n_in)
+            cnt.zero_()
+            u = pkg.gmm_count_footprint(desc, slab)
+            ev = []
+            for f in range(args.warmup + args.steps):
+                cnt.zero_()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                pkg.render_gmm(desc, slab)
+                e1.record(stream)
+                if f >= args.warmup:
+                    ev.append((e0, e1))
+            torch.cuda.synchronize()
+            ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+            n_out = int(cnt.item())
+            if n_out > (n_in if i else W * H):
+                raise RuntimeError(f"slab {i}: {n_out} alive rays out of {n_in if i else W * H} in")
+            # algorithmic bytes of the slab's launch: its footprint records, the
+            # alive list in and out (48 B a ray), the pixels of rays ending here
+            ended = (W * H if i == 0 else n_in) - n_out
+            alg = u * rec_bytes + (n_in + n_out) * 48 + max(ended, 0) * 4
+            rows.append({"slab": i, "z": [z_lo, z_hi], "resident_slices": ns,
+                         "rays_in": n_in if i else W * H, "rays_out": n_out,
+                         "ms": round(ms, 4), "U_records": int(u), "alg_bytes": int(alg),
+                         "GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "generate_s": round(gen_s, 2)})
+            print(f"slab rehearsal ({label}) slab {i} z [{z_lo}, {z_hi}): {ms:.3f} ms, "
+                  f"{n_out} rays alive, U {u}", file=sys.stderr, flush=True)
+            n_in = n_out
+            pkg.free_gmm()
+        return rows
+
+    pkg.free_gmm()
+    torch.cuda.empty_cache()
+    equal = pkg.slabs.slab_bounds(n, R, direction)
+    rows_eq = chain(equal, "equal")
+    free_now, _ = torch.cuda.mem_get_info(dev)
+    cap = pkg.slabs.max_slices_for(n, n, K, free_now)
+    balanced = pkg.slabs.bounds_by_cost(n, R, direction, equal, [r["ms"] for r in rows_eq], cap)
+    rows_bal = chain(balanced, "balanced")
+    period = max(r["ms"] for r in rows_bal)
+    kernel = pkg.last_kernel()
+    worst = max(rows_bal, key=lambda r: r["ms"])
+    cpu = None if args.no_cpu_baseline else gmm_cpu_baseline(m, args.method, W, H, K)
+    out = {
+        "metric": f"Mrays/s + fps at {n}^3 x {K}-component GMM volume, {W}x{H}; % HBM roofline "
+                  f"({R}-slab chain rehearsed on one GPU: pipeline-period estimate)",
+        "value": round(W * H / (period * 1e-3) / 1e6, 3),
+        "unit": "Mrays/s",
+        "n_gpus": 1,
+        "physical_gpus": 1,
+        "rehearsal_shared_gpus": True,
+        "rehearsal_ranks": R,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(period, 4),
+        "fps": round(1e3 / period, 2),
+        "higher_is_better": True,
+        "scaling": None,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic seeded GMM volume (seed {SEED}, DESIGN.md s11.1), one slab in HBM at a time",
+        "config": {
+            "workload": f"{n}^3 x {K}-component GMM volume, {W}x{H}, camera {args.camera}, "
+                        f"queryMethod {args.method}, {R} z-slabs",
+            "volume": [n, n, n], "components": K, "image": [W, H], "camera": args.camera,
+            "query_method": args.method, "density": 0.05,
+            "parallelism": f"z-slabs x{R} rehearsed on 1 GPU (each slab's march timed on its "
+                           "real alive-list input; hand-off and frame reduce not timed)",
+            "period": "max over slabs of the slab's mean march time (HIP events, "
+                      f"{args.steps} frames after {args.warmup} warm-up)",
+            "slabs_equal": rows_eq,
+            "slabs_balanced": rows_bal,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": worst.get("GBps"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": worst.get("frac"), "traffic": None,
+            "traffic_source": "no PMC pass for this workload",
+            "kernel": kernel, "kernel_ms": worst["ms"], "of": f"slowest slab ({worst['slab']})",
+            "alg_bytes_per_launch": worst.get("alg_bytes"), "U_records": worst.get("U_records"),
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    return out
+
+
 def main_gmm(args):
     """GMM volumes.  N = 1: the whole volume resident, one
     launch per frame.  N > 1: rank r holds z-slab r (in the view's march order)
@@ -380,6 +510,9 @@ def main_gmm(args):
     free, _ = torch.cuda.mem_get_info(dev)
     stream = torch.cuda.Stream(device=dev)
     pkg.set_stream(stream)
+    if world == 1 and args.slab_rehearsal:
+        with torch.cuda.stream(stream):  # the counter resets and the launches on one stream
+            return gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes)
     if world == 1:
         need = n ** 3 * 12 * K
         if need > free * 0.95:

@@ -424,7 +424,9 @@ int vr_free_gmm(void);
  * float sum[4], t, pos[3]; uint32 pixel, samples taken, 0, 0).  Rays that end in
  * the slab are written to the frame (d_output etc., pixel y*width + x); rays that
  * leave it alive are appended to d_rays_out (capacity: n_rays_in, or
- * width*height) and counted in *d_n_rays_out (caller-zeroed, device memory).
+ * width*height) and counted in *d_n_rays_out (caller-zeroed, device memory;
+ * a count above the capacity means it was not zeroed: entries past the
+ * capacity are dropped, never written).
  * Slabs must be rendered in the order the view's rays cross them (every ray of
  * the frame must step the same way in z, else VR_ERR_UNSUPPORTED); the chain
  * then reproduces the whole-volume render bit for bit. */
@@ -445,6 +447,11 @@ int vr_render_gmm(const vr_render_desc *desc, const vr_gmm_slab *slab);
  * footprints of all samples taken (algorithmic bytes = U * 8K for the mean,
  * U * 12K for the variance).  Synchronous. */
 int64_t vr_gmm_count_footprint(const vr_render_desc *desc);
+/* U of one slab of a chain (slab as for vr_render_gmm: the samples whose
+ * footprint starts in the slab, from its camera rays or its alive list in).
+ * The counting launch also writes the slab's alive list out (as a render
+ * would) but no pixels.  Synchronous. */
+int64_t vr_gmm_count_footprint_slab(const vr_render_desc *desc, const vr_gmm_slab *slab);
 
 /* library version string */
 const char *vr_version(void);

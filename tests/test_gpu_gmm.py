@@ -127,6 +127,54 @@ def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs):
     pkg.free_gmm()
 
 
+def test_gmm_slab_footprint_and_list_capacity(pkg, orc, gpu):
+    """U of every slab of a chain (vr_gmm_count_footprint_slab, what bench.py
+    --slab-rehearsal prices each slab's launch with) equals the oracle's count of
+    that slab; and a slab launch whose alive-list counter was not zeroed drops
+    the entries past the list's capacity (include/vr.h) instead of writing past it"""
+    import torch
+    dims = (24, 20, 23)
+    K, W, H = 16, 72, 56
+    m = cam(pkg, "C0")
+    bounds = pkg.slabs.slab_bounds(dims[2], 3, pkg.slabs.march_direction(m, W, H))
+    wm, sg = orc.synth_gmm(*dims, K)
+    p = orc.make_params(W, H, m, query_method=1)
+    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    d = pkg.make_desc(out, W, H, m, query_method=1, volume_size=(1, 1, 1))
+    bufs = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    n_in, ref_rays = 0, None
+    for i, (z_lo, z_hi) in enumerate(bounds):
+        zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, dims[2])
+        pkg.synthesize_gmm(dims, K, z_base=zb, nslices=ns)
+        cnt.zero_()
+        s = pkg.gmm_slab(z_lo, z_hi, bufs[i % 2], cnt, d_rays_in=bufs[(i + 1) % 2] if i else None,
+                         n_rays_in=n_in)
+        u = pkg.gmm_count_footprint(d, s)
+        r = orc.render_gmm(wm[zb:zb + ns], sg[zb:zb + ns], dims, p, z_base=zb, slab=(z_lo, z_hi),
+                           rays_in=ref_rays, want_mark=True)
+        assert u == r["U"] and (u > 0 or i > 0), (i, u, r["U"])
+        cnt.zero_()
+        pkg.render_gmm(d, s)
+        torch.cuda.synchronize()
+        n_in, ref_rays = int(cnt.item()), r["rays_out"]
+        assert n_in == ref_rays.shape[0]
+    # capacity: slab 0 from the camera holds at most W*H entries; a counter left at
+    # W*H - 3 lets 3 entries in and drops the rest, the rows past the list untouched
+    zb, ns = pkg.slabs.resident_slices(*bounds[0], dims[2])
+    pkg.synthesize_gmm(dims, K, z_base=zb, nslices=ns)
+    big = torch.full((W * H + 64, 12), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    cnt.fill_(W * H - 3)
+    pkg.render_gmm(d, pkg.gmm_slab(*bounds[0], big, cnt))
+    torch.cuda.synchronize()
+    alive = orc.render_gmm(wm[zb:zb + ns], sg[zb:zb + ns], dims, p, z_base=zb,
+                           slab=bounds[0])["rays_out"].shape[0]
+    assert alive > 3 and int(cnt.item()) == W * H - 3 + alive
+    assert bool((big[W * H:] == 0x5A5A5A5A).all()), "entries written past the list's capacity"
+    assert not bool((big[W * H - 3:W * H] == 0x5A5A5A5A).all())
+    pkg.free_gmm()
+
+
 def test_gmm_footprint_count(pkg, orc, gpu):
     import torch
     dims = (30, 26, 22)

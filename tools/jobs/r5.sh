@@ -16,14 +16,18 @@ launch)  # self-launched N = 2 bench, layout / wide-plane tests, m3 rank-list pa
     timeout -k 10 300 python -u tools/rank_sim.py --camera $CAM --method 3 --modes cost --envs "" "VR_PATH=4" > $O/rank_m3_$CAM.log 2>&1; guard $? rs-m3 $O/rank_m3_$CAM.log
   done ;;
 duo)  # k_march_duo entropy restored: parity, LDS-box bound check (checking build), timing
-  timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "duo or every_kernel_path" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
-  tail -2 $O/pytest.log
+  [ -n "$SKIP_PYTEST" ] || { timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "duo or every_kernel_path" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log; }
   VRDD_LIB=tools/build/variants/boxcheck/libvr.so timeout -k 10 300 python -u tools/box_check.py > $O/box_check.log 2>&1; guard $? boxcheck $O/box_check.log
   tail -3 $O/box_check.log
   for CFG in 512x8 1024x8; do
     timeout -k 10 400 python -u tools/bench_variants.py --variants main --config $CFG --cameras C0 --method 3 --rounds 3 --env "" "VR_PATH=1,VR_DUO=2" "VR_PATH=1,VR_DUO=3" "VR_PATH=1,VR_DUO=4" > $O/variants_${CFG}_m3.log 2>&1; guard $? var $O/variants_${CFG}_m3.log
     grep -v "round\|amdgpu.ids" $O/variants_${CFG}_m3.log
   done ;;
+gmm5)  # BASELINE config 5 rehearsed on one GPU: every slab of the 8-slab chain timed
+  timeout -k 10 600 $PYT tests/test_gpu_gmm.py -k "not at_size" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -2 $O/pytest.log
+  timeout -k 10 1000 python -u bench.py --config gmm2048 --slab-rehearsal --steps 5 --warmup 1 > $O/bench.log 2>&1; guard $? gmm5 $O/bench.log
+  grep '^{' $O/bench.log | cut -c1-600 ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done

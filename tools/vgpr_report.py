@@ -49,10 +49,11 @@ def main():
                     rows.append((name, get("vgpr_count"), "  - .agpr_count" and
                                  re.search(r"^:\s+(\d+)", blk).group(1), get("sgpr_count"),
                                  get("vgpr_spill_count"), get("sgpr_spill_count"),
-                                 get("group_segment_fixed_size")))
-        for name, v, a, s, vs, ss, lds in sorted(set(rows)):
+                                 get("group_segment_fixed_size"),
+                                 get("private_segment_fixed_size"), get("uses_dynamic_stack")))
+        for name, v, a, s, vs, ss, lds, priv, dyn in sorted(set(rows)):
             print(f"{name[:90]:90s} vgpr {v:>4} agpr {a:>3} sgpr {s:>3} "
-                  f"spill v{vs}/s{ss} lds {lds}")
+                  f"spill v{vs}/s{ss} lds {lds} private {priv}{' dynamic-stack' if dyn == 'true' else ''}")
 
 
 if __name__ == "__main__":

@@ -516,9 +516,12 @@ def render_gmm(desc: RenderDesc, slab: Optional[_lib.GmmSlab] = None) -> None:
     check(L.vr_render_gmm(ctypes.byref(desc), None if slab is None else ctypes.byref(slab)))
 
 
-def gmm_count_footprint(desc: RenderDesc) -> int:
-    """U of a whole-volume GMM render (synchronous)"""
-    return int(check(_lib.load().vr_gmm_count_footprint(ctypes.byref(desc))))
+def gmm_count_footprint(desc: RenderDesc, slab: Optional[_lib.GmmSlab] = None) -> int:
+    """U of a whole-volume GMM render, or of one slab of a chain (synchronous)"""
+    L = _lib.load()
+    if slab is None:
+        return int(check(L.vr_gmm_count_footprint(ctypes.byref(desc))))
+    return int(check(L.vr_gmm_count_footprint_slab(ctypes.byref(desc), ctypes.byref(slab))))
 
 
 def version() -> str:

@@ -1921,6 +1921,9 @@ int fill_gmm_params(const vr_render_desc *d, const vr_gmm_slab *slab, vr::Params
         if (!slab->d_rays_out || !slab->d_n_rays_out)
             return fail(VR_ERR_ARG, "a slab launch needs d_rays_out and d_n_rays_out");
         if (slab->n_rays_in && !slab->d_rays_in) return fail(VR_ERR_ARG, "d_rays_in is null");
+        if ((uint64_t)slab->n_rays_in > (uint64_t)d->width * d->height)
+            return fail(VR_ERR_ARG, "%u alive rays in for a %ux%u frame", slab->n_rays_in,
+                        d->width, d->height);
         // slabs must be taken in the order every ray crosses them: the sign of
         // a ray's z step is that of the linear form u M8 + v M9 - 2 M10, so the
         // four frame corners decide whether it is the same for the whole frame
@@ -2063,11 +2066,16 @@ int vr_render_gmm(const vr_render_desc *desc, const vr_gmm_slab *slab) {
 }
 
 int64_t vr_gmm_count_footprint(const vr_render_desc *desc) {
+    return vr_gmm_count_footprint_slab(desc, nullptr);
+}
+
+int64_t vr_gmm_count_footprint_slab(const vr_render_desc *desc, const vr_gmm_slab *slab) {
     vr::Params P;
     uint32_t nblocks = 0;
-    int rc = fill_gmm_params(desc, nullptr, P, nblocks);
+    int rc = fill_gmm_params(desc, slab, P, nblocks);
     if (rc != VR_OK) return rc;
-    const uint64_t nvox = (uint64_t)g.gmm.nx * g.gmm.ny * g.gmm.nz;
+    // one bit per resident voxel (gmm_vox indexes the resident slices)
+    const uint64_t nvox = (uint64_t)g.gmm.nx * g.gmm.ny * (uint64_t)g.gmm.nzs;
     const uint64_t nwords = (nvox + 63) / 64;
     unsigned long long *bits = nullptr;
     VR_HIP(hipMalloc(&bits, nwords * 8 + 8));

@@ -194,7 +194,11 @@ __device__ __forceinline__ void gmm_emit(const Params &P, const GmmState &s, uin
         base = atomicAdd(P.n_rays_out, (uint32_t)__popcll(out));
     base = __shfl(base, __builtin_ctzll(out), 64);
     const uint32_t k = base + (uint32_t)__popcll(out & ((1ull << (lane & ~(uint32_t)(L - 1))) - 1ull));
-    if (sub < 3) {
+    // the list's capacity (include/vr.h): no slab emits more rays than enter
+    // it, so only a counter the caller did not zero reaches it -- such entries
+    // are dropped (the count still says how many), never written past the end
+    const uint64_t cap = P.rays_in ? (uint64_t)P.n_rays_in : (uint64_t)P.W * P.H;
+    if (sub < 3 && (uint64_t)k < cap) {
         uint4 v;
         if (sub == 0) v = make_uint4(__float_as_uint(s.sx), __float_as_uint(s.sy),
                                      __float_as_uint(s.sz), __float_as_uint(s.sw));
