@@ -138,6 +138,10 @@ def parse():
                          "events; reports per-slab ms and the pipeline-period estimate")
     ap.add_argument("--rehearsal-ranks", type=int, default=8,
                     help="--slab-rehearsal: slabs (ranks) of the chain (BASELINE config 5: 8)")
+    ap.add_argument("--rebalance", type=int, default=2,
+                    help="GMM z-slabs (N > 1 and --slab-rehearsal): cost-balancing passes "
+                         "after the equal cut (each: one untimed frame, slabs re-cut by its "
+                         "per-slab costs and regenerated)")
     ap.add_argument("--cpu-row-stride", type=int, default=0,
                     help="CPU baseline renders every k-th row (0 = auto)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -422,12 +426,16 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
 
     pkg.free_gmm()
     torch.cuda.empty_cache()
-    equal = pkg.slabs.slab_bounds(n, R, direction)
-    rows_eq = chain(equal, "equal")
+    bounds = pkg.slabs.slab_bounds(n, R, direction)
+    rows_eq = rows = chain(bounds, "equal")
     free_now, _ = torch.cuda.mem_get_info(dev)
     cap = pkg.slabs.max_slices_for(n, n, K, free_now)
-    balanced = pkg.slabs.bounds_by_cost(n, R, direction, equal, [r["ms"] for r in rows_eq], cap)
-    rows_bal = chain(balanced, "balanced")
+    passes = [max(r["ms"] for r in rows)]
+    for p in range(args.rebalance):
+        bounds = pkg.slabs.bounds_by_cost(n, R, direction, bounds, [r["ms"] for r in rows], cap)
+        rows = chain(bounds, f"balanced {p + 1}")
+        passes.append(max(r["ms"] for r in rows))
+    rows_bal = rows
     period = max(r["ms"] for r in rows_bal)
     kernel = pkg.last_kernel()
     worst = max(rows_bal, key=lambda r: r["ms"])
@@ -461,6 +469,7 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
                       f"{args.steps} frames after {args.warmup} warm-up)",
             "slabs_equal": rows_eq,
             "slabs_balanced": rows_bal,
+            "period_ms_per_pass": [round(v, 4) for v in passes],
         },
         "roofline": {
             "bound": "hbm", "achieved": worst.get("GBps"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -592,29 +601,33 @@ def main_gmm(args):
         # front-loads the work, so one frame on equal slabs measures every rank's
         # march, and all ranks re-cut the slabs by those costs (largest slab cost
         # minimised, each slab within the smallest rank's free HBM), then
-        # generate their new slab (slabs.bounds_by_cost).
-        step(True)
-        drain()
-        ms = ev[-1][0].elapsed_time(ev[-1][1])
-        ev.clear()
-        alive.clear()
-        pkg.free_gmm()
-        free_now, _ = torch.cuda.mem_get_info(dev)
-        cdev = dev if args.dist_backend == "nccl" else "cpu"
-        costs = torch.zeros(world, dtype=torch.float64, device=cdev)
-        costs[rank] = ms
-        dist.all_reduce(costs)
-        cap = torch.tensor([pkg.slabs.max_slices_for(n, n, K, free_now)], dtype=torch.int64,
-                           device=cdev)
-        dist.all_reduce(cap, op=dist.ReduceOp.MIN)
+        # generate their new slab (slabs.bounds_by_cost).  --rebalance passes: the
+        # cut assumes a uniform cost inside each measured slab, so a second pass
+        # on the first cut's costs tightens it (the one-GPU rehearsal of config 5:
+        # period 6.44 ms equal, 4.51 after one pass; profiles/r05).
         direction = pkg.slabs.march_direction(m, W, H)
-        bounds = pkg.slabs.bounds_by_cost(n, world, direction,
-                                          pkg.slabs.slab_bounds(n, world, direction),
-                                          costs.cpu().tolist(), int(cap.item()))
-        z_lo, z_hi = bounds[rank]
-        zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
-        pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
-        torch.cuda.synchronize()
+        bounds = pkg.slabs.slab_bounds(n, world, direction)
+        for _ in range(max(args.rebalance, 1)):
+            step(True)
+            drain()
+            ms = ev[-1][0].elapsed_time(ev[-1][1])
+            ev.clear()
+            alive.clear()
+            pkg.free_gmm()
+            free_now, _ = torch.cuda.mem_get_info(dev)
+            cdev = dev if args.dist_backend == "nccl" else "cpu"
+            costs = torch.zeros(world, dtype=torch.float64, device=cdev)
+            costs[rank] = ms
+            dist.all_reduce(costs)
+            cap = torch.tensor([pkg.slabs.max_slices_for(n, n, K, free_now)], dtype=torch.int64,
+                               device=cdev)
+            dist.all_reduce(cap, op=dist.ReduceOp.MIN)
+            bounds = pkg.slabs.bounds_by_cost(n, world, direction, bounds, costs.cpu().tolist(),
+                                              int(cap.item()))
+            z_lo, z_hi = bounds[rank]
+            zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
+            pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
+            torch.cuda.synchronize()
         balanced = True
     # U before the warm-up (as in main(): the counting pass warms clocks and translation)
     u = pkg.gmm_count_footprint(desc) if world == 1 else None
@@ -678,7 +691,7 @@ def main_gmm(args):
                                                           if args.dist_backend == "nccl"
                                                           else "gloo host staging")),
                 "slab": [z_lo, z_hi],
-                "slab_cut": (None if world == 1 else "measured cost (one untimed frame)"
+                "slab_cut": (None if world == 1 else f"measured cost ({max(args.rebalance, 1)} untimed frame(s))"
                              if balanced else "equal"),
                 "alive_rays_out_rank0": int(np.mean(alive)) if alive else None,
             },

@@ -44,6 +44,13 @@ def main():
                     help="only the ring-8 loop on one vs two alternating render streams")
     ap.add_argument("--priority", type=int, default=0,
                     help="torch stream priority of the render stream (-1 = high)")
+    ap.add_argument("--all-ranks", action="store_true",
+                    help="replay EVERY rank's frame loop as bench.py runs it (ring 8, a wait "
+                         "every 8 frames, two render streams, host included): each rank's "
+                         "frame period, the max over ranks and full frame / max.  Rank 0 also "
+                         "copies N - 1 staged peer buffers into its gather target per frame "
+                         "(device copies standing in for the xGMI receive: a lower bound of "
+                         "its traffic) before the unscatter")
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", args.port)
@@ -159,6 +166,8 @@ def main():
         torch.cuda.synchronize()
         return dt
 
+    if args.all_ranks:
+        return all_ranks(args, pkg, torch, dist, dev, lists, m, W, H, N, slots, frame)
     print(f"{args.config} {args.camera} m{args.method}, rank 0 of {N}: {slots} slots "
           f"({slots * 256} rays), one-rank NCCL group, GPU_MAX_HW_QUEUES="
           f"{os.environ.get('GPU_MAX_HW_QUEUES', '(unset)')}, render stream priority "
@@ -222,6 +231,91 @@ def main():
         else:
             print(f"  live [{what}]: host issue {issue:.4f} ms/frame, frame period {period:.4f} ms"
                   f"  (full frame / period = {t_full / period:.2f}x)", flush=True)
+    dist.destroy_process_group()
+
+
+def all_ranks(args, pkg, torch, dist, dev, lists, m, W, H, N, slots, frame):
+    """Every rank's bench.py N > 1 frame loop in turn on this GPU (tools/host_cost.py
+    --all-ranks): the max over ranks of the live frame period, host issue included."""
+    RING, STREAMS = 8, 2
+    rs_list = [torch.cuda.Stream(device=dev) for _ in range(STREAMS)]
+    assemble = torch.cuda.Stream(device=dev)
+    all_lists = torch.from_numpy(lists.view(np.int32).copy()).to(dev)
+    recvN = [torch.zeros((N, slots * 256), dtype=torch.int32, device=dev) for _ in range(RING)]
+    peers = torch.zeros((N, slots * 256), dtype=torch.int32, device=dev)  # staged peer buffers
+    recv1 = [torch.empty((1, slots * 256), dtype=torch.int32, device=dev) for _ in range(RING)]
+    fdesc = pkg.make_desc(frame, W, H, m, query_method=args.method)
+    st = rs_list[0]
+    pkg.set_stream(st)
+
+    def full_period(k):
+        with torch.cuda.stream(st):
+            for _ in range(k):
+                frame.zero_()
+                pkg.render(fdesc)
+        torch.cuda.synchronize()
+    full_period(40)
+    t0 = time.perf_counter()
+    full_period(100)
+    t_full = (time.perf_counter() - t0) * 10.0
+    print(f"{args.config} {args.camera} m{args.method}: full frame (N = 1 loop, "
+          f"{pkg.last_kernel()}) period {t_full:.4f} ms; N = {N}, {slots} slots per rank, "
+          f"ring {RING}, {STREAMS} render streams, one-rank NCCL gather per frame", flush=True)
+    per = []
+    for r in range(N):
+        with torch.cuda.stream(st):
+            mine = torch.from_numpy(lists[r].view(np.int32).copy()).to(dev)
+            packed = [torch.zeros(slots * 256, dtype=torch.int32, device=dev) for _ in range(RING)]
+            descs = [pkg.make_desc(packed[b], W, H, m, query_method=args.method, d_tile_list=mine,
+                                   n_tiles=slots) for b in range(RING)]
+        torch.cuda.synchronize()
+        works, assembled = [None] * RING, [None] * RING
+        nframe = [0]
+
+        def step():  # bench.py step() at N > 1 for rank r
+            f = nframe[0]
+            b, rs = f % RING, rs_list[f % STREAMS]
+            nframe[0] += 1
+            pkg.set_stream(rs)
+            if f % RING == 0 and f > 0:
+                w = (f - 1) % RING
+                for s_ in rs_list:
+                    with torch.cuda.stream(s_):
+                        if works[w] is not None:
+                            works[w].wait()
+                        if assembled[w] is not None:
+                            s_.wait_event(assembled[w])
+            with torch.cuda.stream(rs):
+                pkg.render(descs[b])
+                works[b] = dist.gather(packed[b], gather_list=list(recv1[b].unbind(0)), dst=0,
+                                       async_op=True)
+            if r == 0:
+                with torch.cuda.stream(assemble):
+                    works[b].wait()
+                    for j in range(1, N):  # the N - 1 peers' buffers arriving
+                        recvN[b][j].copy_(peers[j])
+                    pkg.set_stream(assemble)
+                    pkg.unscatter_tiles(recvN[b], all_lists, N, slots, frame, W, H)
+                    pkg.set_stream(rs)
+                    done = torch.cuda.Event()
+                    done.record(assemble)
+                    assembled[b] = done
+
+        for _ in range(50):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.frames):
+            step()
+        issue = (time.perf_counter() - t0) / args.frames * 1e3
+        torch.cuda.synchronize()
+        period = (time.perf_counter() - t0) / args.frames * 1e3
+        per.append(period)
+        print(f"  rank {r}: host issue {issue:.4f} ms/frame, frame period {period:.4f} ms "
+              f"({pkg.last_kernel()})", flush=True)
+    worst = max(per)
+    print(f"  N = {N}: max over ranks {worst:.4f} ms (rank {per.index(worst)}) -> "
+          f"full frame / max = {t_full / worst:.2f}x", flush=True)
     dist.destroy_process_group()
 
 

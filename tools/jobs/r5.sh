@@ -28,6 +28,11 @@ gmm5)  # BASELINE config 5 rehearsed on one GPU: every slab of the 8-slab chain 
   tail -2 $O/pytest.log
   timeout -k 10 1000 python -u bench.py --config gmm2048 --slab-rehearsal --steps 5 --warmup 1 > $O/bench.log 2>&1; guard $? gmm5 $O/bench.log
   grep '^{' $O/bench.log | cut -c1-600 ;;
+ranks)  # every rank's bench.py frame loop replayed: max over ranks, host + staged peer copies in
+  for CAM in C0 C1; do for N in 2 4 8; do
+    timeout -k 10 300 python -u tools/host_cost.py --camera $CAM --world $N --all-ranks --frames 300 > $O/all_ranks_${CAM}_N$N.log 2>&1; guard $? ranks-$CAM-$N $O/all_ranks_${CAM}_N$N.log
+    grep "max over" $O/all_ranks_${CAM}_N$N.log
+  done; done ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
