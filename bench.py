@@ -324,7 +324,9 @@ def balanced_lists(pkg, lists, world, rank, W, H, m, method, dev, stream, backen
     if backend == "nccl":
         cost = cost.to(dev)
     dist.all_reduce(cost)
-    return pkg.tiles.tile_lists_by_cost(W, H, world, cost.cpu().numpy())
+    share = np.ones(world)
+    share[0] = pkg.tiles.rank0_share(world)  # rank 0 also receives and assembles the frame
+    return pkg.tiles.tile_lists_by_cost(W, H, world, cost.cpu().numpy(), share=share)
 
 
 def gmm_cpu_baseline(m, method, W, H, K):

@@ -208,6 +208,32 @@ def test_cost_lists_balance_ranks_and_xcds(pkg, world):
                 assert np.all(np.diff(blk) <= 0)
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_cost_lists_rank0_share(pkg, world):
+    """a work share below 1 for rank 0 (it also assembles the frame) gives its bins
+    proportionally less cost at the same block counts (equal-size gathers), every
+    tile still dealt once; the other ranks stay balanced"""
+    T = pkg.tiles
+    W, H = 1920, 1080
+    cost = _synthetic_cost(pkg, W, H, seed=world)
+    sh = T.rank0_share(world)
+    assert 0.5 <= sh < 1.0 and T.rank0_share(1) == 1.0
+    share = np.ones(world)
+    share[0] = sh
+    lists = T.tile_lists_by_cost(W, H, world, cost, share=share)
+    real = lists[lists != T.PAD]
+    assert sorted(real.tolist()) == list(range(T.tiles_x(W) * T.tiles_y(H)))
+    eq = T.tile_lists_by_cost(W, H, world, cost)
+    # one slot count for every rank (the gather stays equal-size), within a block
+    # row of the equal deal's (short edge blocks may gather in rank 0's sublists)
+    assert lists.shape[0] == world and abs(lists.shape[1] - eq.shape[1]) <= T.XCDS * T.BLOCK_Y
+    loads = _bin_loads(T, lists, cost).sum(axis=1)
+    assert abs(loads[0] / loads[1:].mean() - sh) < 0.02
+    assert loads[1:].max() / loads[1:].min() < 1.01
+    with pytest.raises(ValueError):
+        T.tile_lists_by_cost(W, H, world, cost, share=np.zeros(world))
+
+
 def test_tile_costs_from_steps(pkg):
     """per wave (64-pixel row): longest ray + 2; misses (-1) cost 1; PAD slots skipped;
     the full-frame form agrees with the packed form"""

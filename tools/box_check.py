@@ -6,7 +6,9 @@ boxcheck:-DVR_BOX_CHECK; VRDD_LIB points the package at it): every frame of
 k_march (VR_DUO=0) and k_march_duo (VR_DUO=2/3/4 samples per box), methods 1-3,
 is rendered with the library's violation counters on (vr_debug_box_check) and
 compared with the default dispatch's frame of the same view.  A violating read
-is counted and skipped by the checking build, never performed.
+is counted and skipped by the checking build, never performed.  Also printed:
+the box voxels and lane slots the frame decoded, as multiples of U (the
+distinct voxels under the footprints, vr_count_footprint).
 
   VRDD_LIB=tools/build/variants/boxcheck/libvr.so python tools/box_check.py
 """
@@ -30,12 +32,13 @@ def main():
     import bench
     pkg = g.load_package()
     L = pkg._lib.load()
-    ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ctr = torch.zeros(6, dtype=torch.int64, device="cuda")
     checking = L.vr_debug_box_check(ctypes.c_void_p(ctr.data_ptr()))
     print(f"library {pkg.LIB_PATH}: checking build {bool(checking)}", flush=True)
     if not checking:
         raise SystemExit("not a -DVR_BOX_CHECK build: nothing would be counted")
     bad_total = 0
+    us = {}
     for spec in args.configs.split(","):
         cfg, cam = spec.split(":")
         n, nb, W, H = bench.CONFIGS[cfg]
@@ -61,9 +64,14 @@ def main():
                 c = ctr.cpu().tolist()
                 same = torch.equal(out, ref)
                 bad_total += c[0] + c[2] + (0 if same else 1)
+                u = us.get((cfg, cam, method))
+                if u is None:
+                    u = us[(cfg, cam, method)] = pkg.count_footprint(
+                        pkg.make_desc(out, W, H, m, query_method=method))
                 print(f"{cfg} {cam} m{method} VR_DUO={duo} {pkg.last_kernel():28s} "
                       f"violations {c[0]} (worst over {c[1]}) boxes outside the volume {c[2]} "
-                      f"frame {'identical to' if same else 'DIFFERS from'} {ref_kernel}",
+                      f"frame {'identical to' if same else 'DIFFERS from'} {ref_kernel}; "
+                      f"decoded {c[3] / u:.3f} U, slots {c[4] / u:.3f} U (U = {u})",
                       flush=True)
         pkg.clear_tuning()
     L.vr_debug_box_check(None)

@@ -51,6 +51,9 @@ def main():
                          "copies N - 1 staged peer buffers into its gather target per frame "
                          "(device copies standing in for the xGMI receive: a lower bound of "
                          "its traffic) before the unscatter")
+    ap.add_argument("--rank0-share", type=float, default=-1.0,
+                    help="rank 0's work share in the cost dealing (bench.py: tiles.rank0_share; "
+                         "-1 = that default, 1 = equal shares)")
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", args.port)
@@ -73,8 +76,11 @@ def main():
     full = torch.zeros(W * H, dtype=torch.int32, device=dev)
     steps = torch.full((W * H,), -1, dtype=torch.int32, device=dev)
     pkg.render(pkg.make_desc(full, W, H, m, query_method=args.method, d_steps=steps))
+    share = np.ones(N)
+    share[0] = pkg.tiles.rank0_share(N) if args.rank0_share < 0 else args.rank0_share
     lists = pkg.tiles.tile_lists_by_cost(W, H, N, pkg.tiles.tile_costs_from_frame(
-        steps.cpu().numpy(), W, H))
+        steps.cpu().numpy(), W, H), share=share)
+    print(f"rank 0 work share {share[0]:.4f}", flush=True)
     slots = lists.shape[1]
     stream = torch.cuda.Stream(device=dev, priority=args.priority)
     assemble = torch.cuda.Stream(device=dev)

@@ -33,6 +33,21 @@ ranks)  # every rank's bench.py frame loop replayed: max over ranks, host + stag
     timeout -k 10 300 python -u tools/host_cost.py --camera $CAM --world $N --all-ranks --frames 300 > $O/all_ranks_${CAM}_N$N.log 2>&1; guard $? ranks-$CAM-$N $O/all_ranks_${CAM}_N$N.log
     grep "max over" $O/all_ranks_${CAM}_N$N.log
   done; done ;;
+compact)  # slice-compacted duo boxes: parity, bound check, config-3 timing; rank-0 share replay
+  timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "duo or every_kernel_path or midsize" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -2 $O/pytest.log
+  VRDD_LIB=tools/build/variants/boxcheck/libvr.so timeout -k 10 300 python -u tools/box_check.py > $O/box_check.log 2>&1; guard $? boxcheck $O/box_check.log
+  tail -1 $O/box_check.log
+  for M in 1 2; do
+    timeout -k 10 400 python -u tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method $M --rounds 5 --env "" "VR_DUO=0" "VR_DUO=3" "VR_DUO=4" > $O/variants_512x8_m$M.log 2>&1; guard $? var $O/variants_512x8_m$M.log
+    grep -v "round\|amdgpu.ids" $O/variants_512x8_m$M.log
+  done
+  timeout -k 10 400 python -u tools/bench_variants.py --variants main --config 256x4@512x512 --cameras C0 --method 1 --rounds 5 --env "" "VR_DUO=0" > $O/variants_256x4.log 2>&1; guard $? var $O/variants_256x4.log
+  grep -v "round\|amdgpu.ids" $O/variants_256x4.log
+  for CAM in C0 C1; do for N in 4 8; do
+    timeout -k 10 300 python -u tools/host_cost.py --camera $CAM --world $N --all-ranks --frames 300 > $O/all_ranks_${CAM}_N$N.log 2>&1; guard $? ranks $O/all_ranks_${CAM}_N$N.log
+    grep "max over" $O/all_ranks_${CAM}_N$N.log
+  done; done ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done

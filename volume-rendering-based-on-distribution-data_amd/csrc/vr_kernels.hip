@@ -153,20 +153,23 @@ __device__ __forceinline__ void mark_foot(const Params &P, const Foot &f) {
 
 // NG groups of 64 box voxels from position p0: all NG loads issue before the
 // first decode waits on them
-template <int B, int M, int NG>
+// ZT: the box's slices are a subset of its z range (k_march_duo, slice_table):
+// slot z of the box holds slice (ztab >> 4 z) & 15 of the range
+template <int B, int M, int NG, bool ZT = false>
 __device__ __forceinline__ void box_chunk(const float *__restrict__ vbase, const Params &P,
                                           float *box, int dx, int dxy, int V, uint32_t lane,
                                           int p0, float rdx, float rdxy, const LogEnt *tab,
-                                          float *st) {
+                                          float *st, uint64_t ztab = 0) {
     const uint32_t sy = (uint32_t)P.sy;
     float rec[NG][B];
 #pragma unroll
     for (int g = 0; g < NG; g++) {
         const int p = min(p0 + g * 64 + (int)lane, V - 1);
-        const int z = (int)(((float)p + 0.5f) * rdxy);
-        const int r = p - z * dxy;
+        const int zs = (int)(((float)p + 0.5f) * rdxy);
+        const int r = p - zs * dxy;
         const int y = (int)(((float)r + 0.5f) * rdx);
         const int x = r - y * dx;
+        const int z = ZT ? (int)((ztab >> (4 * zs)) & 15u) : zs;
         const uint64_t off = (uint64_t)(uint32_t)z * P.sz + (uint32_t)(y * sy + x);
         if constexpr (B == 16 || B == 32) {
             // wide records: the quad loads its 4 lanes' records as contiguous
@@ -219,10 +222,17 @@ __device__ __forceinline__ void box_chunk(const float *__restrict__ vbase, const
 // back-to-back before the first decode waits on them.  A chunk takes only the
 // 64-voxel groups the box still needs (wave-uniform): a 140-voxel box decodes
 // 192 slots, not 256 (512^3 x 8 at 1080p: boxes of ~130-210 voxels).
-template <int B, int M>
+template <int B, int M, bool ZT = false>
 __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, const Params &P,
                                            float *box, int dx, int dxy, int V, uint32_t lane,
-                                           const LogEnt *tab, float *st) {
+                                           const LogEnt *tab, float *st, uint64_t ztab = 0) {
+#ifdef VR_BOX_CHECK
+    // decode counts of the frame: box voxels and lane slots (64 per group) decoded
+    if (lane == 0 && P.box_check) {
+        atomicAdd(P.box_check + 3, (unsigned long long)V);
+        atomicAdd(P.box_check + 4, (unsigned long long)((V + 63) / 64 * 64));
+    }
+#endif
     constexpr int G0 = B >= 32 ? 1 : (B >= 16 ? 2 : 4);
     constexpr int G = G0 < VR_BOX_G ? G0 : VR_BOX_G;  // voxels per lane in flight
     // hardware reciprocals (1 ulp) instead of two IEEE divisions per wave-step:
@@ -233,13 +243,13 @@ __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, cons
     for (int p0 = 0; p0 < V; p0 += 64 * G) {
         const int left = V - p0;  // wave-uniform
         if (G >= 4 && left > 192)
-            box_chunk<B, M, (G >= 4 ? 4 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
+            box_chunk<B, M, (G >= 4 ? 4 : 1), ZT>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st, ztab);
         else if (G >= 3 && left > 128)
-            box_chunk<B, M, (G >= 3 ? 3 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
+            box_chunk<B, M, (G >= 3 ? 3 : 1), ZT>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st, ztab);
         else if (G >= 2 && left > 64)
-            box_chunk<B, M, (G >= 2 ? 2 : 1)>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
+            box_chunk<B, M, (G >= 2 ? 2 : 1), ZT>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st, ztab);
         else
-            box_chunk<B, M, 1>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st);
+            box_chunk<B, M, 1, ZT>(vbase, P, box, dx, dxy, V, lane, p0, rdx, rdxy, tab, st, ztab);
     }
 }
 
@@ -253,15 +263,16 @@ __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, cons
 // reads, ((z1 - bz0) dy + (y1 - by0)) dx + (x1 - bx0), below the box's dx dy dz
 // voxels (those the decode wrote this step), and the box inside the volume.  A
 // violating read is counted and skipped (its sample is 0), never performed.
+// hi: the largest box index the lane reads, V: the voxels decoded this step
+// (dx dy dz, or dx dy x the used slices of a slice-compacted box)
 __device__ __forceinline__ bool box_ok(const Params &P, const Foot &f, int bx0, int by0, int bz0,
-                                       int dx, int dy, int dz) {
-    const int hi = ((f.z1 - bz0) * dy + (f.y1 - by0)) * dx + (f.x1 - bx0);
+                                       int dx, int dy, int dz, int hi, int V) {
     const bool ok = f.x0 >= bx0 && f.y0 >= by0 && f.z0 >= bz0 && f.x1 >= f.x0 &&
                     f.y1 >= f.y0 && f.z1 >= f.z0 && f.x1 < bx0 + dx && f.y1 < by0 + dy &&
-                    f.z1 < bz0 + dz && hi < dx * dy * dz && dx * dy * dz <= P.box_max;
+                    f.z1 < bz0 + dz && hi < V && V <= P.box_max;
     if (!ok && P.box_check) {
         atomicAdd(P.box_check, 1ull);
-        const long long over = (long long)hi + 1 - (long long)dx * dy * dz;
+        const long long over = (long long)hi + 1 - (long long)V;
         if (over > 0) atomicMax(P.box_check + 1, (unsigned long long)over);
     }
     return ok;
@@ -352,7 +363,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #ifdef VR_BOX_CHECK
-                    if (alive && box_ok(P, f, bx0, by0, bz0, dx, dy, dz)) {
+                    if (alive && box_ok(P, f, bx0, by0, bz0, dx, dy, dz,
+                                        ((f.z1 - bz0) * dy + (f.y1 - by0)) * dx + (f.x1 - bx0),
+                                        dx * dy * dz)) {
 #else
                     if (alive) {
 #endif
@@ -401,6 +414,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
     }
     write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
                 sw * P.brightness);
+}
+
+// OR over the 64 lanes (DPP row shifts, then row broadcasts; lane 63 holds it)
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    int x = (int)v;
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+
+// the used slices of a box's z range (bit z of mask) packed as 4-bit offsets,
+// slot s -> slice (table >> 4 s) & 15 (wave-uniform; ranges of <= 16 slices)
+__device__ __forceinline__ uint64_t slice_table(uint32_t mask) {
+    uint64_t t = 0;
+    int s = 0;
+    for (int z = 0; z < 16; z++)
+        if ((mask >> z) & 1u) t |= (uint64_t)z << (4 * s++);
+    return t;
 }
 
 // ---- the LDS-box march, two samples per box (k_march_duo) ----
@@ -463,6 +498,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
         int lo_z = alive ? f[0].z0 : 0x7FFFFFFF;
         int hi_x = alive ? -f[0].x0 : 0x7FFFFFFF, hi_y = alive ? -f[0].y0 : 0x7FFFFFFF;
         int hi_z = alive ? -f[0].z0 : 0x7FFFFFFF;
+        uint32_t incl = alive ? 1u : 0u;  // the samples whose footprints the box covers
         {
             bool reach = alive;
             float tq = t, qx = px, qy = py, qz = pz;
@@ -475,6 +511,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                 qz = qz + stz;
                 f[k] = footprint(P, qx, qy, qz);
                 if (reach) {
+                    incl |= 1u << k;
                     lo_x = min(lo_x, f[k].x0);
                     lo_y = min(lo_y, f[k].y0);
                     lo_z = min(lo_z, f[k].z0);
@@ -492,16 +529,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
         const int by1 = min(-hi_y + 1, P.ny - 1);
         const int bz1 = min(-hi_z + 1, P.nz - 1);
         const int dx = bx1 - bx0 + 1, dy = by1 - by0 + 1, dz = bz1 - bz0 + 1;
-#ifdef VR_BOX_CHECK
-        const bool staged = dx * dy * dz <= P.box_max && box_in_volume(P, bx0, by0, bz0, dx, dy, dz, lane);
-#else
-        const bool staged = dx * dy * dz <= P.box_max;  // wave-uniform
-#endif
+        // The box keeps only the slices some footprint reads: K samples a step
+        // apart leave slices between them that none does (512^3: a step is
+        // 2.56 slices, so {z, z+1} and {z+3, z+4} skip z+2), whose records the
+        // bounding box would fetch and decode for nothing.  Ranges of <= 16
+        // slices are compacted (slot -> slice through slice_table).
+        const bool compact = dz <= 16;  // wave-uniform
+        uint32_t zmask = (1u << min(dz, 31)) - 1u;
+        uint64_t ztab = 0;
+        if (compact) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                if ((incl >> k) & 1u) m |= (1u << (f[k].z0 - bz0)) | (1u << (f[k].z1 - bz0));
+            zmask = wave_or(m);
+            ztab = slice_table(zmask);
+        }
+        const int nzs = compact ? __builtin_popcount(zmask) : dz;
         const int dxy = dx * dy;
+        const int V = dxy * nzs;
+#ifdef VR_BOX_CHECK
+        const bool staged = V <= P.box_max && box_in_volume(P, bx0, by0, bz0, dx, dy, dz, lane);
+#else
+        const bool staged = V <= P.box_max;  // wave-uniform
+#endif
         if (staged) {
             const float *vbase =
                 vol + ((uint64_t)bz0 * P.sz + (uint64_t)by0 * P.sy + (uint64_t)bx0) * (uint64_t)B;
-            decode_box<B, M>(vbase, P, box, dx, dxy, dxy * dz, lane, tab, st);
+            if (compact)
+                decode_box<B, M, true>(vbase, P, box, dx, dxy, V, lane, tab, st, ztab);
+            else
+                decode_box<B, M>(vbase, P, box, dx, dxy, V, lane, tab, st);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -512,14 +570,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
             if (alive) {
                 const Foot &fk = f[k];
                 float sample = 0.0f;
+                // the footprint's slices z0, z1 (= z0 or z0 + 1) sit in adjacent slots
+                const int zs0 = compact ? __builtin_popcount(zmask & ((1u << (fk.z0 - bz0)) - 1u))
+                                        : fk.z0 - bz0;
+                const int b0 = (zs0 * dy + (fk.y0 - by0)) * dx + (fk.x0 - bx0);
+                const int ox = fk.x1 - fk.x0, oy = (fk.y1 - fk.y0) * dx;
+                const int oz = (fk.z1 - fk.z0) * dxy;
 #ifdef VR_BOX_CHECK
-                if (staged && !box_ok(P, fk, bx0, by0, bz0, dx, dy, dz)) {
+                if (staged && !(box_ok(P, fk, bx0, by0, bz0, dx, dy, dz, b0 + oz + oy + ox, V) &&
+                                ((zmask >> (fk.z0 - bz0)) & (zmask >> (fk.z1 - bz0)) & 1u))) {
                 } else
 #endif
                 if (staged) {
-                    const int b0 = ((fk.z0 - bz0) * dy + (fk.y0 - by0)) * dx + (fk.x0 - bx0);
-                    const int ox = fk.x1 - fk.x0, oy = (fk.y1 - fk.y0) * dx;
-                    const int oz = (fk.z1 - fk.z0) * dxy;
                     float sv[8];
                     sv[0] = box[b0];
                     sv[1] = box[b0 + ox];

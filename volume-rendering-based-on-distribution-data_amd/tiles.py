@@ -154,8 +154,19 @@ def tile_costs_from_frame(steps, width: int, height: int) -> np.ndarray:
     return tile_costs_from_steps(packed, np.arange(tx * ty, dtype=np.uint32), tx * ty)
 
 
+def rank0_share(world_size: int) -> float:
+    """Rank 0's share of the render work relative to the other ranks'.  Rank 0
+    also receives the N - 1 peers' tile buffers and assembles the frame (the
+    unscatter, on its own stream beside the next render): replaying every rank's
+    bench.py frame loop on one GPU (tools/host_cost.py --all-ranks, 1024^3 x 8)
+    put rank 0 ~0.02 ms per frame behind the others at every N (N = 8 C0: 0.210
+    vs 0.185-0.192 ms; C1 0.460 vs 0.430-0.444), a fixed cost that is a larger
+    fraction of a rank's frame as N grows."""
+    return 1.0 if world_size <= 1 else max(0.5, 1.0 - 0.0125 * world_size)
+
+
 def tile_lists_by_cost(width: int, height: int, world_size: int, cost,
-                       block=(BLOCK_X, BLOCK_Y)) -> np.ndarray:
+                       block=(BLOCK_X, BLOCK_Y), share=None) -> np.ndarray:
     """Like tile_lists, but dealt by measured per-tile costs (tile_costs_from_steps
     summed over the ranks of a previous frame of the same view).
 
@@ -165,7 +176,10 @@ def tile_lists_by_cost(width: int, height: int, world_size: int, cost,
     (equal-size gathers) and work is balanced over all 8*world XCDs, not only
     over ranks.  A bin's blocks stay in dealing order, i.e. longest first.
     Each rank's 8 XCD sublists are PAD-padded to one length before they are
-    interleaved, so list entry 8*k + g is always the k-th tile of XCD g."""
+    interleaved, so list entry 8*k + g is always the k-th tile of XCD g.
+    share: per-rank work weights (None = equal): a bin's load is compared as
+    load / share of its rank, so a rank with share < 1 ends with the same block
+    count but cheaper blocks (rank0_share: rank 0 also assembles the frame)."""
     tx, ty = tiles_x(width), tiles_y(height)
     BX, BY = int(block[0]), int(block[1])  # tiles per block (tooling sweeps other shapes)
     cost = np.asarray(cost, dtype=np.int64).reshape(ty, tx)
@@ -180,11 +194,14 @@ def tile_lists_by_cost(width: int, height: int, world_size: int, cost,
     load = np.zeros(nbins, dtype=np.int64)
     count = np.zeros(nbins, dtype=np.int64)
     members = [[] for _ in range(nbins)]
-    big = np.iinfo(np.int64).max
+    w = np.ones(world_size) if share is None else np.asarray(share, dtype=np.float64)
+    if w.shape != (world_size,) or not np.all(w > 0):
+        raise ValueError(f"share must hold {world_size} positive weights")
+    wbin = w[np.arange(nbins) % world_size]  # bin g * world_size + r belongs to rank r
     n_plus = 0
     for b in order:
         room = (count < lo) | ((count == lo) & (n_plus < extra))
-        best = int(np.argmin(np.where(room, load, big)))
+        best = int(np.argmin(np.where(room, load / wbin, np.inf)))
         n_plus += int(count[best] == lo)
         load[best] += bcost[b]
         count[best] += 1
