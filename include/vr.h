@@ -317,13 +317,15 @@ const char *vr_last_kernel(void);
  * (segmented).  d_buf must hold 48 * n_slots values.  nullptr turns it off. */
 int vr_debug_wave_clock(uint64_t *d_buf);
 
-/* Tooling: while d_buf (4 x uint64 device memory, caller-zeroed) is non-null, a
+/* Tooling: while d_buf (6 x uint64 device memory, caller-zeroed) is non-null, a
  * library built with -DVR_BOX_CHECK counts the LDS-box bound violations of the
  * staged marches (k_march, k_march_duo): d_buf[0] = reads whose box index or
  * footprint falls outside the wave's box (each such read is skipped),
  * d_buf[1] = the largest box index + 1 - box voxels seen, d_buf[2] = box
- * voxels of a box whose far corner lies outside the volume.  Returns 1 for a
- * checking build, 0 for the default build (which counts nothing). */
+ * voxels of a box whose far corner lies outside the volume; and the decode
+ * work: d_buf[3] = box voxels decoded, d_buf[4] = lane slots spent on them
+ * (64 per group).  Returns 1 for a checking build, 0 for the default build
+ * (which counts nothing). */
 int vr_debug_box_check(uint64_t *d_buf);
 
 /* Device self-test: compares the entropy decode's fast float logarithms (the

@@ -48,6 +48,9 @@ class _Tuning:
     def set(self, key, value):
         self.pkg.set_tuning(key, value)
 
+    def clear(self, key):
+        self.pkg.set_tuning(key, None)
+
 
 @pytest.fixture
 def tune(pkg):

@@ -86,7 +86,8 @@ def test_baked_render_parity(pkg, orc, gpu, baked, nb):
             got = gpu_render(pkg, None, 96, 72, m, method, torch)
             ref = orc.render(vol, orc.make_params(96, 72, m, query_method=method))[:3]
             assert_parity(got, ref, f"baked 24x20x16x{nb} {cam} m{method}")
-            want = "k_march_pipe<B=1,M=0>" if cam == "C0" else "k_march_seg4<B=1,M=0>"
+            # oblique views read the plane's 8 x 2 x 2 brick copy (round 5)
+            want = "k_march_pipe<B=1,M=0>" if cam == "C0" else "k_march_seg4_plane8<B=1,M=0>"
             assert pkg.last_kernel() == want, pkg.last_kernel()
 
 
@@ -110,6 +111,56 @@ def test_baked_paths(pkg, orc, gpu, baked, path, env, tune):
             ref = orc.render(vol, orc.make_params(80, 64, cam, query_method=method))[:3]
             assert_parity(got, ref, f"baked path {path} {env} m{method}")
             assert "M=0" in pkg.last_kernel() or "M=-1" in pkg.last_kernel(), pkg.last_kernel()
+
+
+@pytest.mark.parametrize("dims", [(23, 19, 17), (29, 14, 21), (8, 9, 10), (15, 2, 3)])
+def test_baked_plane8_copy(pkg, orc, gpu, baked, dims, tune):
+    """oblique baked frames filter the method's plane in 8 x 2 x 2 bricks (k_plane8,
+    gather8 MODE 6): ragged x (7-voxel brick runs with one apron voxel), odd y and
+    z (a half brick pair at the far edge), methods 1/2/3, several oblique views,
+    full frames through the segmented and the one-lane marches and rank lists,
+    bit-identical to the oracle; VR_PLANE8=0 keeps the 16 x 2 x 1 plane; the copy
+    counts in layout_info and goes with the planes"""
+    import torch
+    vol = orc.synth_volume(*dims, 4)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    W, H = 88, 64
+    for rot in ((30.0, 45.0), (-25.0, 130.0), (60.0, -20.0), (180.0, 33.0)):
+        m = pkg.camera.display_inv_view(rot)
+        for path in ("", "2"):
+            if path:
+                tune.set("VR_PATH", path)
+            else:
+                tune.clear("VR_PATH")
+            for method in (1, 2, 3):
+                got = gpu_render(pkg, None, W, H, m, method, torch)
+                assert "plane8" in pkg.last_kernel(), (rot, path, pkg.last_kernel())
+                ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+                assert_parity(got, ref, f"plane8 {dims} {rot} path {path} m{method}")
+        tune.clear("VR_PATH")
+        lists = pkg.tiles.tile_lists(W, H, 3, m)
+        n_slots = lists.shape[1]
+        dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+        packed = torch.full((3, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        for r in range(3):
+            pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=2, d_tile_list=dl[r],
+                                     n_tiles=n_slots))
+            assert "plane8" in pkg.last_kernel(), pkg.last_kernel()
+        frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        pkg.unscatter_tiles(packed, dl, 3, n_slots, frame, W, H)
+        torch.cuda.synchronize()
+        ref8 = orc.render(vol, orc.make_params(W, H, m, query_method=2), want_float=False,
+                          want_steps=False)[0]
+        assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref8), rot
+    assert pkg.layout_info()["resident_bytes"] > 0
+    tune.set("VR_PLANE8", "0")
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    got = gpu_render(pkg, None, W, H, m, 1, torch)
+    assert "plane8" not in pkg.last_kernel()
+    assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=1))[:3], "plane8 off")
+    pkg.release_stats()
+    assert pkg.layout_info()["resident_bytes"] == 0
 
 
 def test_baked_tile_lists(pkg, orc, gpu, baked):

@@ -150,6 +150,8 @@ def test_full_frame_baked(pkg, orc, gpu, cam):
             assert_parity(got[:3], ref, f"baked 1024x8 {cam} m{method} ({got[3]})")
             if cam == "S":
                 assert "plane_zrows" in got[3], got[3]
+            if cam == "C1":  # the 8 x 2 x 2 brick copy (round 5)
+                assert "plane8" in got[3], got[3]
     finally:
         pkg.release_stats()
 

@@ -33,9 +33,13 @@ ranks)  # every rank's bench.py frame loop replayed: max over ranks, host + stag
     timeout -k 10 300 python -u tools/host_cost.py --camera $CAM --world $N --all-ranks --frames 300 > $O/all_ranks_${CAM}_N$N.log 2>&1; guard $? ranks-$CAM-$N $O/all_ranks_${CAM}_N$N.log
     grep "max over" $O/all_ranks_${CAM}_N$N.log
   done; done ;;
-compact)  # slice-compacted duo boxes: parity, bound check, config-3 timing; rank-0 share replay
-  timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "duo or every_kernel_path or midsize" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+compact)  # slice-compacted duo boxes: parity, bound check, config-3 timing; rank-0 share replay; plane8
+  timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_gpu_baked.py tests/test_gpu_layout.py -k "duo or every_kernel_path or midsize or baked or plane" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
   tail -2 $O/pytest.log
+  timeout -k 10 900 $PYT tests/test_gpu_fullsize.py -k "baked" > $O/pytest_full.log 2>&1; guard $? pytest $O/pytest_full.log
+  tail -2 $O/pytest_full.log
+  timeout -k 10 400 python -u tools/bench_variants.py --variants main --config 1024x8 --baked --cameras C1,C0 --method 1 --rounds 5 --env "" "VR_PLANE8=0" > $O/variants_baked.log 2>&1; guard $? var $O/variants_baked.log
+  grep -v "round\|amdgpu.ids" $O/variants_baked.log
   VRDD_LIB=tools/build/variants/boxcheck/libvr.so timeout -k 10 300 python -u tools/box_check.py > $O/box_check.log 2>&1; guard $? boxcheck $O/box_check.log
   tail -1 $O/box_check.log
   for M in 1 2; do
@@ -48,6 +52,11 @@ compact)  # slice-compacted duo boxes: parity, bound check, config-3 timing; ran
     timeout -k 10 300 python -u tools/host_cost.py --camera $CAM --world $N --all-ranks --frames 300 > $O/all_ranks_${CAM}_N$N.log 2>&1; guard $? ranks $O/all_ranks_${CAM}_N$N.log
     grep "max over" $O/all_ranks_${CAM}_N$N.log
   done; done ;;
+dbg)  # the 512^3 C1 two-sample frame with and without slice compaction
+  VRDD_LIB=tools/build/variants/boxcheck/libvr.so timeout -k 10 300 python -u tools/box_check.py --configs 512x8:C1,512x8:C0 --methods 1 --duos "VR_DUO=2+VR_DUO_COMPACT=0,2,3" > $O/box_check.log 2>&1
+  grep -v amdgpu $O/box_check.log
+  timeout -k 10 300 python -u tools/box_check.py --any-build --configs 512x8:C1 --methods 1 --duos "VR_DUO=2+VR_DUO_COMPACT=0,2" > $O/main.log 2>&1
+  grep -v amdgpu $O/main.log ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done

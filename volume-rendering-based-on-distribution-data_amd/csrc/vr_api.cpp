@@ -91,7 +91,7 @@ struct State {
         float *buf = nullptr;
         int plane = -1;
         uint64_t sy = 0, sz = 0, bytes = 0;
-    } pcopy[2];
+    } pcopy[3];  // [2]: the 8 x 2 x 2 brick copy for oblique views (k_plane8)
     // layout copies (micro-bricks, axis rows): byte budget (vr_set_layout_budget;
     // UINT64_MAX = the default, layout_budget_bytes) and the cost of the last one
     // made (vr_layout_info)
@@ -175,24 +175,26 @@ void release_plane_copy(int i) {
 void release_plane_copies() {
     release_plane_copy(0);
     release_plane_copy(1);
+    release_plane_copy(2);
 }
 
 uint64_t layout_resident() {
-    return g.brick_bytes + g.acopy[0].bytes + g.acopy[1].bytes + g.pcopy[0].bytes + g.pcopy[1].bytes;
+    return g.brick_bytes + g.acopy[0].bytes + g.acopy[1].bytes + g.pcopy[0].bytes + g.pcopy[1].bytes +
+           g.pcopy[2].bytes;
 }
 
 // Room for a layout copy of `bytes`: within the budget (vr_set_layout_budget)
 // next to the copies already resident (less `freed`, a copy the caller would
 // drop first), and HBM keeps max(4 GiB, 5 %) free after it for the caller.
 // The default budget: two copies of the resident record volume (a brick copy
-// and one axis copy, or both axis copies) plus two copies of one baked plane,
+// and one axis copy, or both axis copies) plus three copies of one baked plane,
 // each with 1/8 for the copies' padding -- what one view class plus one change
 // of view needs, not every copy at once (a third record copy replaces one).
 uint64_t layout_budget_bytes() {
     if (g.layout_budget != UINT64_MAX) return g.layout_budget;
     const uint64_t rec = g.vol ? g.sz * (uint64_t)g.nz * g.nb * sizeof(float) : 0;
     const uint64_t plane = g.stats ? g.stats_plane * sizeof(float) : 0;
-    return 2 * (rec + rec / 8) + 2 * (plane + plane / 8);
+    return 2 * (rec + rec / 8) + 3 * (plane + plane / 8);
 }
 
 bool layout_room(uint64_t bytes, uint64_t freed = 0) {
@@ -752,6 +754,8 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         }
     }
     if (P.path != 2 && P.path != 7) P.axis_view = 0;  // 7: the segmented march reads the copy too
+    P.duo_compact = 1;  // k_march_duo: only the slices the footprints read (VR_DUO_COMPACT=0: all)
+    if (const char *e = vr::tuning("VR_DUO_COMPACT")) P.duo_compact = std::atoi(e) != 0;
     if (const char *e = vr::tuning("VR_DUO")) {  // 0 / 1: one sample per box, 2-4: that many
         const int v = std::atoi(e);
         if (v >= 0 && v <= 4) P.duo = v;
@@ -822,8 +826,9 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
 // slower everywhere but 512^3 C1 (within 3 %).  VR_PATH (2 / 7) overrides;
 // P.seg_lanes keeps a VR_SEG setting.
 int baked_path(const vr_render_desc *d, vr::Params &P) {
-    // a plane's axis copy (P.plane_axis) makes a side / top view row-aligned
-    const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f || P.plane_axis != 0;
+    // a plane's axis copy (P.plane_axis 1 / 2) makes a side / top view row-aligned
+    const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f || P.plane_axis == 1 ||
+                            P.plane_axis == 2;
     int path = along_rows ? 2 : 7;
     int seg = 4;
     // A rank's tile list (multi-GPU) has few rays, so its longest step chains
@@ -1035,18 +1040,28 @@ bool ensure_axis_copy(int axis) {
 // filters gets a copy with that axis in the brick rows (k_plane_axis), the
 // axis-rows idea of ensure_axis_copy for planes: one per axis, made on the
 // first such frame within the layout budget, dropped with the planes.
+// Axis 3 (round 5): oblique views get the plane in 8 x 2 x 2 bricks
+// (k_plane8, gather8 MODE 6), whose lines also hold a footprint's z pair
+// (per 64x4-tile line floor at 1024^3 C1: 3.77 -> 3.47 GB);
+// VR_PLANE8=0 keeps such views on the 16 x 2 x 1 plane.
 bool ensure_plane_copy(int plane, int axis) {
-    if (const char *e = vr::tuning("VR_ZROWS"))
+    if (const char *e = vr::tuning(axis == 3 ? "VR_PLANE8" : "VR_ZROWS"))
         if (std::atoi(e) == 0) return false;
     const int i = axis - 1;
     if (g.pcopy[i].buf && g.pcopy[i].plane == plane) return true;
     if (!g.stats || plane < 0 || plane > 2) return false;
     const uint32_t nf = axis == 2 ? g.nz : g.ny, np = axis == 2 ? g.ny : g.nx;
-    const uint64_t ns = axis == 2 ? (uint64_t)g.nx : (uint64_t)g.nz;
-    if (nf >= (1u << 16) || np > 65535 || ns > 65535) return false;
+    uint64_t ns = axis == 2 ? (uint64_t)g.nx : (uint64_t)g.nz;
+    if (nf >= (1u << 16) || np > 65535 || ns > 65535 || g.nx > 65535) return false;
     uint64_t dsy = 0, dsz = 0;
-    vr::plane_pitches(nf, np, dsy, dsz);
-    if (dsz >= (1ull << 32)) return false;  // gather8 MODE 4/5: 32-bit in-slice offsets
+    if (axis == 3) {
+        vr::plane8_pitches(g.nx, g.ny, dsy, dsz);
+        ns = (uint64_t)(g.nz + 1) / 2;  // slice pairs
+    } else {
+        vr::plane_pitches(nf, np, dsy, dsz);
+    }
+    // gather8 MODE 4/5/6: 32-bit offsets inside a slice (pair)
+    if (dsz >= (1ull << 32)) return false;
     const uint64_t bytes = (dsz * ns + 4) * sizeof(float);
     const uint64_t freed = g.pcopy[i].bytes;  // another plane's copy of this axis
     if (!layout_room(bytes, freed)) return false;
@@ -1057,9 +1072,12 @@ bool ensure_plane_copy(int plane, int axis) {
         return false;
     }
     const auto t0 = std::chrono::steady_clock::now();
+    const float *src = g.stats + (uint64_t)plane * g.stats_plane;
     if (hipMemsetAsync(buf, 0, bytes, g.stream) != hipSuccess ||
-        vr::launch_plane_axis(g.stats + (uint64_t)plane * g.stats_plane, g.stats_sy, g.stats_sz,
-                              buf, dsy, dsz, g.nx, g.ny, g.nz, axis, g.stream) != hipSuccess ||
+        (axis == 3 ? vr::launch_plane8(src, g.stats_sy, g.stats_sz, buf, dsy, dsz, g.nx, g.ny,
+                                       g.nz, g.stream)
+                   : vr::launch_plane_axis(src, g.stats_sy, g.stats_sz, buf, dsy, dsz, g.nx,
+                                           g.ny, g.nz, axis, g.stream)) != hipSuccess ||
         hipStreamSynchronize(g.stream) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFree(buf);
@@ -1681,9 +1699,11 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
         // axis in the brick rows (ensure_plane_copy), marched as row-aligned
         P.plane_axis = 0;
         if (qm <= 3 && std::fabs(desc->inv_view[0]) < 0.95f) {
-            const int ax = std::fabs(desc->inv_view[8]) >= 0.95f ? 2
+            int ax = std::fabs(desc->inv_view[8]) >= 0.95f ? 2
                          : std::fabs(desc->inv_view[4]) >= 0.95f ? 1 : 0;
-            if (ax && ensure_plane_copy(qm - 1, ax)) {
+            // oblique views: the 8 x 2 x 2 brick copy (axis 3)
+            if (!ax) ax = 3;
+            if (ensure_plane_copy(qm - 1, ax)) {
                 const State::PlaneCopy &c = g.pcopy[ax - 1];
                 baked = c.buf;
                 P.sy = c.sy;

@@ -99,11 +99,12 @@ struct Params {
     uint32_t head_slots;
     int head_lanes;
     int head_tail;               // the rest of such a list: 0 seg_lanes windows, 1 one lane per ray (k_march_pipe_head)
-    int plane_axis;              // baked frame on a plane's axis copy: 1 y rows, 2 z rows (gather8 MODE 3 + axis)
+    int plane_axis;              // baked frame on a plane's copy: 1 y rows, 2 z rows (gather8 MODE 4 / 5), 3 8x2x2 bricks (MODE 6)
     int duo;                     // LDS-box march (path 1, B <= 8, m1/m2/m3): samples per box (k_march_duo), 0/1 = k_march
     // tooling (vr_debug_box_check; only a -DVR_BOX_CHECK build reads it): LDS-box
     // bound violations {count, worst index - box size, box voxels, lane footprint}
     unsigned long long *box_check;
+    int duo_compact;             // k_march_duo: box of the used slices only (1) or the whole z range (0)
 };
 
 // Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one
@@ -156,6 +157,32 @@ __host__ __device__ __forceinline__ uint32_t plane_bx(uint32_t x) {
 __host__ __device__ __forceinline__ uint64_t plane_index(uint32_t x, uint32_t y, uint32_t z,
                                                          uint64_t sy, uint64_t sz) {
     return (uint64_t)z * sz + (uint32_t)((y >> 1) * (uint32_t)sy + (y & 1u) * 16u + plane_bx(x));
+}
+
+// Oblique-view copy of a baked plane (round 5): 8 x 2 x 2 bricks -- one 128-B
+// line holds 8 x-neighbours of two y rows and two z slices -- whose x runs
+// overlap by one voxel (brick kx covers x = 7 kx .. 7 kx + 7), so a footprint's
+// x-pair is still one 8-byte load and its z pair often shares the line.  Row
+// pitch sy (floats per row of bricks: a y pair), slice-pair pitch sz.
+constexpr uint32_t kPlane8Stride = 7;
+__host__ __device__ __forceinline__ void plane8_pitches(uint32_t nx, uint32_t ny, uint64_t &sy,
+                                                        uint64_t &sz) {
+    const uint64_t nbx = nx > 0 ? (uint64_t)(nx - 1) / kPlane8Stride + 1 : 0;
+    sy = nbx * 32u;
+    sz = (uint64_t)((ny + 1) / 2) * sy;
+}
+// x / 7 (exact for x < 2^30: 0x24924925 = (2^32 + 3) / 7) and the offset of
+// x's pair (x, x + 1) in its brick row
+__host__ __device__ __forceinline__ uint32_t plane8_bx(uint32_t x) {
+    const uint32_t kx = (uint32_t)(((uint64_t)x * 0x24924925ull) >> 32);
+    return kx * 32u + (x - kPlane8Stride * kx);
+}
+// index of voxel (x, y, z) in its home brick (x = 7 k, k > 0, is also stored at
+// offset 7 of brick k - 1, where pairs starting at 7 k - 1 read it)
+__host__ __device__ __forceinline__ uint64_t plane8_index(uint32_t x, uint32_t y, uint32_t z,
+                                                          uint64_t sy, uint64_t sz) {
+    return (uint64_t)(z >> 1) * sz +
+           (uint32_t)((y >> 1) * (uint32_t)sy + (y & 1u) * 8u + (z & 1u) * 16u + plane8_bx(x));
 }
 
 constexpr int kBoxMax = 1024;    // default per-wave box capacity (4 KiB of f32 statistics)

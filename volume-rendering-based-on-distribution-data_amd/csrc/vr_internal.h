@@ -94,6 +94,10 @@ hipError_t launch_axis_copy(const float *vol, const Params &P, float *out, uint6
                             uint64_t asy, uint64_t asz, hipStream_t s);
 // axis copy of one baked plane (views along y / z, vr_stats.hip k_plane_axis):
 // axis 1 y rows, 2 z rows, into plane_pitches(fast, pair) = (dsy, dsz) bricks
+// 8 x 2 x 2 brick copy of one baked plane (oblique views, vr_stats.hip k_plane8)
+// into plane8_pitches(nx, ny) = (dsy, dsz) bricks
+hipError_t launch_plane8(const float *src, uint64_t ssy, uint64_t ssz, float *out, uint64_t dsy,
+                         uint64_t dsz, int nx, int ny, int nz, hipStream_t s);
 hipError_t launch_plane_axis(const float *src, uint64_t ssy, uint64_t ssz, float *out,
                              uint64_t dsy, uint64_t dsz, int nx, int ny, int nz, int axis,
                              hipStream_t s);

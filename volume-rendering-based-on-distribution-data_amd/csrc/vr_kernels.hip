@@ -264,10 +264,11 @@ __device__ __forceinline__ void decode_box(const float *__restrict__ vbase, cons
 // voxels (those the decode wrote this step), and the box inside the volume.  A
 // violating read is counted and skipped (its sample is 0), never performed.
 // hi: the largest box index the lane reads, V: the voxels decoded this step
-// (dx dy dz, or dx dy x the used slices of a slice-compacted box)
+// (dx dy dz, or dx dy x the used slices of a slice-compacted box); slices:
+// the footprint's slices are among the box's (slice-compacted boxes)
 __device__ __forceinline__ bool box_ok(const Params &P, const Foot &f, int bx0, int by0, int bz0,
-                                       int dx, int dy, int dz, int hi, int V) {
-    const bool ok = f.x0 >= bx0 && f.y0 >= by0 && f.z0 >= bz0 && f.x1 >= f.x0 &&
+                                       int dx, int dy, int dz, int hi, int V, bool slices = true) {
+    const bool ok = slices && f.x0 >= bx0 && f.y0 >= by0 && f.z0 >= bz0 && f.x1 >= f.x0 &&
                     f.y1 >= f.y0 && f.z1 >= f.z0 && f.x1 < bx0 + dx && f.y1 < by0 + dy &&
                     f.z1 < bz0 + dz && hi < V && V <= P.box_max;
     if (!ok && P.box_check) {
@@ -534,7 +535,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
         // 2.56 slices, so {z, z+1} and {z+3, z+4} skip z+2), whose records the
         // bounding box would fetch and decode for nothing.  Ranges of <= 16
         // slices are compacted (slot -> slice through slice_table).
-        const bool compact = dz <= 16;  // wave-uniform
+        const bool compact = dz <= 16 && P.duo_compact;  // wave-uniform
         uint32_t zmask = (1u << min(dz, 31)) - 1u;
         uint64_t ztab = 0;
         if (compact) {
@@ -577,8 +578,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                 const int ox = fk.x1 - fk.x0, oy = (fk.y1 - fk.y0) * dx;
                 const int oz = (fk.z1 - fk.z0) * dxy;
 #ifdef VR_BOX_CHECK
-                if (staged && !(box_ok(P, fk, bx0, by0, bz0, dx, dy, dz, b0 + oz + oy + ox, V) &&
-                                ((zmask >> (fk.z0 - bz0)) & (zmask >> (fk.z1 - bz0)) & 1u))) {
+                if (staged && !box_ok(P, fk, bx0, by0, bz0, dx, dy, dz, b0 + oz + oy + ox, V,
+                                      !compact || ((zmask >> (fk.z0 - bz0)) &
+                                                   (zmask >> (fk.z1 - bz0)) & 1u))) {
                 } else
 #endif
                 if (staged) {
@@ -2741,6 +2743,9 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
                     } else if (P.plane_axis == 2) {
                         note_kernel("k_march_pipe_plane_zrows", B, method);
                         hipLaunchKernelGGL((k_march_pipe<1, 0, 5>), grid, block, occupancy_lds(P), s, vol, P);
+                    } else if (P.plane_axis == 3) {  // 8 x 2 x 2 brick copy (MODE 6)
+                        note_kernel("k_march_pipe_plane8", B, method);
+                        hipLaunchKernelGGL((k_march_pipe<1, 0, 6>), grid, block, occupancy_lds(P), s, vol, P);
                     } else {
                         hipLaunchKernelGGL((k_march_pipe<1, 0>), grid, block, occupancy_lds(P), s, vol, P);
                     }

@@ -251,6 +251,31 @@ __device__ __forceinline__ void gather8(const float *__restrict__ vol, const Par
         }
         return;
     }
+    if constexpr (MODE == 6) {
+        // a baked plane's 8 x 2 x 2 brick copy (oblique views, vr_stats.hip
+        // k_plane8): the four pair loads of MODE 1 with the z pair inside the
+        // brick (offset 16) -- a footprint whose z0 is even reads one line per y
+        // row pair instead of two
+        static_assert(B == 1, "baked planes hold one float per voxel");
+        const uint32_t bx = plane8_bx((uint32_t)f.x0);
+        const bool ox = f.x1 != f.x0;
+        const uint32_t sy = (uint32_t)P.sy;  // a slice pair of the copy is < 2^32 floats
+        const uint32_t y0 = ((uint32_t)f.y0 >> 1) * sy + ((uint32_t)f.y0 & 1u) * 8u + bx;
+        const uint32_t y1 = ((uint32_t)f.y1 >> 1) * sy + ((uint32_t)f.y1 & 1u) * 8u + bx;
+        const uint64_t z0 = (uint64_t)((uint32_t)f.z0 >> 1) * P.sz + ((uint32_t)f.z0 & 1u) * 16u;
+        const uint64_t z1 = (uint64_t)((uint32_t)f.z1 >> 1) * P.sz + ((uint32_t)f.z1 & 1u) * 16u;
+        const vr_f2a4 a = load_pair64(vol, z0 + y0), b = load_pair64(vol, z0 + y1);
+        const vr_f2a4 c = load_pair64(vol, z1 + y0), d = load_pair64(vol, z1 + y1);
+        rec[0][0] = a.x;
+        rec[1][0] = ox ? a.y : a.x;
+        rec[2][0] = b.x;
+        rec[3][0] = ox ? b.y : b.x;
+        rec[4][0] = c.x;
+        rec[5][0] = ox ? c.y : c.x;
+        rec[6][0] = d.x;
+        rec[7][0] = ox ? d.y : d.x;
+        return;
+    }
     if constexpr (MODE == 3) {  // axis-rows copy: all three axes strided
         const uint64_t x0 = (uint64_t)f.x0 * P.sx, x1 = (uint64_t)f.x1 * P.sx;
         const uint64_t y0 = (uint64_t)f.y0 * P.sy, y1 = (uint64_t)f.y1 * P.sy;

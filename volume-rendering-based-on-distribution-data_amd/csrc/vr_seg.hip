@@ -324,6 +324,8 @@ static hipError_t seg_launch(int method, const float *vol, const Params &P, uint
                 hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE, 4>), grid, block, occupancy_lds(P), s, vol, P);
             else if (P.plane_axis == 2)
                 hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE, 5>), grid, block, occupancy_lds(P), s, vol, P);
+            else if (P.plane_axis == 3)  // the 8 x 2 x 2 brick copy (oblique views, MODE 6)
+                hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE, 6>), grid, block, occupancy_lds(P), s, vol, P);
             else
                 hipLaunchKernelGGL((k_march_seg<1, 0, S, PIPE>), grid, block, occupancy_lds(P), s, vol, P);
             break;
@@ -415,7 +417,8 @@ bool launch_march_seg(int nb, int method, int S, const float *vol, const Params 
         char kind[40];
         snprintf(kind, sizeof kind, S < 0 ? "k_march_segp%d%s" : "k_march_seg%d%s", S < 0 ? -S : S,
                  (P.avol && method >= 1 && method <= 3) ? (P.asy == 1 ? "_yrows" : "_zrows")
-                 : (nb == 1 && method == 0 && P.plane_axis) ? (P.plane_axis == 1 ? "_plane_yrows" : "_plane_zrows")
+                 : (nb == 1 && method == 0 && P.plane_axis)
+                     ? (P.plane_axis == 1 ? "_plane_yrows" : P.plane_axis == 2 ? "_plane_zrows" : "_plane8")
                  : "");
         note_kernel(kind, nb, method);
     }

@@ -15,6 +15,7 @@
 
 #include "vr_internal.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace vr {
@@ -273,6 +274,40 @@ hipError_t launch_plane_axis(const float *src, uint64_t ssy, uint64_t ssz, float
     const uint32_t gy = axis == 2 ? (uint32_t)(ny + 1) / 2u : (uint32_t)nz;
     hipLaunchKernelGGL(k_plane_axis, dim3(tiles_x * tiles_f, gy), dim3(256), 0, s, src, ssy, ssz,
                        out, dsy, dsz, (uint32_t)nx, (uint32_t)ny, (uint32_t)nz, axis, tiles_x);
+    return hipGetLastError();
+}
+
+// the 8 x 2 x 2 brick copy of a 16 x 2 x 1 plane (oblique views, gather8 MODE
+// 6): one thread per copy float, in the copy's order (brick, then y, z, x in
+// the brick), so the writes are whole lines; the reads walk 8-voxel x runs of
+// the source bricks
+__global__ __launch_bounds__(256) void k_plane8(const float *__restrict__ src, uint64_t ssy,
+                                                uint64_t ssz, float *__restrict__ out,
+                                                uint64_t total, uint32_t nbx, uint32_t nyp,
+                                                uint32_t nx, uint32_t ny, uint32_t nz) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256u + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * 256u) {
+        const uint32_t o = (uint32_t)(e & 31u);
+        const uint64_t brick = e >> 5;
+        const uint32_t kx = (uint32_t)(brick % nbx);
+        const uint64_t rest = brick / nbx;
+        const uint32_t yp = (uint32_t)(rest % nyp), zp = (uint32_t)(rest / nyp);
+        const uint32_t x = kPlane8Stride * kx + (o & 7u), y = 2u * yp + ((o >> 3) & 1u);
+        const uint32_t z = 2u * zp + (o >> 4);
+        out[e] = (x < nx && y < ny && z < nz) ? src[plane_index(x, y, z, ssy, ssz)] : 0.0f;
+    }
+}
+
+hipError_t launch_plane8(const float *src, uint64_t ssy, uint64_t ssz, float *out, uint64_t dsy,
+                         uint64_t dsz, int nx, int ny, int nz, hipStream_t s) {
+    if (nx <= 0 || ny <= 0 || nz <= 0 || nx >= 65536 || ny >= 65536 || nz >= 65536)
+        return hipErrorInvalidValue;
+    const uint32_t nbx = (uint32_t)(dsy / 32u), nyp = (uint32_t)(ny + 1) / 2u;
+    const uint64_t total = dsz * (uint64_t)((nz + 1) / 2);
+    if (dsz != (uint64_t)nyp * dsy) return hipErrorInvalidValue;
+    const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 1u << 20);
+    hipLaunchKernelGGL(k_plane8, dim3((uint32_t)blocks), dim3(256), 0, s, src, ssy, ssz, out,
+                       total, nbx, nyp, (uint32_t)nx, (uint32_t)ny, (uint32_t)nz);
     return hipGetLastError();
 }
 
