@@ -610,7 +610,10 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // 8-bin entropy of row-aligned views: the LDS-box march with the rolled
     // LDS-column entropy (k_march<8,3>, 128 VGPRs) beats the wave-staged march:
     // 1024^3 C0 4.31 -> 3.52 ms, 512^3 3.10 -> 1.63 (round 4,
-    // profiles/r04/variants_1024x8_m3.log, variants_512x8_m3.log)
+    // profiles/r04/variants_1024x8_m3.log, variants_512x8_m3.log).  Rank tile
+    // lists too: cost-dealt 1024^3 C0 lists, max over ranks, k_march vs the
+    // wave-staged march N = 2 1.99 vs 2.52 ms, N = 4 1.52 vs 1.67, N = 8 1.51 vs
+    // 1.51 (round 5, profiles/r05/rank_sim_m3_C0_paths.log)
     if (along_rows && d->query_method == 3 && g.nb == 8) P.path = 1;
     // ... and of oblique views of a volume coarse for the frame (>= 4 pixels per
     // voxel of the x-y face): 512^3 C1 m3 8.32 -> 5.11 ms; at 1024^3 the quad
