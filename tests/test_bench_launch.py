@@ -75,3 +75,19 @@ def test_self_launch_starts_ranks_with_world_size(tmp_path, capfd):
     rc = b.relay_ranks(cmd)
     out, _ = capfd.readouterr()
     assert rc == 0 and out.strip().splitlines() == ['{"ws": "2"}']
+
+
+def test_self_launched_ranks_failing_fail_the_parent():
+    """no GPU here: `bench.py --gpus 2` starts its 2 ranks, they fail (no device),
+    and the parent exits non-zero with no JSON line instead of hanging or
+    reporting a one-rank run"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--config", "128x1",
+                        "--dist-backend", "gloo", "--no-cpu-baseline", "--steps", "1",
+                        "--warmup", "0"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "starting 2 ranks" in r.stderr
