@@ -57,6 +57,11 @@ dbg)  # the 512^3 C1 two-sample frame with and without slice compaction
   grep -v amdgpu $O/box_check.log
   timeout -k 10 300 python -u tools/box_check.py --any-build --configs 512x8:C1 --methods 1 --duos "VR_DUO=2+VR_DUO_COMPACT=0,2" > $O/main.log 2>&1
   grep -v amdgpu $O/main.log ;;
+sweep)  # baked C1 on the 8x2x2 copy: occupancy caps and ray splits; config 3 compaction / tile blocks
+  timeout -k 10 600 python -u tools/bench_variants.py --variants main --config 1024x8 --baked --cameras C1 --method 1 --rounds 4 --env "" "VR_WG_PER_CU=3" "VR_WG_PER_CU=6" "VR_WG_PER_CU=8" "VR_SEG=-4" "VR_SEG=2" "VR_SEG=-2" "VR_SEG=8" > $O/variants_baked_C1.log 2>&1; guard $? var $O/variants_baked_C1.log
+  grep -v "round\|amdgpu.ids" $O/variants_baked_C1.log
+  timeout -k 10 600 python -u tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method 1 --rounds 6 --env "" "VR_DUO_COMPACT=0" "VR_XBLOCK=1,8" "VR_XBLOCK=2,4" "VR_XBLOCK=1,2" > $O/variants_512x8.log 2>&1; guard $? var $O/variants_512x8.log
+  grep -v "round\|amdgpu.ids" $O/variants_512x8.log ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
