@@ -428,6 +428,8 @@ def test_errors_do_not_exit(pkg, gpu):
     # K samples per footprint box (k_march_duo, m1/m2/m3), with direct-path fallbacks
     ("1", {"VR_DUO": "2"}), ("1", {"VR_DUO": "2", "VR_BOX_MAX": "64"}),
     ("1", {"VR_DUO": "3"}), ("1", {"VR_DUO": "4", "VR_BOX_MAX": "64"}),
+    # slice-compacted duo boxes (VR_DUO_COMPACT, off by default)
+    ("1", {"VR_DUO": "2", "VR_DUO_COMPACT": "1"}), ("1", {"VR_DUO": "4", "VR_DUO_COMPACT": "1"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
@@ -447,9 +449,10 @@ def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
             assert_parity(got, ref, f"path {path} {env} nb={nb} m{method}")
 
 
+@pytest.mark.parametrize("compact", ["0", "1"])
 @pytest.mark.parametrize("k", ["2", "3", "4"])
 @pytest.mark.parametrize("nb", [1, 2, 8])
-def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune):
+def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune, compact):
     """k_march_duo (K samples per footprint box; mean, variance and entropy -- the
     entropy instance restored in round 5 with k_march's LDS log table and record
     columns): rays ending on any sample of a box (opacity, tfar),
@@ -457,6 +460,7 @@ def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune):
     import torch
     tune.set("VR_PATH", "1")
     tune.set("VR_DUO", k)
+    tune.set("VR_DUO_COMPACT", compact)
     vol = orc.synth_volume(30, 26, 22, nb)
     pkg.init_distribution(vol)
     cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),

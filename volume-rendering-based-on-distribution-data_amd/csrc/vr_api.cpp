@@ -757,7 +757,11 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         }
     }
     if (P.path != 2 && P.path != 7) P.axis_view = 0;  // 7: the segmented march reads the copy too
-    P.duo_compact = 1;  // k_march_duo: only the slices the footprints read (VR_DUO_COMPACT=0: all)
+    // k_march_duo boxes of only the slices the footprints read (VR_DUO_COMPACT=1):
+    // 512^3 x 8 C0 decodes 2.12 -> 2.00 U but runs 0.624 -> 0.681 ms (the slot
+    // table and the per-lane slot counts cost more than the skipped slices;
+    // round 5, profiles/r05/sweep), so the default keeps the whole z range
+    P.duo_compact = 0;
     if (const char *e = vr::tuning("VR_DUO_COMPACT")) P.duo_compact = std::atoi(e) != 0;
     if (const char *e = vr::tuning("VR_DUO")) {  // 0 / 1: one sample per box, 2-4: that many
         const int v = std::atoi(e);

@@ -530,11 +530,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
         const int by1 = min(-hi_y + 1, P.ny - 1);
         const int bz1 = min(-hi_z + 1, P.nz - 1);
         const int dx = bx1 - bx0 + 1, dy = by1 - by0 + 1, dz = bz1 - bz0 + 1;
-        // The box keeps only the slices some footprint reads: K samples a step
-        // apart leave slices between them that none does (512^3: a step is
-        // 2.56 slices, so {z, z+1} and {z+3, z+4} skip z+2), whose records the
-        // bounding box would fetch and decode for nothing.  Ranges of <= 16
-        // slices are compacted (slot -> slice through slice_table).
+        // P.duo_compact (VR_DUO_COMPACT=1, off by default): the box keeps only
+        // the slices some footprint reads -- K samples a step apart leave
+        // slices between them that none does (512^3: a step is 2.56 slices, so
+        // {z, z+1} and {z+3, z+4} skip z+2).  Ranges of <= 16 slices are
+        // compacted (slot -> slice through slice_table).  It decodes 6 % fewer
+        // voxels at 512^3 C0 but the table and slot counts cost more: 0.624 ->
+        // 0.681 ms.
         const bool compact = dz <= 16 && P.duo_compact;  // wave-uniform
         uint32_t zmask = (1u << min(dz, 31)) - 1u;
         uint64_t ztab = 0;
