@@ -417,6 +417,11 @@ int vr_synthesize_gmm(vr_extent dims, int ncomp, uint64_t seed, int z_base, int 
 int vr_gmm_info(vr_extent *dims, int *ncomp, int *z_base, int *nslices, const float **d_wm,
                 const float **d_sigma);
 int vr_free_gmm(void);
+/* Two GMM volumes may be resident, in slots 0 and 1 (a rank of a two-segment
+ * slab chain holds a front and a back z-range): every vr_*gmm*
+ * call acts on the selected slot (0 until changed); vr_free_gmm frees only it,
+ * freeCudaBuffers both. */
+int vr_gmm_select(int slot);
 
 /* Slab of a slab-chained render (out-of-core and multi-GPU sort-last, DESIGN.md
  * 11.2).  The launch takes the samples whose trilinear footprint starts in

@@ -96,7 +96,7 @@ EXPORTS = [
     "vr_load_reference_files", "vr_init_flex", "vr_flex_process", "vr_flex_info",
     "vr_parse_span_list", "vr_parse_fractal_histogram", "vr_parse_simple_histogram",
     "vr_load_flex_files", "vr_debug_wave_clock", "vr_debug_box_check",
-    "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_render_gmm",
+    "vr_init_gmm", "vr_synthesize_gmm", "vr_gmm_info", "vr_free_gmm", "vr_gmm_select", "vr_render_gmm",
     "vr_gmm_count_footprint", "vr_gmm_count_footprint_slab", "vr_bake_stats", "vr_release_stats", "vr_stats_info",
     "vr_set_tuning", "vr_clear_tuning", "vr_stream_read", "vr_set_layout_budget",
     "vr_layout_info",
@@ -212,6 +212,8 @@ def load() -> ctypes.CDLL:
     L.vr_render_gmm.restype = i32
     L.vr_gmm_count_footprint.argtypes = [ctypes.POINTER(RenderDesc)]
     L.vr_gmm_count_footprint.restype = ctypes.c_int64
+    L.vr_gmm_select.argtypes = [ctypes.c_int]
+    L.vr_gmm_select.restype = ctypes.c_int
     L.vr_gmm_count_footprint_slab.argtypes = [ctypes.POINTER(RenderDesc), ctypes.POINTER(GmmSlab)]
     L.vr_gmm_count_footprint_slab.restype = ctypes.c_int64
     L.vr_bake_stats.argtypes = []

@@ -499,6 +499,11 @@ def free_gmm() -> None:
     check(_lib.load().vr_free_gmm())
 
 
+def gmm_select(slot: int) -> None:
+    """Select GMM slot 0 or 1 (include/vr.h vr_gmm_select): the GMM calls act on it"""
+    check(_lib.load().vr_gmm_select(int(slot)))
+
+
 def gmm_slab(z_lo: int, z_hi: int, d_rays_out, d_n_rays_out, d_rays_in=None,
              n_rays_in: int = 0) -> _lib.GmmSlab:
     s = _lib.GmmSlab()
@@ -535,7 +540,7 @@ __all__ = [
     "volume_info",
     "volume_layout",
     "set_stream", "set_tuning", "clear_tuning", "make_desc", "render", "count_footprint", "footprint_bytes", "unscatter_tiles", "last_kernel", "debug_wave_clock", "stream_read", "version",
-    "init_gmm", "synthesize_gmm", "gmm_info", "free_gmm", "gmm_slab", "render_gmm",
+    "init_gmm", "synthesize_gmm", "gmm_info", "free_gmm", "gmm_select", "gmm_slab", "render_gmm",
     "gmm_count_footprint", "bake_stats", "release_stats", "stats_info", "set_layout_budget",
     "layout_info",
     "VRError", "PAD",

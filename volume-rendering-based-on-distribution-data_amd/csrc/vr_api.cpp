@@ -65,7 +65,11 @@ struct State {
         float *wm = nullptr, *sg = nullptr;
         bool owned = false;
         int nx = 0, ny = 0, nz = 0, K = 0, z_base = 0, nzs = 0;
-    } gmm;
+    } gmm;  // the selected slot's volume (vr_gmm_select)
+    // the other slot's volume while not selected (a rank of a two-segment slab
+    // chain holds a front and a back z-range)
+    Gmm gmm_parked[2];
+    int gmm_slot = 0;
     // baked statistics (basicDataProcessing / vr_bake_stats, vr_stats.hip):
     // four planes of stats_plane floats for the raw volume (methods 1/2/3 and
     // method 7's corner mean) and
@@ -1861,13 +1865,26 @@ int vr_unscatter_tiles(const uint32_t *d_packed, const uint32_t *d_tile_lists, u
 
 namespace {
 
+void release_gmm_volume(State::Gmm &v) {
+    if (v.owned) {
+        if (v.wm) (void)hipFree(v.wm);
+        if (v.sg) (void)hipFree(v.sg);
+    }
+    v = State::Gmm{};
+}
+
+// the selected slot's GMM volume
 void release_gmm() {
     g.volume_epoch++;
-    if (g.gmm.owned) {
-        if (g.gmm.wm) (void)hipFree(g.gmm.wm);
-        if (g.gmm.sg) (void)hipFree(g.gmm.sg);
-    }
-    g.gmm = State::Gmm{};
+    release_gmm_volume(g.gmm);
+}
+
+// both slots' (freeCudaBuffers)
+void release_all_gmm() {
+    release_gmm();
+    release_gmm_volume(g.gmm_parked[0]);
+    release_gmm_volume(g.gmm_parked[1]);
+    g.gmm_slot = 0;
 }
 
 int check_gmm_shape(vr_extent dims, int K, int z_base, int nzs) {
@@ -2077,6 +2094,17 @@ int vr_gmm_info(vr_extent *dims, int *ncomp, int *z_base, int *nslices, const fl
     return VR_OK;
 }
 
+int vr_gmm_select(int slot) {
+    if (slot != 0 && slot != 1) return fail(VR_ERR_ARG, "GMM slot %d (0 or 1)", slot);
+    if (slot == g.gmm_slot) return VR_OK;
+    g.gmm_parked[g.gmm_slot] = g.gmm;
+    g.gmm = g.gmm_parked[slot];
+    g.gmm_parked[slot] = State::Gmm{};
+    g.gmm_slot = slot;
+    g.volume_epoch++;  // (the tile order is keyed on what is resident)
+    return VR_OK;
+}
+
 int vr_free_gmm(void) {
     release_gmm();
     return VR_OK;
@@ -2233,7 +2261,7 @@ void freeCudaBuffers(void) {
     release_volume();
     release_codec();
     release_flex();
-    release_gmm();
+    release_all_gmm();
 }
 
 void setTextureFilterMode(bool bLinearFilter) { g.linear_filter = bLinearFilter; }
