@@ -136,6 +136,9 @@ def parse():
                     help="GMM volumes on ONE GPU: every rank's z-slab of the --rehearsal-ranks "
                          "chain generated in turn (untimed) and its march timed with HIP "
                          "events; reports per-slab ms and the pipeline-period estimate")
+    ap.add_argument("--segments", type=int, default=1, choices=[1, 2],
+                    help="GMM z-slab chains: z segments per rank (2: a thin front and a thick "
+                         "back one, slabs.two_segment_bounds)")
     ap.add_argument("--rehearsal-ranks", type=int, default=8,
                     help="--slab-rehearsal: slabs (ranks) of the chain (BASELINE config 5: 8)")
     ap.add_argument("--rebalance", type=int, default=2,
@@ -426,25 +429,40 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
             pkg.free_gmm()
         return rows
 
+    def owners(nseg):
+        return list(range(nseg)) if nseg == R else pkg.slabs.segment_owner(nseg, R)
+
+    def rank_period(rows):
+        """max over ranks of the summed march time of the segments a rank holds"""
+        per = [0.0] * R
+        for r, row in zip(owners(len(rows)), rows):
+            row["rank"] = r
+            per[r] += row["ms"]
+        return max(per), per
+
     pkg.free_gmm()
     torch.cuda.empty_cache()
     bounds = pkg.slabs.slab_bounds(n, R, direction)
     rows_eq = rows = chain(bounds, "equal")
     free_now, _ = torch.cuda.mem_get_info(dev)
     cap = pkg.slabs.max_slices_for(n, n, K, free_now)
-    passes = [max(r["ms"] for r in rows)]
+    passes = [rank_period(rows)[0]]
     for p in range(args.rebalance):
-        bounds = pkg.slabs.bounds_by_cost(n, R, direction, bounds, [r["ms"] for r in rows], cap)
+        costs = [r["ms"] for r in rows]
+        if args.segments == 2:  # every rank a front and a back segment (DESIGN.md 11.3)
+            bounds = pkg.slabs.two_segment_bounds(n, R, direction, bounds, costs, cap)
+        else:
+            bounds = pkg.slabs.bounds_by_cost(n, R, direction, bounds, costs, cap)
         rows = chain(bounds, f"balanced {p + 1}")
-        passes.append(max(r["ms"] for r in rows))
+        passes.append(rank_period(rows)[0])
     rows_bal = rows
-    period = max(r["ms"] for r in rows_bal)
+    period, per_rank = rank_period(rows_bal)
     kernel = pkg.last_kernel()
     worst = max(rows_bal, key=lambda r: r["ms"])
     cpu = None if args.no_cpu_baseline else gmm_cpu_baseline(m, args.method, W, H, K)
     out = {
         "metric": f"Mrays/s + fps at {n}^3 x {K}-component GMM volume, {W}x{H}; % HBM roofline "
-                  f"({R}-slab chain rehearsed on one GPU: pipeline-period estimate)",
+                  f"({R}-rank slab chain rehearsed on one GPU: pipeline-period estimate)",
         "value": round(W * H / (period * 1e-3) / 1e6, 3),
         "unit": "Mrays/s",
         "n_gpus": 1,
@@ -465,10 +483,13 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
                         f"queryMethod {args.method}, {R} z-slabs",
             "volume": [n, n, n], "components": K, "image": [W, H], "camera": args.camera,
             "query_method": args.method, "density": 0.05,
-            "parallelism": f"z-slabs x{R} rehearsed on 1 GPU (each slab's march timed on its "
-                           "real alive-list input; hand-off and frame reduce not timed)",
-            "period": "max over slabs of the slab's mean march time (HIP events, "
+            "parallelism": f"z-slabs x{R} ranks ({args.segments} segment(s) each) rehearsed on 1 "
+                           "GPU (each segment's march timed on its real alive-list input; "
+                           "hand-off and frame reduce not timed)",
+            "segments_per_rank": args.segments,
+            "period": "max over ranks of its segments' summed mean march time (HIP events, "
                       f"{args.steps} frames after {args.warmup} warm-up)",
+            "rank_ms": [round(v, 4) for v in per_rank],
             "slabs_equal": rows_eq,
             "slabs_balanced": rows_bal,
             "period_ms_per_pass": [round(v, 4) for v in passes],
@@ -483,6 +504,197 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
+    return out
+
+
+def gmm_two_segment_run(args, pkg, torch, dist, dev, stream, m, n, K, W, H, rank, world, ndev):
+    """N > 1 GMM chain with two z segments per rank (--segments 2, DESIGN.md
+    11.3): rank r holds front segment r in GMM slot 0 and back segment 2N-1-r in
+    slot 1 (slabs.two_segment_bounds, segment_owner).  Ranks run a tick schedule
+    (slabs.two_segment_ticks): at tick t, the front march of frame t - r (input
+    from rank r - 1 over the forward group), then the back march of frame
+    t - (2N-1-r) (input from rank r + 1 over the backward group; rank N-1 takes
+    its own front output of the tick before), alive lists handed on by isend,
+    each frame summed on rank 0 by an asynchronous reduce on a third group once
+    the rank's back march of it is done.  Untimed balancing frames first
+    (per-segment costs all-reduced, segments re-cut and regenerated), then the
+    timed steady-state ticks: each completes one frame."""
+    S = pkg.slabs
+    R = world
+    direction = S.march_direction(m, W, H)
+    fwd, bwd, asm = (dist.new_group(list(range(world))) for _ in range(3))
+    cdev = dev if args.dist_backend == "nccl" else "cpu"
+    front_i, back_i = rank, 2 * R - 1 - rank
+    RING = 2 * R + 2
+    frames = [torch.zeros(W * H, dtype=torch.int32, device=dev) for _ in range(RING)]
+    descs = [pkg.make_desc(f, W, H, m, query_method=args.method, volume_size=(1, 1, 1))
+             for f in frames]
+    lst = lambda: torch.zeros((W * H, S.RAY_WORDS), dtype=torch.int32, device=dev)
+    f_in, b_in, b_out = lst(), lst(), lst()
+    f_out = [lst(), lst()]  # rank N-1: its back march reads the previous tick's front output
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    own_front = [None, None]  # rank N-1: (buffer, count) of its front output by frame parity
+
+    def generate(bounds):
+        for slot, i in ((0, front_i), (1, back_i)):
+            pkg.gmm_select(slot)
+            pkg.free_gmm()
+        torch.cuda.empty_cache()
+        for slot, i in ((0, front_i), (1, back_i)):
+            pkg.gmm_select(slot)
+            zb, ns = S.resident_slices(*bounds[i], n)
+            pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
+        torch.cuda.synchronize()
+
+    state = {"works": [None] * RING, "sf": None, "sb": None}
+
+    def run_ticks(t0, t1, nframes, seg_ev=None):
+        for t in range(t0, t1):
+            ff, fb = S.two_segment_ticks(rank, R, t)
+            if 0 <= ff < nframes:
+                b = ff % RING
+                if state["works"][b] is not None:
+                    state["works"][b].wait()
+                    state["works"][b] = None
+                frames[b].zero_()
+                pkg.gmm_select(0)
+                n_in = S.recv_alive(rank - 1, f_in, dist, group=fwd) if rank > 0 else 0
+                out = f_out[ff % 2]
+                if state["sf"] is not None:
+                    state["sf"].wait()
+                cnt.zero_()
+                if seg_ev is not None:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                pkg.render_gmm(descs[b], pkg.gmm_slab(*bounds[front_i], out, cnt,
+                                                      d_rays_in=f_in if rank > 0 else None,
+                                                      n_rays_in=n_in))
+                if seg_ev is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record(stream)
+                    seg_ev[0].append((e0, e1))
+                n_out = int(cnt.item())
+                if rank < R - 1:
+                    state["sf"] = S.isend_alive(out, n_out, rank + 1, dist, group=fwd)
+                else:
+                    own_front[ff % 2] = (out, n_out)
+            if 0 <= fb < nframes:
+                b = fb % RING
+                pkg.gmm_select(1)
+                if rank == R - 1:
+                    rin, n_in = own_front[fb % 2]
+                else:
+                    n_in = S.recv_alive(rank + 1, b_in, dist, group=bwd)
+                    rin = b_in
+                if state["sb"] is not None:
+                    state["sb"].wait()
+                cnt.zero_()
+                if seg_ev is not None:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                pkg.render_gmm(descs[b], pkg.gmm_slab(*bounds[back_i], b_out, cnt, d_rays_in=rin,
+                                                      n_rays_in=n_in))
+                if seg_ev is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record(stream)
+                    seg_ev[1].append((e0, e1))
+                n_out = int(cnt.item())
+                if rank > 0:
+                    state["sb"] = S.isend_alive(b_out, n_out, rank - 1, dist, group=bwd)
+                elif n_out:
+                    raise RuntimeError(f"{n_out} rays alive past the last segment")
+                state["works"][b] = S.reduce_frame(frames[b], dist, group=asm, async_op=True)
+
+    def drain():
+        for w in state["works"]:
+            if w is not None:
+                w.wait()
+        state["works"] = [None] * RING
+        for k in ("sf", "sb"):
+            if state[k] is not None:
+                state[k].wait()
+                state[k] = None
+        torch.cuda.synchronize()
+
+    # initial cut: uniform cost; then balancing frames (untimed): per-segment
+    # march times all-reduced, segments re-cut by them and regenerated
+    free_now, _ = torch.cuda.mem_get_info(dev)
+    cap_t = torch.tensor([S.max_slices_for(n, n, K, free_now)], dtype=torch.int64, device=cdev)
+    dist.all_reduce(cap_t, op=dist.ReduceOp.MIN)
+    cap = int(cap_t.item())
+    bounds = S.two_segment_bounds(n, R, direction, max_slices=cap)
+    generate(bounds)
+    passes = []
+    for _ in range(max(args.rebalance, 1)):
+        nf = 2
+        ev = ([], [])
+        run_ticks(0, nf + 2 * R - 1, nf, seg_ev=ev)
+        drain()
+        costs = torch.zeros(2 * R, dtype=torch.float64, device=cdev)
+        costs[front_i] = float(np.mean([a.elapsed_time(b) for a, b in ev[0]])) if ev[0] else 0.0
+        costs[back_i] = float(np.mean([a.elapsed_time(b) for a, b in ev[1]])) if ev[1] else 0.0
+        dist.all_reduce(costs)
+        c = costs.cpu().tolist()
+        passes.append(max(c[i] + c[2 * R - 1 - i] for i in range(R)))
+        bounds = S.two_segment_bounds(n, R, direction, bounds, c, cap)
+        generate(bounds)
+    # steady state: W warm-up frames' worth of ticks, then K timed ticks (each
+    # completes one frame at rank 0), then the pipeline drains (untimed)
+    F = args.warmup + args.steps + 2 * R
+    t_start = args.warmup + 2 * R - 1
+    run_ticks(0, t_start, F)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_ticks(t_start, t_start + args.steps, F)
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    run_ticks(t_start + args.steps, F + 2 * R - 1, F)
+    drain()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    if args.dump_frame and rank == 0:
+        last = frames[(F - 1) % RING]
+        np.save(args.dump_frame, last.cpu().numpy().view(np.uint32).reshape(H, W))
+    out = None
+    if rank == 0:
+        phys = min(world, max(ndev, 1))
+        out = {
+            "metric": f"Mrays/s + fps at {n}^3 x {K}-component GMM volume, {W}x{H}; % HBM roofline",
+            "value": round(W * H / (elapsed / args.steps) / 1e6, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "physical_gpus": phys,
+            "rehearsal_shared_gpus": world > phys,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "fps": round(1e3 / ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": None if world > phys else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic seeded GMM volume (seed {SEED}, DESIGN.md s11.1)",
+            "config": {
+                "workload": f"{n}^3 x {K}-component GMM volume, {W}x{H}, camera {args.camera}, "
+                            f"queryMethod {args.method}",
+                "volume": [n, n, n], "components": K, "image": [W, H], "camera": args.camera,
+                "query_method": args.method, "density": 0.05,
+                "parallelism": (f"z-slab chain x{world}, two segments per rank + " +
+                                ("RCCL send/recv of alive rays + reduce"
+                                 if args.dist_backend == "nccl" else "gloo host staging")),
+                "segments": [list(b) for b in bounds],
+                "balance_pass_max_rank_ms": [round(v, 4) for v in passes],
+            },
+            "roofline": None,
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
     return out
 
 
@@ -524,6 +736,10 @@ def main_gmm(args):
     if world == 1 and args.slab_rehearsal:
         with torch.cuda.stream(stream):  # the counter resets and the launches on one stream
             return gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes)
+    if world > 1 and args.segments == 2:
+        with torch.cuda.stream(stream):
+            return gmm_two_segment_run(args, pkg, torch, dist, dev, stream, m, n, K, W, H, rank,
+                                       world, ndev)
     if world == 1:
         need = n ** 3 * 12 * K
         if need > free * 0.95:

@@ -294,3 +294,57 @@ def test_stream_bounds(pkg):
         sb(10, 0, 1)
     with pytest.raises(ValueError):
         sb(10, 4, 0)
+
+
+def test_two_segment_bounds(pkg):
+    """two z segments per rank: the 2N segments cover the volume in march order,
+    rank r holds segments r and 2N-1-r, a front-loaded cost profile gives every
+    rank about C / N (one slab per rank could not: the back slabs hit the HBM
+    cap), and the thickest rank fits the cap"""
+    S = pkg.slabs
+    n, R = 2048, 8
+    b = S.slab_bounds(n, R, -1)
+    c = [5.98, 6.44, 3.74, 1.19, 0.47, 0.07, 0.0, 0.0]  # the measured equal-slab chain
+    cap = S.max_slices_for(n, n, 16, 288e9)
+    seg = S.two_segment_bounds(n, R, -1, b, c, cap)
+    assert len(seg) == 2 * R and seg[0][1] == n and seg[-1][0] == 0
+    assert all(seg[i][0] == seg[i + 1][1] for i in range(2 * R - 1))  # contiguous, march order
+    own = S.segment_owner(2 * R, R)
+    assert own == list(range(R)) + list(range(R - 1, -1, -1))
+    dens = S._march_density(n, -1, b, c)
+    pre = np.concatenate([[0.0], np.cumsum(dens)])
+    per, thick = [0.0] * R, [0] * R
+    for (lo, hi), r in zip(seg, own):
+        per[r] += pre[n - lo] - pre[n - hi]
+        thick[r] += hi - lo + 1
+    assert max(per) < 1.05 * sum(c) / R
+    assert max(thick) <= cap + 1
+    one = S.bounds_by_cost(n, R, -1, b, c, cap)  # one slab per rank: bound by the cap
+    one_max = max(pre[n - lo] - pre[n - hi] for lo, hi in one)
+    assert max(per) < 0.6 * one_max
+    # uniform cost: equal work per rank; ascending march order too
+    seg = S.two_segment_bounds(64, 4, 1)
+    assert seg[0][0] == 0 and seg[-1][1] == 64
+    work = [0] * 4
+    for (lo, hi), r in zip(seg, S.segment_owner(8, 4)):
+        work[r] += hi - lo
+    assert max(work) - min(work) <= 2
+    with pytest.raises(ValueError):
+        S.two_segment_bounds(n, R, -1, b, c, max_slices=200)
+
+
+def test_two_segment_ticks_wait_only_on_earlier_ticks(pkg):
+    """the tick schedule: every frame's 2N segments are marched in march order,
+    each at a later tick than the segment it takes its alive list from, and in
+    the steady state every rank marches one front and one back segment a tick"""
+    S = pkg.slabs
+    for R in (1, 2, 3, 8):
+        when = {}
+        for t in range(6 * R + 4):
+            for r in range(R):
+                ff, fb = S.two_segment_ticks(r, R, t)
+                when[(ff, r)] = t
+                when[(fb, 2 * R - 1 - r)] = t
+        for f in range(3):
+            ticks = [when[(f, i)] for i in range(2 * R)]  # segment i of frame f
+            assert all(ticks[i + 1] == ticks[i] + 1 for i in range(2 * R - 1)), (R, ticks)

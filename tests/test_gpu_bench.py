@@ -67,3 +67,26 @@ def test_bench_gmm_single_and_two_slab_frames_agree(gpu, tmp_path):
     a, b = np.load(f1), np.load(f2)
     assert a.shape == (256, 256) and np.count_nonzero(a) > 0
     assert np.array_equal(a, b), f"{int(np.sum(a != b))} pixels differ between N=1 and N=2"
+    # two z segments per rank (--segments 2: front + back, tick-scheduled chain),
+    # ranks started by bench.py itself
+    f3 = str(tmp_path / "g3.npy")
+    out3 = _run([sys.executable, "bench.py", "--gpus", "2", *args, "--dist-backend", "gloo",
+                 "--segments", "2", "--dump-frame", f3], tmp_path)
+    assert out3["n_gpus"] == 2 and "two segments" in out3["config"]["parallelism"]
+    assert len(out3["config"]["segments"]) == 4
+    c = np.load(f3)
+    assert np.array_equal(a, c), f"{int(np.sum(a != c))} pixels differ (two segments per rank)"
+
+
+def test_bench_gmm_slab_rehearsal(gpu, tmp_path):
+    """--slab-rehearsal on one GPU: every segment of the chain generated and timed
+    in turn, one and two segments per rank; the period is the slowest rank's"""
+    for seg in ("1", "2"):
+        out = _run([sys.executable, "bench.py", "--config", "gmm96", "--slab-rehearsal",
+                    "--rehearsal-ranks", "3", "--segments", seg, "--steps", "2", "--warmup", "1",
+                    "--no-cpu-baseline"], tmp_path)
+        cfg = out["config"]
+        assert out["n_gpus"] == 1 and out["scaling"] is None and out["rehearsal_shared_gpus"]
+        assert len(cfg["slabs_balanced"]) == 3 * int(seg)
+        assert abs(out["ms_per_step"] - max(cfg["rank_ms"])) < 1e-3
+        assert cfg["slabs_balanced"][0]["rays_in"] == 256 * 256

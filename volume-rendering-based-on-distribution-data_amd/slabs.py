@@ -112,6 +112,98 @@ def bounds_by_cost(nz: int, n: int, direction: int, bounds, costs,
     return [(nz - b, nz - a) for a, b in march]
 
 
+def _march_density(nz: int, direction: int, bounds, costs) -> np.ndarray:
+    """per-slice cost in march order (index 0 = first crossed), uniform inside
+    each measured segment (bounds in z, any order, covering [0, nz))"""
+    dens = np.zeros(nz, dtype=np.float64)
+    for (lo, hi), c in zip(bounds, costs):
+        for z in range(lo, hi):
+            k = z if direction > 0 else nz - 1 - z
+            dens[k] = max(float(c), 1e-9) / (hi - lo)
+    return dens
+
+
+def _equal_cost_cuts(pre: np.ndarray, a: int, b: int, n: int) -> List[int]:
+    """n + 1 cut points a = c0 < c1 < ... < cn = b (march-order slices) with
+    about equal cost between them (pre: prefix sums of the density), every part
+    at least one slice"""
+    cuts = [a]
+    for i in range(1, n):
+        target = pre[a] + (pre[b] - pre[a]) * i / n
+        c = int(np.searchsorted(pre, target, side="left"))
+        c = min(max(c, cuts[-1] + 1), b - (n - i))
+        cuts.append(c)
+    cuts.append(b)
+    return cuts
+
+
+def segment_owner(n_segments: int, world: int) -> List[int]:
+    """rank holding each segment of a two-segment chain (march order): the front
+    segments 0 .. N-1 on ranks 0 .. N-1, the back ones N .. 2N-1 snaking back on
+    N-1 .. 0, so rank r holds segments r and 2N-1-r"""
+    assert n_segments == 2 * world
+    return list(range(world)) + list(range(world - 1, -1, -1))
+
+
+def two_segment_bounds(nz: int, world: int, direction: int, bounds=None, costs=None,
+                       max_slices: Optional[int] = None) -> List[Tuple[int, int]]:
+    """2N z-ranges [z_lo, z_hi) in march order for a chain in which every rank
+    holds two segments (segment_owner): a thin front one and a thick back one.
+
+    Early ray termination front-loads the work: with one slab per rank the back
+    ranks idle while their slabs (at the HBM cap) still cannot take work off the
+    front ones (config 5: 4.2 ms period for 19 ms of work on 8 ranks).  Here the
+    volume is cut at a split S (march order) into a back region [S, nz), cut
+    into N equal-thickness segments (it holds little work: the slices that
+    fill the HBM), and a front region [0, S) cut so that rank r's front segment
+    r carries C / N minus the cost of its back segment N-1-r (C: the frame's
+    cost), i.e. every rank carries about C / N.  S is chosen for the smallest
+    slowest rank, then the thinnest rank (its two segments + their halo slices,
+    which must fit max_slices + 1 resident slices).  bounds/costs: a measured
+    partition (any number of segments, z coordinates) and its costs; None =
+    uniform cost."""
+    if direction == 0:
+        raise ValueError("rays of this view cross z-slabs in both directions")
+    if world < 1 or 2 * world > nz:
+        raise ValueError(f"{2 * world} segments cannot partition {nz} slices")
+    if bounds is None:
+        dens = np.ones(nz, dtype=np.float64)
+    else:
+        dens = _march_density(nz, direction, bounds, costs)
+    pre = np.concatenate([[0.0], np.cumsum(dens)])
+    total = pre[-1]
+    cands = []
+    for S in range(world, nz - world + 1):
+        back = [S + ((nz - S) * j) // world for j in range(world + 1)]
+        if any(back[j + 1] <= back[j] for j in range(world)):
+            continue
+        front = [0]
+        for r in range(world - 1):
+            j = world - 1 - r  # rank r's back segment
+            want = max(total / world - (pre[back[j + 1]] - pre[back[j]]), 0.0)
+            c = int(np.searchsorted(pre, pre[front[-1]] + want, side="left"))
+            front.append(min(max(c, front[-1] + 1), S - (world - 1 - r)))
+        front.append(S)
+        if any(front[r + 1] <= front[r] for r in range(world)):
+            continue
+        per = [(pre[front[r + 1]] - pre[front[r]]) +
+               (pre[back[world - r]] - pre[back[world - 1 - r]]) for r in range(world)]
+        thick = max((front[r + 1] - front[r]) + (back[world - r] - back[world - 1 - r]) + 2
+                    for r in range(world))
+        if max_slices is None or thick <= max_slices + 1:
+            cands.append((max(per), thick, front, back))
+    if not cands:
+        raise ValueError(f"no two-segment cut of {nz} slices fits {max_slices} slices per rank")
+    # the cheapest slowest rank (within 2 %: slice discretisation), then the thinnest
+    floor = min(c[0] for c in cands)
+    _, _, front, back = min((c for c in cands if c[0] <= floor * 1.02), key=lambda c: (c[1], c[0]))
+    cuts = front + back[1:]
+    march = [(cuts[i], cuts[i + 1]) for i in range(2 * world)]
+    if direction > 0:
+        return march
+    return [(nz - b, nz - a) for a, b in march]
+
+
 def max_slices_for(nx: int, ny: int, ncomp: int, hbm_bytes: float, reserve: float = 0.1) -> int:
     """Largest slab (slices, excluding its halo slice) whose GMM records fit in
     hbm_bytes with a `reserve` fraction left for frame and alive-list buffers."""
@@ -125,47 +217,85 @@ def resident_slices(z_lo: int, z_hi: int, nz: int) -> Tuple[int, int]:
     return z_lo, min(z_hi + 1, nz) - z_lo
 
 
-def _staged(dist) -> bool:
+def _staged(dist, group=None) -> bool:
     """gloo carries only host tensors: device buffers are staged through host
     memory (multi-rank rehearsal on one GPU; never for measurement)"""
-    return dist.get_backend() == "gloo"
+    return dist.get_backend(group) == "gloo"
 
 
-def send_alive(rays, count: int, dst: int, dist) -> None:
+def send_alive(rays, count: int, dst: int, dist, group=None) -> None:
     """Send an alive list (first `count` rows of an (n, 12) int32 tensor) to rank
     dst: the count first, then the rows (RCCL point-to-point over xGMI on GPUs)."""
     import torch
-    dev = "cpu" if _staged(dist) else rays.device
+    dev = "cpu" if _staged(dist, group) else rays.device
     c = torch.tensor([count], dtype=torch.int64, device=dev)
-    dist.send(c, dst)
+    dist.send(c, dst, group=group)
     if count:
-        dist.send(rays[:count].contiguous().to(dev), dst)
+        dist.send(rays[:count].contiguous().to(dev), dst, group=group)
 
 
-def recv_alive(src: int, out, dist) -> int:
+class _Sends:
+    """pending isends of an alive list and the tensors they read"""
+
+    def __init__(self, works, keep):
+        self.works, self.keep = works, keep
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works, self.keep = [], []
+
+
+def isend_alive(rays, count: int, dst: int, dist, group=None) -> _Sends:
+    """send_alive without blocking: the count and the rows go out as isends;
+    wait() on the result before `rays` is written again (with NCCL it makes the
+    calling stream wait for the transfer)"""
+    import torch
+    dev = "cpu" if _staged(dist, group) else rays.device
+    c = torch.tensor([count], dtype=torch.int64, device=dev)
+    keep, works = [c], [dist.isend(c, dst, group=group)]
+    if count:
+        t = rays[:count].contiguous().to(dev)
+        keep.append(t)
+        works.append(dist.isend(t, dst, group=group))
+    return _Sends(works, keep)
+
+
+def recv_alive(src: int, out, dist, group=None) -> int:
     """Receive an alive list from rank src into out ((cap, 12) int32 tensor);
     returns its length."""
     import torch
-    dev = "cpu" if _staged(dist) else out.device
+    dev = "cpu" if _staged(dist, group) else out.device
     c = torch.zeros(1, dtype=torch.int64, device=dev)
-    dist.recv(c, src)
+    dist.recv(c, src, group=group)
     n = int(c.item())
     if n > out.shape[0]:
         raise RuntimeError(f"alive list of {n} rays exceeds the buffer ({out.shape[0]})")
     if n:
         if dev == "cpu" and out.is_cuda:
             buf = torch.empty((n, out.shape[1]), dtype=out.dtype)
-            dist.recv(buf, src)
+            dist.recv(buf, src, group=group)
             out[:n].copy_(buf)
         else:
             buf = out[:n]
-            dist.recv(buf, src)
+            dist.recv(buf, src, group=group)
     return n
 
 
 class _Done:
     def wait(self):
         return True
+
+
+def two_segment_ticks(rank: int, world: int, tick: int):
+    """(front frame, back frame) rank `rank` marches at `tick` of a two-segment
+    chain (segment_owner): front segment `rank` of frame tick - rank, back
+    segment 2N-1-rank of frame tick - (2N-1-rank).  A front segment's input was
+    handed on by rank - 1 one tick earlier, a back segment's by rank + 1 one
+    tick earlier (rank N-1's back input is its own front output of the tick
+    before), so every wait points to an earlier tick: no rank waits on a later
+    one, and in the steady state every tick completes one frame."""
+    return tick - rank, tick - (2 * world - 1 - rank)
 
 
 def reduce_frame(frame, dist, group=None, async_op=False):
