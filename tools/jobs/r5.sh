@@ -62,6 +62,11 @@ sweep)  # baked C1 on the 8x2x2 copy: occupancy caps and ray splits; config 3 co
   grep -v "round\|amdgpu.ids" $O/variants_baked_C1.log
   timeout -k 10 600 python -u tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method 1 --rounds 6 --env "" "VR_DUO_COMPACT=0" "VR_XBLOCK=1,8" "VR_XBLOCK=2,4" "VR_XBLOCK=1,2" > $O/variants_512x8.log 2>&1; guard $? var $O/variants_512x8.log
   grep -v "round\|amdgpu.ids" $O/variants_512x8.log ;;
+seg2)  # two segments per rank: GPU tests (gloo N = 2 chain, rehearsal), config 5 rehearsal
+  timeout -k 10 900 $PYT tests/test_gpu_bench.py tests/test_gpu_gmm.py -k "gmm and not at_size" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -2 $O/pytest.log
+  timeout -k 10 1000 python -u bench.py --config gmm2048 --slab-rehearsal --segments 2 --steps 5 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1; guard $? gmm5 $O/bench.log
+  grep '^{' $O/bench.log | cut -c1-400 ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
