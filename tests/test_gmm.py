@@ -348,3 +348,97 @@ def test_two_segment_ticks_wait_only_on_earlier_ticks(pkg):
         for f in range(3):
             ticks = [when[(f, i)] for i in range(2 * R)]  # segment i of frame f
             assert all(ticks[i + 1] == ticks[i] + 1 for i in range(2 * R - 1)), (R, ticks)
+
+
+def _two_segment_worker(rank, world, port, q):
+    """bench.py's --segments 2 schedule on the CPU: rank r marches front segment r
+    and back segment 2N-1-r of the oracle's GMM volume at the ticks of
+    slabs.two_segment_ticks, alive lists handed on by isend / recv over two gloo
+    groups (forward, backward), frames summed by a reduce on a third"""
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as g
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        orc = g.load_oracle()
+        S = g.load_package().slabs
+        pkg = g.load_package()
+        dims = (18, 16, 21)
+        m = pkg.camera.display_inv_view((30.0, 45.0))
+        W, H, R, F = 48, 40, world, 3
+        p = orc.make_params(W, H, m, query_method=1, density=0.3)
+        fwd, bwd, asm = (dist.new_group(list(range(world))) for _ in range(3))
+        bounds = S.two_segment_bounds(dims[2], R, S.march_direction(m, W, H))
+        vols = {}
+        for i in (rank, 2 * R - 1 - rank):
+            zb, ns = S.resident_slices(*bounds[i], dims[2])
+            vols[i] = (zb,) + orc.synth_gmm(*dims, 8, z_base=zb, nslices=ns)
+        frames = {f: np.zeros((H, W), np.uint32) for f in range(F)}
+        buf_in = torch.zeros((W * H, S.RAY_WORDS), dtype=torch.int32)
+        own, pend = {}, []
+
+        def march(i, f, rin):
+            zb, wm, sg = vols[i]
+            r = orc.render_gmm(wm, sg, dims, p, z_base=zb, slab=bounds[i], rays_in=rin)
+            frames[f] += r["out"]  # pixels of rays ending in this segment (others 0)
+            return torch.from_numpy(r["rays_out"].view(np.int32).copy())
+
+        for t in range(F + 2 * R - 1):
+            ff, fb = S.two_segment_ticks(rank, R, t)
+            if 0 <= ff < F:
+                rin = None
+                if rank > 0:
+                    n = S.recv_alive(rank - 1, buf_in, dist, group=fwd)
+                    rin = buf_in[:n].numpy().view(np.uint32).copy()
+                out = march(rank, ff, rin)
+                if rank < R - 1:
+                    pend.append(S.isend_alive(out, out.shape[0], rank + 1, dist, group=fwd))
+                else:
+                    own[ff] = out
+            if 0 <= fb < F:
+                if rank == R - 1:
+                    rin = own.pop(fb).numpy().view(np.uint32)
+                else:
+                    n = S.recv_alive(rank + 1, buf_in, dist, group=bwd)
+                    rin = buf_in[:n].numpy().view(np.uint32).copy()
+                out = march(2 * R - 1 - rank, fb, rin)
+                if rank > 0:
+                    pend.append(S.isend_alive(out, out.shape[0], rank - 1, dist, group=bwd))
+                else:
+                    assert out.shape[0] == 0
+        for w in pend:
+            w.wait()
+        res = []
+        for f in range(F):
+            tt = torch.from_numpy(frames[f].view(np.int32).copy())
+            dist.reduce(tt, 0, op=dist.ReduceOp.SUM, group=asm)
+            res.append(tt.numpy().view(np.uint32).copy())
+        if rank == 0:
+            q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_two_segment_chain_matches_whole_volume(orc, pkg, world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_two_segment_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(180)
+        assert pr.exitcode == 0
+    got = q.get()
+    dims = (18, 16, 21)
+    wm, sg = orc.synth_gmm(*dims, 8)
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    full = orc.render_gmm(wm, sg, dims, orc.make_params(48, 40, m, query_method=1, density=0.3))
+    assert np.count_nonzero(full["out"]) > 0
+    for f in got:
+        assert np.array_equal(f, full["out"])
