@@ -93,15 +93,29 @@ def relay_ranks(cmd, env=None):
     replace itself) and stream its output: JSON lines (rank 0's result) to stdout,
     everything else to stderr, so the caller sees exactly one JSON line.  Returns
     the launcher's return code (non-zero when any rank failed)."""
+    import signal
     import subprocess
     env = dict(os.environ if env is None else env)
     env[LAUNCHED_ENV] = "1"
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
-    for line in p.stdout:
-        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
-        sys.stdout.flush()
-    return p.wait()
+
+    def stop(signum, _frame):  # a killed parent takes its ranks with it
+        p.terminate()  # torch.distributed.run forwards it to the ranks
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+        sys.exit(128 + signum)
+    old = {sg: signal.signal(sg, stop) for sg in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for line in p.stdout:
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+        return p.wait()
+    finally:
+        for sg, h in old.items():
+            signal.signal(sg, h)
 
 
 def parse():
