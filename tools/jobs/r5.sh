@@ -67,6 +67,11 @@ seg2)  # two segments per rank: GPU tests (gloo N = 2 chain, rehearsal), config 
   tail -2 $O/pytest.log
   timeout -k 10 1000 python -u bench.py --config gmm2048 --slab-rehearsal --segments 2 --steps 5 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1; guard $? gmm5 $O/bench.log
   grep '^{' $O/bench.log | cut -c1-400 ;;
+m3duo)  # entropy: several samples per slice-compacted box (no gap slices at 1024^3)
+  for CFG in 1024x8 512x8; do
+    timeout -k 10 600 python -u tools/bench_variants.py --variants main --config $CFG --cameras C0 --method 3 --rounds 3 --env "" "VR_PATH=1,VR_DUO=2,VR_DUO_COMPACT=1" "VR_PATH=1,VR_DUO=2,VR_DUO_COMPACT=1,VR_BOX_MAX=2048" "VR_PATH=1,VR_DUO=3,VR_DUO_COMPACT=1,VR_BOX_MAX=2048" "VR_PATH=1,VR_BOX_MAX=2048" > $O/variants_${CFG}_m3.log 2>&1; guard $? var $O/variants_${CFG}_m3.log
+    grep -v "round\|amdgpu.ids" $O/variants_${CFG}_m3.log
+  done ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
