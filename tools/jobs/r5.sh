@@ -6,6 +6,13 @@ cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
 J=${1:?job}; O=gpurun_out/$J; mkdir -p $O
 guard() { rc=$1; if [ $rc -ne 0 ]; then echo "$2 failed rc=$rc"; tail -30 $3; exit $rc; fi; }
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+# a heartbeat file under gpurun_out: tests that run bench.py as a subprocess print
+# nothing for minutes on a fresh box (first torch import); every step still has
+# its own timeout, so a real hang ends there
+( while sleep 50; do date >> $O/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+timeout -k 10 300 python -c "import torch; print('torch', torch.__version__, torch.cuda.is_available())" || exit 1
 case $J in
 launch)  # self-launched N = 2 bench, layout / wide-plane tests, m3 rank-list paths
   timeout -k 10 600 $PYT tests/test_gpu_bench.py tests/test_gpu_layout.py > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
