@@ -375,17 +375,19 @@ def _two_segment_worker(rank, world, port, q):
         for i in (rank, 2 * R - 1 - rank):
             zb, ns = S.resident_slices(*bounds[i], dims[2])
             vols[i] = (zb,) + orc.synth_gmm(*dims, 8, z_base=zb, nslices=ns)
-        frames = {f: np.zeros((H, W), np.uint32) for f in range(F)}
+        frames = {f: torch.zeros((H, W), dtype=torch.int32) for f in range(F)}
         buf_in = torch.zeros((W * H, S.RAY_WORDS), dtype=torch.int32)
-        own, pend = {}, []
+        own, pend, works = {}, [], {}
 
         def march(i, f, rin):
             zb, wm, sg = vols[i]
             r = orc.render_gmm(wm, sg, dims, p, z_base=zb, slab=bounds[i], rays_in=rin)
-            frames[f] += r["out"]  # pixels of rays ending in this segment (others 0)
+            frames[f] += torch.from_numpy(r["out"].view(np.int32))  # rays ending here
             return torch.from_numpy(r["rays_out"].view(np.int32).copy())
 
         for t in range(F + 2 * R - 1):
+            if t == 2 * R - 1:
+                dist.barrier()  # as bench.py's timed window: ranks mid-pipeline
             ff, fb = S.two_segment_ticks(rank, R, t)
             if 0 <= ff < F:
                 rin = None
@@ -408,15 +410,15 @@ def _two_segment_worker(rank, world, port, q):
                     pend.append(S.isend_alive(out, out.shape[0], rank - 1, dist, group=bwd))
                 else:
                     assert out.shape[0] == 0
+                # the rank's last touch of frame fb: its share summed on rank 0,
+                # asynchronously (ranks reach a frame's reduce at different ticks)
+                works[fb] = S.reduce_frame(frames[fb], dist, group=asm, async_op=True)
         for w in pend:
             w.wait()
-        res = []
-        for f in range(F):
-            tt = torch.from_numpy(frames[f].view(np.int32).copy())
-            dist.reduce(tt, 0, op=dist.ReduceOp.SUM, group=asm)
-            res.append(tt.numpy().view(np.uint32).copy())
+        for w in works.values():
+            w.wait()
         if rank == 0:
-            q.put(res)
+            q.put([frames[f].numpy().view(np.uint32).copy() for f in range(F)])
     finally:
         dist.destroy_process_group()
 

@@ -298,18 +298,38 @@ def two_segment_ticks(rank: int, world: int, tick: int):
     return tick - rank, tick - (2 * world - 1 - rank)
 
 
+class _StagedReduce:
+    """an asynchronous gloo reduce of a host copy; wait() puts the sum back into
+    rank 0's device frame"""
+
+    def __init__(self, work, host, frame, root):
+        self.work, self.host, self.frame, self.root = work, host, frame, root
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            if self.root:
+                self.frame.copy_(self.host)
+            self.work = None
+        return True
+
+
 def reduce_frame(frame, dist, group=None, async_op=False):
     """Sum the ranks' frames on rank 0: each pixel was written by the one slab
     where its ray ended (or by none: a miss), every other rank holds 0 there.
-    async_op (RCCL): returns the work handle; its wait() makes the calling
-    stream wait for the reduce.  gloo (staged through host memory) completes
+    async_op: returns a handle whose wait() completes the reduce (RCCL: makes
+    the calling stream wait for it; gloo, staged through host memory: waits and
+    copies the sum into rank 0's frame) -- a rank may not block in it while
+    the ranks it waits for still need this rank (the two-segment schedule's
+    ranks reduce a frame at different ticks).  Without async_op it completes
     before returning."""
-    if _staged(dist) and frame.is_cuda:
+    if _staged(dist, group) and frame.is_cuda:
         h = frame.cpu()
-        dist.reduce(h, 0, op=dist.ReduceOp.SUM, group=group)
-        if dist.get_rank() == 0:
-            frame.copy_(h)
-        return _Done()
+        w = dist.reduce(h, 0, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        r = _StagedReduce(w, h, frame, dist.get_rank() == 0)
+        if not async_op:
+            r.wait()
+        return r
     w = dist.reduce(frame, 0, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
     return w if async_op else _Done()
 
