@@ -139,8 +139,9 @@ int vr_stats_info(const float **d_raw, uint64_t *raw_plane, const float **d_code
 
 /* Layout copies (the micro-brick and axis-rows copies above) are made only
  * within a byte budget: vr_set_layout_budget(bytes) caps their total HBM
- * (default UINT64_MAX = two record-volume copies plus two baked-plane copies,
- * 1/8 padding each: one view class and one change of view; 0 = never make
+ * (default UINT64_MAX = two record-volume copies plus three baked-plane
+ * copies, 1/8 padding each, plus 64 MiB for small volumes' padding: one view
+ * class and one change of view; 0 = never make
  * one, every view marches the records' x rows) and drops resident copies that
  * exceed a lowered budget.  vr_layout_info: bytes resident in copies, copies
  * made since load, and the time and size of the last one made (each is built
