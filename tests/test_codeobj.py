@@ -2,8 +2,8 @@
 metadata, runs nothing).  The LDS-box marches must use no scratch: the
 round-4 k_march_duo<8,3> fault came from a register-capped
 variant build whose duo spilled ~1 KB per lane to a private segment; the shipped
-k_march / k_march_duo instances keep private_segment_fixed_size 0, no dynamic
-stack and at most 256 VGPRs."""
+k_march / k_march_duo / k_march_wgbox instances keep private_segment_fixed_size 0,
+no dynamic stack and at most 256 VGPRs (128 for the 1024-lane workgroup boxes)."""
 import os
 import re
 import subprocess
@@ -52,10 +52,15 @@ def _kernels():
 def test_box_marches_use_no_scratch():
     ks = _kernels()
     box = {n: v for n, v in ks.items()
-           if n and re.match(r"_ZN2vr(11k_march_duo|7k_march)I", n)}
+           if n and re.match(r"_ZN2vr(11k_march_duo|7k_march|13k_march_wgbox)I", n)}
     duo = [n for n in box if "k_march_duo" in n]
     # every (B, M, K) instance of the duo ships: B in 1, 2, 4, 8; M in 1..3; K in 2..4
     assert len(duo) == 4 * 3 * 3, sorted(duo)
+    # workgroup boxes: B in 4, 8; M in 1, 2; K in 2, 4; R in 2, 4 -- less 8-bin K = 4 at
+    # R = 4, which would spill at 1024 lanes' 128 VGPRs
+    wg = [n for n in box if "k_march_wgbox" in n]
+    assert len(wg) == 16 - 2, sorted(wg)
+    assert all(box[n]["vgpr"] <= 128 for n in wg if n.endswith("ELi4EEEvPKfNS_6ParamsE")), wg
     bad = {n: v for n, v in box.items() if v["private"] or v["dynamic_stack"]}
     assert not bad, bad
     assert all(v["vgpr"] <= 256 for v in box.values()), {n: v["vgpr"] for n, v in box.items()}

@@ -83,6 +83,25 @@ static int ray_lines(int x, int y, int nsteps, uint32_t *out /* 8 per step */) {
         lin_axis(py * 0.5f + 0.5f, N, &y0, &y1);
         lin_axis(pz * 0.5f + 0.5f, N, &z0, &z1);
         int ys[2] = {y0, y1}, zs[2] = {z0, z1};
+        if (LAYOUT == 11 || LAYOUT == 12) {
+            /* baked planes as gather8 reads them, 4-B voxels, 32 per line.
+               11: y-pair rows -- element (x, y0, z) holds (v[z][y0][x], v[z][y0+1][x]),
+                   16 x per line, runs of 15 x + one apron voxel: a footprint is
+                   two 16-B loads (z0, z1), one line each.
+               12: 8x2x2 bricks, runs of 7 x + apron (k_plane8): four 8-B loads. */
+            for (int c = 0; c < 4; c++) {
+                uint32_t l;
+                if (LAYOUT == 11)
+                    l = (uint32_t)(((uint64_t)zs[c >> 1] * N + y0) * (N / 15 + 1) + x0 / 15);
+                else
+                    l = (uint32_t)(((uint64_t)(zs[c >> 1] >> 1) * (N / 2) + (ys[c & 1] >> 1)) *
+                                   (N / 7 + 1) + x0 / 7);
+                out[k++] = l;
+                out[k++] = l;
+            }
+            px += sx; py += sy; pz += sz;
+            continue;
+        }
         for (int c = 0; c < 4; c++) {
             out[k++] = line_of(x0, ys[c & 1], zs[c >> 1]);
             out[k++] = line_of(x1, ys[c & 1], zs[c >> 1]);
@@ -123,7 +142,7 @@ int main(int argc, char **argv) {
     fseek(f, 128, SEEK_SET); /* npy v1 header of this shape is 128 bytes */
     if (fread(steps, 4, W * H, f) != W * H) return 1;
     fclose(f);
-    const size_t nlines = (size_t)N * N * N * 32 / 128;
+    const size_t nlines = (size_t)N * N * N * 32 / 128 * ((LAYOUT == 11 || LAYOUT == 12) ? 2 : 1);
     uint8_t *bits = calloc(nlines / 8 + 1, 1);
     uint64_t samples = 0, per_tile = 0, per_wave_step = 0, per_tile_step = 0, per_wave = 0;
     uint64_t per_ring = 0, max_ring = 0, max_tile_step = 0;

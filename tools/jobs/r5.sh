@@ -79,6 +79,21 @@ m3duo)  # entropy: several samples per slice-compacted box (no gap slices at 102
     timeout -k 10 600 python -u tools/bench_variants.py --variants main --config $CFG --cameras C0 --method 3 --rounds 3 --env "" "VR_PATH=1,VR_DUO=2,VR_DUO_COMPACT=1" "VR_PATH=1,VR_DUO=2,VR_DUO_COMPACT=1,VR_BOX_MAX=2048" "VR_PATH=1,VR_DUO=3,VR_DUO_COMPACT=1,VR_BOX_MAX=2048" "VR_PATH=1,VR_BOX_MAX=2048" > $O/variants_${CFG}_m3.log 2>&1; guard $? var $O/variants_${CFG}_m3.log
     grep -v "round\|amdgpu.ids" $O/variants_${CFG}_m3.log
   done ;;
+wg)  # workgroup boxes (k_march_wgbox): parity, then config 3 / config 2 timing by rows and capacity
+  timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "wgbox" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -2 $O/pytest.log
+  for M in 1 2; do
+    timeout -k 10 500 python -u tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method $M --rounds 5 --env "" "VR_WG_ROWS=2" "VR_WG_ROWS=4" "VR_WG_ROWS=2,VR_BOX_WG=6144" "VR_WG_ROWS=4,VR_BOX_WG=6144" "VR_WG_ROWS=2,VR_WG_PER_CU=3" > $O/variants_512x8_m$M.log 2>&1; guard $? var $O/variants_512x8_m$M.log
+    grep -v "round\|amdgpu.ids" $O/variants_512x8_m$M.log
+  done
+  timeout -k 10 400 python -u tools/bench_variants.py --variants main --config 256x4@512x512 --cameras C0 --method 1 --rounds 5 --env "" "VR_WG_ROWS=2" "VR_WG_ROWS=4" > $O/variants_256x4.log 2>&1; guard $? var $O/variants_256x4.log
+  grep -v "round\|amdgpu.ids" $O/variants_256x4.log ;;
+wgpmc)  # fabric bytes per dispatch: per-wave duo vs workgroup boxes at 512^3 C0
+  for E in "" "VR_WG_ROWS=2" "VR_WG_ROWS=4,VR_BOX_WG=6144"; do
+    N=${E:-duo}; N=${N//[=,]/_}
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_$N -o p -- python tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method 1 --rounds 1 --reps 3 --env "$E" > $O/pmc_$N.log 2>&1; guard $? pmc-$N $O/pmc_$N.log
+    python tools/pmc_summary.py $O/pmc_$N "k_march_" | tee $O/pmc_$N.txt
+  done ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done

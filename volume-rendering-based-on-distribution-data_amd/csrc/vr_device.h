@@ -105,6 +105,8 @@ struct Params {
     // bound violations {count, worst index - box size, box voxels, lane footprint}
     unsigned long long *box_check;
     int duo_compact;             // k_march_duo: box of the used slices only (1) or the whole z range (0)
+    int wg_rows;                 // k_march_wgbox: tile rows per workgroup (2 / 4), 0 = per-wave boxes
+    int box_wg;                  // k_march_wgbox: workgroup box capacity (voxels)
 };
 
 // Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one

@@ -629,6 +629,192 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
                 sw * P.brightness);
 }
 
+// ---- the workgroup-box march (k_march_wgbox) ----
+// k_march_duo's boxes are per wave (16 x 4 pixels).  At 512^3 x 8, 1080p, C0 a
+// wave's ~8 x 2 footprint centres need a box of ~9 x 3.4 voxels per slice, and
+// the rows it shares with the tile below -- another workgroup, steps ahead or
+// behind -- are fetched again: the frame decodes ~2.1 voxels per voxel of U
+// and its fabric traffic is 1.98 x the algorithmic bytes.
+// Here a workgroup of R x 256 lanes takes R vertically adjacent tiles (64 x 4R
+// pixels, a 16 x 4 block per wave) and marches them in lockstep: per step the
+// union box of all its lanes' K footprints is fetched and decoded once, by all
+// lanes together, into one LDS box; then every lane blends its own samples.
+// Samples, their order and the compositing are k_march_duo's (bit-identical).
+// Each step: the waves' bounds meet through LDS minima (three rotating sets:
+// set s is cleared two steps before its reuse, so one barrier orders it),
+// a barrier, the decode, a barrier, the samples.  A union box larger than
+// P.box_wg voxels (the first steps of rays entering far apart) samples directly.
+template <int B, int M, int NG>
+__device__ __forceinline__ void wg_chunk(const float *__restrict__ vbase, const Params &P, float *box,
+                                         int dx, int dxy, int V, int p0, int nt, uint32_t tid,
+                                         float rdx, float rdxy) {
+    const uint32_t sy = (uint32_t)P.sy;
+    float rec[NG][B];
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        const int p = min(p0 + g * nt + (int)tid, V - 1);  // clamped: every load issues
+        const int z = (int)(((float)p + 0.5f) * rdxy);
+        const int r = p - z * dxy;
+        const int y = (int)(((float)r + 0.5f) * rdx);
+        const int x = r - y * dx;
+        load_rec<B>(vbase, (uint64_t)(uint32_t)z * P.sz + (uint32_t)(y * sy + x), rec[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        const int p = p0 + g * nt + (int)tid;
+        if (p < V) box[p] = record_stat<B, M>(rec[g], P.enorm);
+    }
+}
+
+template <int B, int M, int K, int R>
+__global__ __launch_bounds__(256 * R) void k_march_wgbox(const float *__restrict__ vol, Params P) {
+    static_assert(M == 1 || M == 2, "mean, variance");
+    static_assert(K >= 2 && K <= 4 && (R == 2 || R == 4), "samples per box, tile rows");
+    constexpr int NT = 256 * R;
+    constexpr int G = B >= 8 ? 2 : 4;  // voxels per lane in flight
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    int *red = reinterpret_cast<int *>(lds);  // 3 sets x 8: min lo x/y/z, min -hi x/y/z
+    float *box = lds + 24;
+    // the group's top tile: an entry of the grouped frame order, or raster groups
+    uint32_t top;
+    if (P.perm) {
+        top = P.perm[blockIdx.x];
+    } else {
+        const uint32_t gi = xcd_slot(blockIdx.x, gridDim.x);
+        top = (gi / P.tiles_x) * R * P.tiles_x + gi % P.tiles_x;
+    }
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t lx = (w & 3u) * 16u + (lane >> 2), ly = (w >> 2) * kTileH + (lane & 3u);
+    const uint32_t x = (top % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (top / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.CW && y < P.CH;
+    const uint64_t o = (uint64_t)y * P.W + x;
+    if (tid < 24) red[tid] = 0x7FFFFFFF;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    __syncthreads();
+    int set = 0;
+    for (int i = 0; i < kMaxSteps; i += K) {
+        Foot f[K];
+        f[0] = footprint(P, px, py, pz);
+        int lo_x = alive ? f[0].x0 : 0x7FFFFFFF, lo_y = alive ? f[0].y0 : 0x7FFFFFFF;
+        int lo_z = alive ? f[0].z0 : 0x7FFFFFFF;
+        int hi_x = alive ? -f[0].x0 : 0x7FFFFFFF, hi_y = alive ? -f[0].y0 : 0x7FFFFFFF;
+        int hi_z = alive ? -f[0].z0 : 0x7FFFFFFF;
+        {
+            bool reach = alive;
+            float tq = t, qx = px, qy = py, qz = pz;
+#pragma unroll
+            for (int k = 1; k < K; k++) {
+                tq = tq + kTStep;
+                reach = reach && !(tq > r.tfar) && i + k < kMaxSteps;
+                qx = qx + stx;
+                qy = qy + sty;
+                qz = qz + stz;
+                f[k] = footprint(P, qx, qy, qz);
+                if (reach) {
+                    lo_x = min(lo_x, f[k].x0);
+                    lo_y = min(lo_y, f[k].y0);
+                    lo_z = min(lo_z, f[k].z0);
+                    hi_x = min(hi_x, -f[k].x0);
+                    hi_y = min(hi_y, -f[k].y0);
+                    hi_z = min(hi_z, -f[k].z0);
+                }
+            }
+        }
+        dpp_min3(lo_x, lo_y, lo_z);
+        dpp_min3(hi_x, hi_y, hi_z);
+        int *rs = red + 8 * set;
+        if (lane == 0 && lo_x != 0x7FFFFFFF) {  // a wave with a live lane
+            atomicMin(rs + 0, lo_x);
+            atomicMin(rs + 1, lo_y);
+            atomicMin(rs + 2, lo_z);
+            atomicMin(rs + 3, hi_x);
+            atomicMin(rs + 4, hi_y);
+            atomicMin(rs + 5, hi_z);
+        }
+        __syncthreads();
+        const int bx0 = rs[0], by0 = rs[1], bz0 = rs[2];
+        const int nhx = rs[3], nhy = rs[4], nhz = rs[5];
+        // set + 2 (mod 3) was read last step, before this barrier, and is next
+        // written two steps on, after the next barrier
+        const int clr = set == 0 ? 2 : set - 1;
+        if (tid < 6) red[8 * clr + tid] = 0x7FFFFFFF;
+        set = set == 2 ? 0 : set + 1;
+        if (bx0 == 0x7FFFFFFF) break;  // no live ray in the workgroup (uniform)
+        const int bx1 = min(-nhx + 1, P.nx - 1);
+        const int by1 = min(-nhy + 1, P.ny - 1);
+        const int bz1 = min(-nhz + 1, P.nz - 1);
+        const int dx = bx1 - bx0 + 1, dy = by1 - by0 + 1, dz = bz1 - bz0 + 1;
+        const int dxy = dx * dy;
+        const int V = dxy * dz;
+        const bool staged = V <= P.box_wg;  // workgroup-uniform
+        if (staged) {
+            const float *vbase =
+                vol + ((uint64_t)bz0 * P.sz + (uint64_t)by0 * P.sy + (uint64_t)bx0) * (uint64_t)B;
+            const float rdx = __builtin_amdgcn_rcpf((float)dx), rdxy = __builtin_amdgcn_rcpf((float)dxy);
+            for (int p0 = 0; p0 < V; p0 += NT * G) {
+                if (V - p0 > NT)
+                    wg_chunk<B, M, G>(vbase, P, box, dx, dxy, V, p0, NT, tid, rdx, rdxy);
+                else
+                    wg_chunk<B, M, 1>(vbase, P, box, dx, dxy, V, p0, NT, tid, rdx, rdxy);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if (alive) {  // the ray reached this sample (t <= tfar): f[k] is in the box
+                const Foot &fk = f[k];
+                float sample;
+                if (staged) {
+                    const int b0 = ((fk.z0 - bz0) * dy + (fk.y0 - by0)) * dx + (fk.x0 - bx0);
+                    const int ox = fk.x1 - fk.x0, oy = (fk.y1 - fk.y0) * dx;
+                    const int oz = (fk.z1 - fk.z0) * dxy;
+                    float sv[8];
+                    sv[0] = box[b0];
+                    sv[1] = box[b0 + ox];
+                    sv[2] = box[b0 + oy];
+                    sv[3] = box[b0 + oy + ox];
+                    sv[4] = box[b0 + oz];
+                    sv[5] = box[b0 + oz + ox];
+                    sv[6] = box[b0 + oz + oy];
+                    sv[7] = box[b0 + oz + oy + ox];
+                    sample = blend8(sv, fk);
+                } else {
+                    sample = sample_direct<B, M>(vol, P, fk);
+                }
+                n = i + k + 1;
+                if (composite(P, sample, sx, sy, sz, sw)) {
+                    alive = false;
+                } else {
+                    t = t + kTStep;
+                    if (t > r.tfar || i + k + 1 >= kMaxSteps) {
+                        alive = false;
+                    } else {
+                        px = px + stx;
+                        py = py + sty;
+                        pz = pz + stz;
+                    }
+                }
+            }
+        }
+        // the next step's decode rewrites the box only after its barrier, which
+        // every wave reaches after these reads
+    }
+    if (!valid) return;
+    if (n == 0) {  // miss (K:302-303): nothing written
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 __device__ __forceinline__ int wave_incl_scan(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
@@ -2822,6 +3008,34 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         // P.duo samples per footprint box (k_march_duo; fill_params: coarse
         // row-aligned 8-bin full frames, VR_DUO)
         const int k = P.duo;
+        // workgroup boxes of P.wg_rows tile rows (fill_params: full frames, 4 / 8 bins)
+        if constexpr (B == 4 || B == 8) {
+            if ((k == 2 || k == 4) && (method == 1 || method == 2) && !P.tile_list &&
+                (P.wg_rows == 2 || P.wg_rows == 4) && P.box_wg > 0 &&
+                !(B == 8 && k == 4 && P.wg_rows == 4)) {  // (1024 lanes: 128 VGPRs, would spill)
+                static const char *names[2][2] = {{"k_march_wgbox2_k2", "k_march_wgbox2_k4"},
+                                                  {"k_march_wgbox4_k2", "k_march_wgbox4_k4"}};
+                note_kernel(names[P.wg_rows == 4][k == 4], B, method);
+                const size_t wl = cap_lds(P, P.wg_per_cu, (24u + (size_t)P.box_wg) * sizeof(float));
+                const dim3 wblock(256u * (uint32_t)P.wg_rows);
+#define VR_WG_L(MM, KK, RR) hipLaunchKernelGGL((k_march_wgbox<B, MM, KK, RR>), grid, wblock, wl, s, vol, P)
+                switch ((P.wg_rows == 4 ? 8 : 0) + (k == 4 ? 4 : 0) + method) {
+                case 1: VR_WG_L(1, 2, 2); break;
+                case 2: VR_WG_L(2, 2, 2); break;
+                case 5: VR_WG_L(1, 4, 2); break;
+                case 6: VR_WG_L(2, 4, 2); break;
+                case 9: VR_WG_L(1, 2, 4); break;
+                case 10: VR_WG_L(2, 2, 4); break;
+                case 13: if constexpr (B != 8) VR_WG_L(1, 4, 4); break;
+                case 14: if constexpr (B != 8) VR_WG_L(2, 4, 4); break;
+                }
+#undef VR_WG_L
+                return hipGetLastError();
+            }
+        }
+        // a grouped launch (fill_params: grid and order by groups of rows) that no
+        // instance above took would cover only some of the tiles
+        if (P.wg_rows) return hipErrorInvalidValue;
         if (k >= 2 && k <= 4 && method >= 1 && method <= 3 && P.box_max > 0) {
             note_kernel(k == 2 ? "k_march_duo" : k == 3 ? "k_march_duo3" : "k_march_duo4", B, method);
 #define VR_DUO_L(MM, KK) hipLaunchKernelGGL((k_march_duo<B, MM, KK>), grid, block, lds, s, vol, P)
