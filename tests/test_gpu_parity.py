@@ -494,11 +494,13 @@ def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune, compact):
 
 
 @pytest.mark.parametrize("order", [None, "0", "1,3", "2,2"])
-@pytest.mark.parametrize("rows,k", [("2", "2"), ("2", "4"), ("4", "2"), ("4", "4")])
+@pytest.mark.parametrize("rows,k", [("2", "2"), ("2", "4"), ("4", "2"), ("4", "4"),
+                                    ("2p", "2"), ("2p", "4")])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_wgbox_march(pkg, orc, gpu, nb, rows, k, order, tune):
     """k_march_wgbox (R tile rows per workgroup marching in lockstep, one union
-    footprint box per step): every frame bit-identical to the oracle -- ragged
+    footprint box per step) and k_march_wgpipe (the next box loaded during this
+    step's samples): every frame bit-identical to the oracle -- ragged
     frames whose last group hangs off the image, rays ending on any sample of a
     box, union boxes over the capacity (direct samples), grouped / raster frame
     orders (VR_XBLOCK), a clipped render_kernel launch -- and tile lists keep the
@@ -506,13 +508,17 @@ def test_wgbox_march(pkg, orc, gpu, nb, rows, k, order, tune):
     import torch
     tune.set("VR_PATH", "1")
     tune.set("VR_DUO", k)
+    pipe = rows.endswith("p")  # k_march_wgpipe: the next box in flight
+    rows = rows.rstrip("p")
     tune.set("VR_WG_ROWS", rows)
+    tune.set("VR_WG_PIPE", "1" if pipe else "0")
     if order is not None:
         tune.set("VR_XBLOCK", order)
     vol = orc.synth_volume(30, 26, 22, nb)
     pkg.init_distribution(vol)
-    name = f"k_march_wgbox{rows}_k{k}<" if not (nb == 8 and k == "4" and rows == "4") \
-        else "k_march_duo4<"
+    name = f"k_march_wg{'pipe' if pipe else 'box'}{rows}_k{k}<"
+    if nb == 8 and k == "4" and rows == "4":
+        name = "k_march_duo4<"
     cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),
             pkg.camera.display_inv_view((0.0, 90.0))]
     for W, H in ((72, 40), (80, 44), (136, 96)):

@@ -94,6 +94,18 @@ wgpmc)  # fabric bytes per dispatch: per-wave duo vs workgroup boxes at 512^3 C0
     timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_$N -o p -- python tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method 1 --rounds 1 --reps 3 --env "$E" > $O/pmc_$N.log 2>&1; guard $? pmc-$N $O/pmc_$N.log
     python tools/pmc_summary.py $O/pmc_$N "k_march_" | tee $O/pmc_$N.txt
   done ;;
+wgp)  # workgroup boxes with the next box in flight (k_march_wgpipe): parity, timing, fabric bytes
+  timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "wgbox" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -2 $O/pytest.log
+  for M in 1 2; do
+    timeout -k 10 500 python -u tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method $M --rounds 5 --env "" "VR_WG_ROWS=2,VR_WG_PIPE=1" "VR_WG_ROWS=2,VR_WG_PIPE=1,VR_BOX_WG=1536" "VR_WG_ROWS=2,VR_WG_PIPE=1,VR_BOX_WG=6144" "VR_WG_ROWS=2,VR_WG_PIPE=1,VR_DUO=4,VR_BOX_WG=6144" "VR_WG_ROWS=2" > $O/variants_512x8_m$M.log 2>&1; guard $? var $O/variants_512x8_m$M.log
+    grep -v "round\|amdgpu.ids" $O/variants_512x8_m$M.log
+  done
+  timeout -k 10 400 python -u tools/bench_variants.py --variants main --config 256x4@512x512 --cameras C0 --method 1 --rounds 5 --env "" "VR_WG_ROWS=2,VR_WG_PIPE=1" > $O/variants_256x4.log 2>&1; guard $? var $O/variants_256x4.log
+  grep -v "round\|amdgpu.ids" $O/variants_256x4.log
+  E="VR_WG_ROWS=2,VR_WG_PIPE=1"
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_pipe -o p -- python tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method 1 --rounds 1 --reps 3 --env "$E" > $O/pmc_pipe.log 2>&1; guard $? pmc $O/pmc_pipe.log
+  python tools/pmc_summary.py $O/pmc_pipe "k_march_" | tee $O/pmc_pipe.txt ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done

@@ -818,6 +818,8 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // records; VR_WG_ROWS = 0 / 2 / 4 overrides, VR_BOX_WG the capacity.
     P.wg_rows = 0;
     P.box_wg = 3072;
+    P.wg_pipe = 0;
+    if (const char *e = vr::tuning("VR_WG_PIPE")) P.wg_pipe = std::atoi(e) != 0;
     if (for_render && P.path == 1 && P.duo >= 2 && !d->d_tile_list && !codec && !flex &&
         (g.nb == 4 || g.nb == 8) && (d->query_method == 1 || d->query_method == 2) &&
         !g.stats) {
@@ -829,6 +831,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
             const int v = std::atoi(e);
             if (v >= 0 && v <= 8192) P.box_wg = v;
         }
+        if (P.wg_pipe) P.box_wg = std::min(P.box_wg, 8000);  // two boxes in 64 KiB of LDS
         // the instances march_b launches: K = 2 / 4, less 8-bin K = 4 at 4 rows
         if ((P.duo != 2 && P.duo != 4) || P.box_wg == 0 || (g.nb == 8 && P.duo == 4 && P.wg_rows == 4))
             P.wg_rows = 0;

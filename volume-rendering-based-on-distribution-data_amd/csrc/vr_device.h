@@ -107,6 +107,7 @@ struct Params {
     int duo_compact;             // k_march_duo: box of the used slices only (1) or the whole z range (0)
     int wg_rows;                 // k_march_wgbox: tile rows per workgroup (2 / 4), 0 = per-wave boxes
     int box_wg;                  // k_march_wgbox: workgroup box capacity (voxels)
+    int wg_pipe;                 // workgroup boxes with the next box in flight (k_march_wgpipe, 2 rows)
 };
 
 // Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one

@@ -815,6 +815,225 @@ __global__ __launch_bounds__(256 * R) void k_march_wgbox(const float *__restrict
                 sw * P.brightness);
 }
 
+// Union bounds (minima of lo, minima of -hi, per axis) of the footprints of
+// samples skip .. skip + K - 1 ahead of this lane's current one, over those the
+// ray reaches by tfar (K:700-705) -- the same float adds the samples take, so
+// the footprints are the ones the march will read.  Rays that end by opacity
+// before them are still counted (a superset: a box is never too small).
+template <int K>
+__device__ __forceinline__ void union_feet(const Params &P, bool alive, float t, float tfar,
+                                           float px, float py, float pz, float stx, float sty,
+                                           float stz, int i, int skip, int (&lo)[3], int (&nhi)[3]) {
+    lo[0] = lo[1] = lo[2] = nhi[0] = nhi[1] = nhi[2] = 0x7FFFFFFF;
+    bool reach = alive;
+    float tq = t, qx = px, qy = py, qz = pz;
+    for (int m = 0; m < skip + K; m++) {
+        if (m > 0) {
+            tq = tq + kTStep;
+            reach = reach && !(tq > tfar) && i + m < kMaxSteps;
+            qx = qx + stx;
+            qy = qy + sty;
+            qz = qz + stz;
+        }
+        if (m >= skip && reach) {
+            const Foot f = footprint(P, qx, qy, qz);
+            lo[0] = min(lo[0], f.x0);
+            lo[1] = min(lo[1], f.y0);
+            lo[2] = min(lo[2], f.z0);
+            nhi[0] = min(nhi[0], -f.x0);
+            nhi[1] = min(nhi[1], -f.y0);
+            nhi[2] = min(nhi[2], -f.z0);
+        }
+    }
+    dpp_min3(lo[0], lo[1], lo[2]);
+    dpp_min3(nhi[0], nhi[1], nhi[2]);
+}
+
+// The workgroup box march with the next box in flight (k_march_wgpipe, R = 2):
+// k_march_wgbox waits, every step, for the slowest of its waves' box loads
+// behind two barriers with nothing to overlap them.  Here the union box of the
+// NEXT K samples is bounded first (positions K steps ahead, same float adds),
+// its first 512 G voxels are loaded into registers (G per lane), this step's
+// samples are blended from the current decoded box while those loads fly, and
+// only then are they decoded into the other LDS box (a larger box's remaining
+// voxels, up to P.box_wg, are loaded and decoded after them).  One step:
+// bounds -> barrier -> issue loads -> samples -> decode -> barrier.
+// Bit-identical to k_march_duo.
+template <int B, int M, int K, int R>
+__global__ __launch_bounds__(256 * R) __attribute__((amdgpu_waves_per_eu(M == 1 || B < 8 ? 4 : 2, 8))) void k_march_wgpipe(const float *__restrict__ vol, Params P) {
+    static_assert(M == 1 || M == 2, "mean, variance");
+    static_assert(K >= 2 && K <= 4 && R == 2, "samples per box, tile rows");
+    constexpr int NT = 256 * R;
+    constexpr int G = B >= 8 ? 2 : 4;  // voxels per lane in flight during the samples
+    constexpr int PRE = NT * G;
+    const int CAP = P.box_wg;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    int *red = reinterpret_cast<int *>(lds);  // 3 sets x 8 (k_march_wgbox)
+    float *stat = lds + 24;                   // two decoded boxes of CAP voxels
+    uint32_t top;
+    if (P.perm) {
+        top = P.perm[blockIdx.x];
+    } else {
+        const uint32_t gi = xcd_slot(blockIdx.x, gridDim.x);
+        top = (gi / P.tiles_x) * R * P.tiles_x + gi % P.tiles_x;
+    }
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t lx = (w & 3u) * 16u + (lane >> 2), ly = (w >> 2) * kTileH + (lane & 3u);
+    const uint32_t x = (top % P.tiles_x) * kTileW + lx;
+    const uint32_t y = (top / P.tiles_x) * kTileH + ly;
+    const bool valid = x < P.CW && y < P.CH;
+    const uint64_t o = (uint64_t)y * P.W + x;
+    if (tid < 24) red[tid] = 0x7FFFFFFF;
+    Ray r;
+    bool alive = valid && make_ray(P, x, y, r);
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sw = 0.0f;
+    float t = r.tnear;
+    float px = r.ox + r.dx * r.tnear, py = r.oy + r.dy * r.tnear, pz = r.oz + r.dz * r.tnear;
+    const float stx = r.dx * kTStep, sty = r.dy * kTStep, stz = r.dz * kTStep;
+    int n = 0;
+    const uint32_t syp = (uint32_t)P.sy;
+    float rec[G][B];
+    // the box a step reads: origin, extent, voxels; V = 0 = sample directly
+    int bx0 = 0, by0 = 0, bz0 = 0, dx = 1, dy = 1, V = 0;
+    bool more = true;  // some lane reaches the box
+    // bounds of the box `skip` steps ahead -> set s; the next box's origin /
+    // extent / voxels (0 when larger than CAP) and whether any lane reaches it
+    int set = 0;
+    auto next_box = [&](int i, int skip, int &nx0, int &ny0, int &nz0, int &ndx, int &ndy, int &nV) {
+        int lo[3], nhi[3];
+        union_feet<K>(P, alive, t, r.tfar, px, py, pz, stx, sty, stz, i, skip, lo, nhi);
+        int *rs = red + 8 * set;
+        if (lane == 0 && lo[0] != 0x7FFFFFFF) {
+            atomicMin(rs + 0, lo[0]);
+            atomicMin(rs + 1, lo[1]);
+            atomicMin(rs + 2, lo[2]);
+            atomicMin(rs + 3, nhi[0]);
+            atomicMin(rs + 4, nhi[1]);
+            atomicMin(rs + 5, nhi[2]);
+        }
+        __syncthreads();
+        // workgroup-uniform: scalar registers
+        nx0 = __builtin_amdgcn_readfirstlane(rs[0]);
+        ny0 = __builtin_amdgcn_readfirstlane(rs[1]);
+        nz0 = __builtin_amdgcn_readfirstlane(rs[2]);
+        const int hx = __builtin_amdgcn_readfirstlane(rs[3]);
+        const int hy = __builtin_amdgcn_readfirstlane(rs[4]);
+        const int hz = __builtin_amdgcn_readfirstlane(rs[5]);
+        const int clr = set == 0 ? 2 : set - 1;  // read last step, written two steps on
+        if (tid < 6) red[8 * clr + tid] = 0x7FFFFFFF;
+        set = set == 2 ? 0 : set + 1;
+        if (nx0 == 0x7FFFFFFF) return false;
+        ndx = min(-hx + 1, P.nx - 1) - nx0 + 1;
+        ndy = min(-hy + 1, P.ny - 1) - ny0 + 1;
+        const int ndz = min(-hz + 1, P.nz - 1) - nz0 + 1;
+        nV = ndx * ndy * ndz;
+        if (nV > CAP) nV = 0;
+        return true;
+    };
+    auto issue = [&](int nx0, int ny0, int nz0, int ndx, int ndy, int nV, int p0) {
+        const float *vbase =
+            vol + ((uint64_t)nz0 * P.sz + (uint64_t)ny0 * P.sy + (uint64_t)nx0) * (uint64_t)B;
+        const int ndxy = ndx * ndy;
+        const float rdx = __builtin_amdgcn_rcpf((float)ndx), rdxy = __builtin_amdgcn_rcpf((float)ndxy);
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int p = min(p0 + g * NT + (int)tid, nV - 1);  // clamped: every load issues
+            const int z = (int)(((float)p + 0.5f) * rdxy);
+            const int rr = p - z * ndxy;
+            const int yy = (int)(((float)rr + 0.5f) * rdx);
+            const int xx = rr - yy * ndx;
+            load_rec<B>(vbase, (uint64_t)(uint32_t)z * P.sz + (uint32_t)(yy * syp + xx), rec[g]);
+        }
+    };
+    auto decode = [&](float *dst, int nV, int p0) {
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int p = p0 + g * NT + (int)tid;
+            if (p < nV) dst[p] = record_stat<B, M>(rec[g], P.enorm);
+        }
+    };
+    // the voxels past the first PRE (boxes larger than the registers hold)
+    auto rest = [&](float *dst, int nx0, int ny0, int nz0, int ndx, int ndy, int nV) {
+        for (int p0 = PRE; p0 < nV; p0 += PRE) {
+            issue(nx0, ny0, nz0, ndx, ndy, nV, p0);
+            decode(dst, nV, p0);
+        }
+    };
+    __syncthreads();  // the bound sets are initialised
+    {  // prologue: the first box, loaded and decoded synchronously
+        int nx0 = 0, ny0 = 0, nz0 = 0, ndx = 1, ndy = 1, nV = 0;
+        more = next_box(0, 0, nx0, ny0, nz0, ndx, ndy, nV);
+        if (more && nV) {
+            issue(nx0, ny0, nz0, ndx, ndy, nV, 0);
+            decode(stat, nV, 0);
+            rest(stat, nx0, ny0, nz0, ndx, ndy, nV);
+        }
+        bx0 = nx0; by0 = ny0; bz0 = nz0; dx = ndx; dy = ndy; V = more ? nV : 0;
+        __syncthreads();
+    }
+    int cur = 0;
+    for (int i = 0; more && i < kMaxSteps; i += K) {
+        // the next box: bounded, then its loads in flight during this step's samples
+        int nx0 = 0, ny0 = 0, nz0 = 0, ndx = 1, ndy = 1, nV = 0;
+        const bool next = i + K < kMaxSteps && next_box(i, K, nx0, ny0, nz0, ndx, ndy, nV);
+        if (next && nV) issue(nx0, ny0, nz0, ndx, ndy, nV, 0);
+        const float *box = stat + cur * CAP;
+        const int dxy = dx * dy;
+#pragma unroll 1  // (unrolled, the 8-bin mean needs one VGPR too many at 4 waves per SIMD)
+        for (int k = 0; k < K; k++) {
+            if (alive) {  // the ray reached this sample: its footprint is in the box
+                const Foot fk = footprint(P, px, py, pz);
+                float sample;
+                if (V) {
+                    const int b0 = ((fk.z0 - bz0) * dy + (fk.y0 - by0)) * dx + (fk.x0 - bx0);
+                    const int ox = fk.x1 - fk.x0, oy = (fk.y1 - fk.y0) * dx;
+                    const int oz = (fk.z1 - fk.z0) * dxy;
+                    float sv[8];
+                    sv[0] = box[b0];
+                    sv[1] = box[b0 + ox];
+                    sv[2] = box[b0 + oy];
+                    sv[3] = box[b0 + oy + ox];
+                    sv[4] = box[b0 + oz];
+                    sv[5] = box[b0 + oz + ox];
+                    sv[6] = box[b0 + oz + oy];
+                    sv[7] = box[b0 + oz + oy + ox];
+                    sample = blend8(sv, fk);
+                } else {
+                    sample = sample_direct<B, M>(vol, P, fk);
+                }
+                n = i + k + 1;
+                if (composite(P, sample, sx, sy, sz, sw)) {
+                    alive = false;
+                } else {
+                    t = t + kTStep;
+                    if (t > r.tfar || i + k + 1 >= kMaxSteps) {
+                        alive = false;
+                    } else {
+                        px = px + stx;
+                        py = py + sty;
+                        pz = pz + stz;
+                    }
+                }
+            }
+        }
+        if (next && nV) {
+            decode(stat + (cur ^ 1) * CAP, nV, 0);
+            rest(stat + (cur ^ 1) * CAP, nx0, ny0, nz0, ndx, ndy, nV);
+        }
+        __syncthreads();  // the next box is decoded; this one is free
+        cur ^= 1;
+        more = next;
+        bx0 = nx0; by0 = ny0; bz0 = nz0; dx = ndx; dy = ndy; V = next ? nV : 0;
+    }
+    if (!valid) return;
+    if (n == 0) {  // miss (K:302-303): nothing written
+        write_miss(P, o);
+        return;
+    }
+    write_pixel(P, o, n, sx * P.brightness, sy * P.brightness, sz * P.brightness,
+                sw * P.brightness);
+}
+
 __device__ __forceinline__ int wave_incl_scan(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
@@ -3013,6 +3232,19 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             if ((k == 2 || k == 4) && (method == 1 || method == 2) && !P.tile_list &&
                 (P.wg_rows == 2 || P.wg_rows == 4) && P.box_wg > 0 &&
                 !(B == 8 && k == 4 && P.wg_rows == 4)) {  // (1024 lanes: 128 VGPRs, would spill)
+                if (P.wg_pipe && P.wg_rows == 2) {  // next box in flight (k_march_wgpipe)
+                    note_kernel(k == 2 ? "k_march_wgpipe2_k2" : "k_march_wgpipe2_k4", B, method);
+                    const size_t pl = cap_lds(P, P.wg_per_cu, (24u + 2u * (size_t)P.box_wg) * sizeof(float));
+#define VR_WGP_L(MM, KK) hipLaunchKernelGGL((k_march_wgpipe<B, MM, KK, 2>), grid, dim3(512), pl, s, vol, P)
+                    switch ((k == 4 ? 4 : 0) + method) {
+                    case 1: VR_WGP_L(1, 2); break;
+                    case 2: VR_WGP_L(2, 2); break;
+                    case 5: VR_WGP_L(1, 4); break;
+                    case 6: VR_WGP_L(2, 4); break;
+                    }
+#undef VR_WGP_L
+                    return hipGetLastError();
+                }
                 static const char *names[2][2] = {{"k_march_wgbox2_k2", "k_march_wgbox2_k4"},
                                                   {"k_march_wgbox4_k2", "k_march_wgbox4_k4"}};
                 note_kernel(names[P.wg_rows == 4][k == 4], B, method);
