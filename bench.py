@@ -461,6 +461,7 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
     free_now, _ = torch.cuda.mem_get_info(dev)
     cap = pkg.slabs.max_slices_for(n, n, K, free_now)
     passes = [rank_period(rows)[0]]
+    best = None  # the balanced cut with the shortest period (a run keeps that cut)
     for p in range(args.rebalance):
         costs = [r["ms"] for r in rows]
         if args.segments == 2:  # every rank a front and a back segment
@@ -469,7 +470,13 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
             bounds = pkg.slabs.bounds_by_cost(n, R, direction, bounds, costs, cap)
         rows = chain(bounds, f"balanced {p + 1}")
         passes.append(rank_period(rows)[0])
+        if best is None or passes[-1] < best[0]:
+            best = (passes[-1], bounds)
     rows_bal = rows
+    if best is not None and args.rebalance > 1:
+        # the kept cut measured again: its period is this fresh run's, not the
+        # minimum over noisy passes
+        rows_bal = chain(best[1], "kept cut")
     period, per_rank = rank_period(rows_bal)
     kernel = pkg.last_kernel()
     worst = max(rows_bal, key=lambda r: r["ms"])
@@ -507,6 +514,8 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
             "slabs_equal": rows_eq,
             "slabs_balanced": rows_bal,
             "period_ms_per_pass": [round(v, 4) for v in passes],
+            "kept_pass": passes.index(min(passes[1:])) if len(passes) > 1 else 0,
+            "kept_cut_remeasured": args.rebalance > 1,
         },
         "roofline": {
             "bound": "hbm", "achieved": worst.get("GBps"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -639,6 +648,7 @@ def gmm_two_segment_run(args, pkg, torch, dist, dev, stream, m, n, K, W, H, rank
     bounds = S.two_segment_bounds(n, R, direction, max_slices=cap)
     generate(bounds)
     passes = []
+    best = None  # (period, cut) of the best measured pass: the steady state runs that cut
     for _ in range(max(args.rebalance, 1)):
         nf = 2
         ev = ([], [])
@@ -650,7 +660,12 @@ def gmm_two_segment_run(args, pkg, torch, dist, dev, stream, m, n, K, W, H, rank
         dist.all_reduce(costs)
         c = costs.cpu().tolist()
         passes.append(max(c[i] + c[2 * R - 1 - i] for i in range(R)))
+        if best is None or passes[-1] < best[0]:
+            best = (passes[-1], list(bounds))
         bounds = S.two_segment_bounds(n, R, direction, bounds, c, cap)
+        generate(bounds)
+    if list(bounds) != best[1]:  # the last re-cut is unmeasured: run the best measured cut
+        bounds = best[1]
         generate(bounds)
     # steady state: W warm-up frames' worth of ticks, then K timed ticks (each
     # completes one frame at rank 0), then the pipeline drains (untimed)

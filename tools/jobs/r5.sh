@@ -106,6 +106,10 @@ wgp)  # workgroup boxes with the next box in flight (k_march_wgpipe): parity, ti
   E="VR_WG_ROWS=2,VR_WG_PIPE=1"
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_pipe -o p -- python tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method 1 --rounds 1 --reps 3 --env "$E" > $O/pmc_pipe.log 2>&1; guard $? pmc $O/pmc_pipe.log
   python tools/pmc_summary.py $O/pmc_pipe "k_march_" | tee $O/pmc_pipe.txt ;;
+seg2b)  # config 5 rehearsal, two segments per rank, more balancing passes (the shortest period's cut kept)
+  [ -n "$BENCH_ONLY" ] || { timeout -k 10 600 $PYT tests/test_gpu_bench.py -k "gmm" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log; tail -2 $O/pytest.log; }
+  timeout -k 10 1100 python -u bench.py --config gmm2048 --slab-rehearsal --segments 2 --rebalance ${PASSES:-5} --steps 5 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1; guard $? gmm5 $O/bench.log
+  grep '^{' $O/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['config']['period_ms_per_pass'], d['config']['kept_pass'], d['config']['rank_ms'])" ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
