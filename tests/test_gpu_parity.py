@@ -560,6 +560,33 @@ def test_wgbox_march(pkg, orc, gpu, nb, rows, k, order, tune):
     assert pkg.last_kernel().startswith("k_march_duo"), pkg.last_kernel()
 
 
+@pytest.mark.parametrize("box_wg", [None, "64"])
+@pytest.mark.parametrize("rows", ["2", "4"])
+def test_wgbox_entropy(pkg, orc, gpu, rows, box_wg, tune):
+    """k_march_wgbox for 8-bin entropy (one sample per union box, k_march's LDS log
+    table and record columns): row-aligned and oblique full frames, ragged sizes,
+    dense and thin media, union boxes over the capacity (direct samples, 2 corners
+    in flight), bit-identical to the oracle"""
+    import torch
+    tune.set("VR_PATH", "1")
+    tune.set("VR_WG_ROWS", rows)
+    if box_wg:
+        tune.set("VR_BOX_WG", box_wg)
+    vol = orc.synth_volume(30, 26, 22, 8)
+    pkg.init_distribution(vol)
+    cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))]
+    for W, H in ((72, 40), (136, 96)):
+        for cam in cams:
+            for density in (0.05, 3.0):
+                got = gpu_render(pkg, None, W, H, cam, 3, torch, density=density)
+                assert pkg.last_kernel().startswith(f"k_march_wgbox{rows}_k1<B=8,M=3>"), \
+                    pkg.last_kernel()
+                ref = orc.render(vol, orc.make_params(W, H, cam, query_method=3,
+                                                      density=density))[:3]
+                assert_parity(got, ref, f"wgbox entropy R={rows} {W}x{H} d={density} "
+                                        f"box_wg={box_wg}")
+
+
 @pytest.mark.parametrize("seg", ["2", "4", "-2", "-4"])
 @pytest.mark.parametrize("nb", [1, 2, 8])
 def test_segmented_march_early_exit(pkg, orc, gpu, seg, nb, tune):

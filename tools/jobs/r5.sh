@@ -110,6 +110,19 @@ seg2b)  # config 5 rehearsal, two segments per rank, more balancing passes (the 
   [ -n "$BENCH_ONLY" ] || { timeout -k 10 600 $PYT tests/test_gpu_bench.py -k "gmm" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log; tail -2 $O/pytest.log; }
   timeout -k 10 1100 python -u bench.py --config gmm2048 --slab-rehearsal --segments 2 --rebalance ${PASSES:-5} --steps 5 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1; guard $? gmm5 $O/bench.log
   grep '^{' $O/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['config']['period_ms_per_pass'], d['config']['kept_pass'], d['config']['rank_ms'])" ;;
+cg)  # entropy workgroup boxes; direct-path corner batch 2 (variant cg2: fewer VGPRs in the box marches)
+  timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "wgbox" > $O/pytest.log 2>&1; guard $? pytest $O/pytest.log
+  tail -2 $O/pytest.log
+  timeout -k 10 600 python -u tools/bench_variants.py --variants main,cg2 --config 1024x8 --cameras C0 --method 3 --rounds 4 --env "" "VR_WG_ROWS=2" "VR_WG_ROWS=4" "VR_WG_ROWS=2,VR_BOX_WG=4096" > $O/variants_1024x8_m3.log 2>&1; guard $? var $O/variants_1024x8_m3.log
+  grep -v "round\|amdgpu.ids" $O/variants_1024x8_m3.log
+  for M in 1 2; do
+    timeout -k 10 500 python -u tools/bench_variants.py --variants main,cg2 --config 512x8 --cameras C0 --method $M --rounds 5 --env "" > $O/variants_512x8_m$M.log 2>&1; guard $? var $O/variants_512x8_m$M.log
+    grep -v "round\|amdgpu.ids" $O/variants_512x8_m$M.log
+  done
+  timeout -k 10 500 python -u tools/bench_variants.py --variants main,cg2 --config 512x8 --cameras C0 --method 3 --rounds 3 --env "" "VR_WG_ROWS=2" > $O/variants_512x8_m3.log 2>&1; guard $? var $O/variants_512x8_m3.log
+  grep -v "round\|amdgpu.ids" $O/variants_512x8_m3.log
+  timeout -k 10 400 python -u tools/bench_variants.py --variants main,cg2 --config 256x4@512x512 --cameras C0 --method 1 --rounds 5 --env "" > $O/variants_256x4.log 2>&1; guard $? var $O/variants_256x4.log
+  grep -v "round\|amdgpu.ids" $O/variants_256x4.log ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done

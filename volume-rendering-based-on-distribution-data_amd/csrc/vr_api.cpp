@@ -820,8 +820,9 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     P.box_wg = 3072;
     P.wg_pipe = 0;
     if (const char *e = vr::tuning("VR_WG_PIPE")) P.wg_pipe = std::atoi(e) != 0;
-    if (for_render && P.path == 1 && P.duo >= 2 && !d->d_tile_list && !codec && !flex &&
-        (g.nb == 4 || g.nb == 8) && (d->query_method == 1 || d->query_method == 2) &&
+    const bool wg_m3 = g.nb == 8 && d->query_method == 3 && P.duo <= 1;  // k_march<8,3>'s frames
+    if (for_render && P.path == 1 && (P.duo >= 2 || wg_m3) && !d->d_tile_list && !codec && !flex &&
+        (g.nb == 4 || g.nb == 8) && (d->query_method == 1 || d->query_method == 2 || wg_m3) &&
         !g.stats) {
         if (const char *e = vr::tuning("VR_WG_ROWS")) {
             const int v = std::atoi(e);
@@ -832,9 +833,15 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
             if (v >= 0 && v <= 8192) P.box_wg = v;
         }
         if (P.wg_pipe) P.box_wg = std::min(P.box_wg, 8000);  // two boxes in 64 KiB of LDS
-        // the instances march_b launches: K = 2 / 4, less 8-bin K = 4 at 4 rows
-        if ((P.duo != 2 && P.duo != 4) || P.box_wg == 0 || (g.nb == 8 && P.duo == 4 && P.wg_rows == 4))
+        // the instances march_b launches: K = 2 / 4, less 8-bin K = 4 at 4 rows;
+        // 8-bin entropy K = 1 (not pipelined)
+        if (wg_m3) {
+            if (P.box_wg == 0) P.wg_rows = 0;
+            P.wg_pipe = 0;
+        } else if ((P.duo != 2 && P.duo != 4) || P.box_wg == 0 ||
+                   (g.nb == 8 && P.duo == 4 && P.wg_rows == 4)) {
             P.wg_rows = 0;
+        }
     }
     // The quad march (path 0: oblique views, B = 8, methods 1-3) of a rank's tile
     // list of <= 700 K rays (N >= 4 GPUs at 1080p) takes two lanes per ray

@@ -647,7 +647,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
 template <int B, int M, int NG>
 __device__ __forceinline__ void wg_chunk(const float *__restrict__ vbase, const Params &P, float *box,
                                          int dx, int dxy, int V, int p0, int nt, uint32_t tid,
-                                         float rdx, float rdxy) {
+                                         float rdx, float rdxy, const LogEnt *tab = nullptr,
+                                         float *st = nullptr) {
     const uint32_t sy = (uint32_t)P.sy;
     float rec[NG][B];
 #pragma unroll
@@ -662,19 +663,35 @@ __device__ __forceinline__ void wg_chunk(const float *__restrict__ vbase, const 
 #pragma unroll
     for (int g = 0; g < NG; g++) {
         const int p = p0 + g * nt + (int)tid;
-        if (p < V) box[p] = record_stat<B, M>(rec[g], P.enorm);
+        if (p < V) box[p] = box_stat<B, M>(rec[g], P, st, tid & 63u, tab);
     }
 }
 
+// Entropy (M = 3, 8 bins, K = 1: one sample per box, as k_march<8,3>): the
+// decode is most of the frame's VALU, and the union box of R tile rows decodes
+// ~20 % fewer slots per wave-step than the per-wave boxes;
+// k_march's LDS log table and per-wave record columns (entropy_stash) sit at
+// the front of the LDS.
 template <int B, int M, int K, int R>
-__global__ __launch_bounds__(256 * R) void k_march_wgbox(const float *__restrict__ vol, Params P) {
-    static_assert(M == 1 || M == 2, "mean, variance");
-    static_assert(K >= 2 && K <= 4 && (R == 2 || R == 4), "samples per box, tile rows");
+__global__ __launch_bounds__(256 * R) __attribute__((amdgpu_waves_per_eu(M == 3 ? 4 : 1, 8))) void k_march_wgbox(const float *__restrict__ vol, Params P) {
+    static_assert(M == 1 || M == 2 || (M == 3 && B == 8 && K == 1), "mean, variance; 8-bin entropy");
+    static_assert(K >= 1 && K <= 4 && (R == 2 || R == 4), "samples per box, tile rows");
     constexpr int NT = 256 * R;
-    constexpr int G = B >= 8 ? 2 : 4;  // voxels per lane in flight
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    int *red = reinterpret_cast<int *>(lds);  // 3 sets x 8: min lo x/y/z, min -hi x/y/z
-    float *box = lds + 24;
+    // voxels per lane in flight (entropy: one, within 128 VGPRs)
+    constexpr int G = M == 3 ? 1 : (B >= 8 ? 2 : 4);
+    extern __shared__ __attribute__((aligned(32))) float lds[];
+    const LogEnt *tab = nullptr;
+    float *st = nullptr;
+    float *base = lds;
+    if constexpr (M == 3) {  // [log table][R x 4 waves' record columns][bounds][box]
+        LogEnt *tb = reinterpret_cast<LogEnt *>(lds);
+        copy_logtab(tb);
+        tab = tb;
+        st = lds + 65u * (sizeof(LogEnt) / 4u) + (threadIdx.x >> 6) * 64u * B;
+        base = lds + 65u * (sizeof(LogEnt) / 4u) + 4u * R * 64u * B;
+    }
+    int *red = reinterpret_cast<int *>(base);  // 3 sets x 8: min lo x/y/z, min -hi x/y/z
+    float *box = base + 24;
     // the group's top tile: an entry of the grouped frame order, or raster groups
     uint32_t top;
     if (P.perm) {
@@ -739,8 +756,13 @@ __global__ __launch_bounds__(256 * R) void k_march_wgbox(const float *__restrict
             atomicMin(rs + 5, hi_z);
         }
         __syncthreads();
-        const int bx0 = rs[0], by0 = rs[1], bz0 = rs[2];
-        const int nhx = rs[3], nhy = rs[4], nhz = rs[5];
+        // workgroup-uniform: scalar registers
+        const int bx0 = __builtin_amdgcn_readfirstlane(rs[0]);
+        const int by0 = __builtin_amdgcn_readfirstlane(rs[1]);
+        const int bz0 = __builtin_amdgcn_readfirstlane(rs[2]);
+        const int nhx = __builtin_amdgcn_readfirstlane(rs[3]);
+        const int nhy = __builtin_amdgcn_readfirstlane(rs[4]);
+        const int nhz = __builtin_amdgcn_readfirstlane(rs[5]);
         // set + 2 (mod 3) was read last step, before this barrier, and is next
         // written two steps on, after the next barrier
         const int clr = set == 0 ? 2 : set - 1;
@@ -760,9 +782,9 @@ __global__ __launch_bounds__(256 * R) void k_march_wgbox(const float *__restrict
             const float rdx = __builtin_amdgcn_rcpf((float)dx), rdxy = __builtin_amdgcn_rcpf((float)dxy);
             for (int p0 = 0; p0 < V; p0 += NT * G) {
                 if (V - p0 > NT)
-                    wg_chunk<B, M, G>(vbase, P, box, dx, dxy, V, p0, NT, tid, rdx, rdxy);
+                    wg_chunk<B, M, G>(vbase, P, box, dx, dxy, V, p0, NT, tid, rdx, rdxy, tab, st);
                 else
-                    wg_chunk<B, M, 1>(vbase, P, box, dx, dxy, V, p0, NT, tid, rdx, rdxy);
+                    wg_chunk<B, M, 1>(vbase, P, box, dx, dxy, V, p0, NT, tid, rdx, rdxy, tab, st);
             }
             __syncthreads();
         }
@@ -786,7 +808,7 @@ __global__ __launch_bounds__(256 * R) void k_march_wgbox(const float *__restrict
                     sv[7] = box[b0 + oz + oy + ox];
                     sample = blend8(sv, fk);
                 } else {
-                    sample = sample_direct<B, M>(vol, P, fk);
+                    sample = sample_direct_cg<B, M, M == 3 ? 2 : VR_DIRECT_CG>(vol, P, fk, tab, st);  // (rare: registers)
                 }
                 n = i + k + 1;
                 if (composite(P, sample, sx, sy, sz, sw)) {
@@ -3229,6 +3251,17 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
         const int k = P.duo;
         // workgroup boxes of P.wg_rows tile rows (fill_params: full frames, 4 / 8 bins)
         if constexpr (B == 4 || B == 8) {
+            if (B == 8 && method == 3 && k <= 1 && !P.tile_list && (P.wg_rows == 2 || P.wg_rows == 4) &&
+                P.box_wg > 0) {  // 8-bin entropy, one sample per box
+                note_kernel(P.wg_rows == 4 ? "k_march_wgbox4_k1" : "k_march_wgbox2_k1", B, method);
+                const size_t el = cap_lds(P, P.wg_per_cu, 65 * sizeof(LogEnt) + 4u * P.wg_rows * 64u * B * sizeof(float) +
+                                                              (24u + (size_t)P.box_wg) * sizeof(float));
+                if (P.wg_rows == 4)
+                    hipLaunchKernelGGL((k_march_wgbox<8, 3, 1, 4>), grid, dim3(1024), el, s, vol, P);
+                else
+                    hipLaunchKernelGGL((k_march_wgbox<8, 3, 1, 2>), grid, dim3(512), el, s, vol, P);
+                return hipGetLastError();
+            }
             if ((k == 2 || k == 4) && (method == 1 || method == 2) && !P.tile_list &&
                 (P.wg_rows == 2 || P.wg_rows == 4) && P.box_wg > 0 &&
                 !(B == 8 && k == 4 && P.wg_rows == 4)) {  // (1024 lanes: 128 VGPRs, would spill)
