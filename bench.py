@@ -155,7 +155,7 @@ def parse():
                          "back one, slabs.two_segment_bounds)")
     ap.add_argument("--rehearsal-ranks", type=int, default=8,
                     help="--slab-rehearsal: slabs (ranks) of the chain (BASELINE config 5: 8)")
-    ap.add_argument("--rebalance", type=int, default=2,
+    ap.add_argument("--rebalance", type=int, default=4,
                     help="GMM z-slabs (N > 1 and --slab-rehearsal): cost-balancing passes "
                          "after the equal cut (each: one untimed frame, slabs re-cut by its "
                          "per-slab costs and regenerated)")

@@ -123,6 +123,9 @@ cg)  # entropy workgroup boxes; direct-path corner batch 2 (variant cg2: fewer V
   grep -v "round\|amdgpu.ids" $O/variants_512x8_m3.log
   timeout -k 10 400 python -u tools/bench_variants.py --variants main,cg2 --config 256x4@512x512 --cameras C0 --method 1 --rounds 5 --env "" > $O/variants_256x4.log 2>&1; guard $? var $O/variants_256x4.log
   grep -v "round\|amdgpu.ids" $O/variants_256x4.log ;;
+gmm5k)  # config 5 rehearsal (two segments per rank) under rocprofv3 --kernel-trace --stats
+  timeout -k 10 1100 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o gmm2048 -- python -u bench.py --config gmm2048 --slab-rehearsal --segments 2 --rebalance 2 --steps 5 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1; guard $? gmm5k $O/bench.log
+  grep '^{' $O/bench.log | cut -c1-300 ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
