@@ -126,6 +126,13 @@ cg)  # entropy workgroup boxes; direct-path corner batch 2 (variant cg2: fewer V
 gmm5k)  # config 5 rehearsal (two segments per rank) under rocprofv3 --kernel-trace --stats
   timeout -k 10 1100 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o gmm2048 -- python -u bench.py --config gmm2048 --slab-rehearsal --segments 2 --rebalance 2 --steps 5 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1; guard $? gmm5k $O/bench.log
   grep '^{' $O/bench.log | cut -c1-300 ;;
+knobs)  # occupancy / samples-per-box sweep of configs 2 and 3 on the final build
+  timeout -k 10 500 python -u tools/bench_variants.py --variants main --config 512x8 --cameras C0 --method 1 --rounds 4 --env "" "VR_WG_PER_CU=3" "VR_WG_PER_CU=5" "VR_WG_PER_CU=6" "VR_BOX_MAX=512" "VR_BOX_MAX=2048" "VR_NO_LPT=1" > $O/variants_512x8.log 2>&1; guard $? var $O/variants_512x8.log
+  grep -v "round\|amdgpu.ids" $O/variants_512x8.log
+  timeout -k 10 500 python -u tools/bench_variants.py --variants main --config 256x4@512x512 --cameras C0 --method 1 --rounds 5 --env "" "VR_DUO=2" "VR_DUO=3" "VR_WG_PER_CU=2" "VR_WG_PER_CU=3" "VR_WG_PER_CU=6" "VR_XBLOCK=0" "VR_XBLOCK=1,1" > $O/variants_256x4.log 2>&1; guard $? var $O/variants_256x4.log
+  grep -v "round\|amdgpu.ids" $O/variants_256x4.log
+  timeout -k 10 500 python -u tools/bench_variants.py --variants main --config 128x1@256x256 --cameras C0 --method 1 --rounds 5 --env "" "VR_SEG=-2" "VR_SEG=4" "VR_WG_PER_CU=2" "VR_XBLOCK=0" > $O/variants_128x1.log 2>&1; guard $? var $O/variants_128x1.log
+  grep -v "round\|amdgpu.ids" $O/variants_128x1.log ;;
 *) echo "unknown job $J"; exit 2 ;;
 esac
 echo done
