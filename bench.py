@@ -63,15 +63,18 @@ LAUNCHED_ENV = "VR_BENCH_RANKS_LAUNCHED"  # set by the self-launch in the ranks'
 def launch_plan(gpus, argv, env):
     """What `bench.py --gpus N` does before any GPU call: ("run", None) = this
     process is the (only or one) rank; ("spawn", cmd) = start N ranks as fresh
-    child processes with cmd; ("error", why) = refuse.  Pure, so the CPU tests
-    cover every branch (tests/test_bench_launch.py)."""
+    child processes with cmd; ("error", why) = refuse.  gpus None = the flag was
+    not given: an external launcher's WORLD_SIZE decides (`torchrun
+    --nproc-per-node 8 bench.py` runs 8 ranks), else one rank.  Only an explicit
+    --gpus that differs from WORLD_SIZE is refused.  Pure, so the CPU tests cover
+    every branch (tests/test_bench_launch.py)."""
     ws = env.get("WORLD_SIZE")
     if ws is not None:
-        if int(ws) != gpus:
+        if gpus is not None and int(ws) != gpus:
             return "error", (f"--gpus {gpus} but WORLD_SIZE {ws}: the launcher started a "
                              f"different number of ranks than asked for")
         return "run", None
-    if gpus <= 1:
+    if gpus is None or gpus <= 1:
         return "run", None
     if env.get(LAUNCHED_ENV):
         return "error", "self-launched rank without WORLD_SIZE (launcher did not set it)"
@@ -120,7 +123,8 @@ def relay_ranks(cmd, env=None):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="1024x8", choices=sorted(CONFIGS) + sorted(GMM_CONFIGS))
@@ -155,6 +159,9 @@ def parse():
                          "back one, slabs.two_segment_bounds)")
     ap.add_argument("--rehearsal-ranks", type=int, default=8,
                     help="--slab-rehearsal: slabs (ranks) of the chain (BASELINE config 5: 8)")
+    ap.add_argument("--link-gbs", type=float, default=153.0,
+                    help="--slab-rehearsal: assumed xGMI point-to-point rate per link (GB/s) "
+                         "for the alive-list hand-off and the frame reduce in the period")
     ap.add_argument("--rebalance", type=int, default=4,
                     help="GMM z-slabs (N > 1 and --slab-rehearsal): cost-balancing passes "
                          "after the equal cut (each: one untimed frame, slabs re-cut by its "
@@ -187,7 +194,11 @@ def traffic_entry(args, kernel, world):
     committed PMC passes (profiles/traffic.json, tools/pmc_traffic.py), or
     (None, why not): only entries measured on this same libvr.so build (its
     sha256) and kernel count -- a rebuilt library needs a new PMC pass"""
-    if world != 1 or not args.traffic_json or not os.path.exists(args.traffic_json):
+    if world != 1:
+        return None, ("no PMC pass of a rank's tile list: the committed passes "
+                      "(profiles/traffic.json) are keyed by whole-frame single-GPU workloads, "
+                      "and rocprofv3 --pmc is not run under the multi-rank launcher")
+    if not args.traffic_json or not os.path.exists(args.traffic_json):
         return None, None
     import __graft_entry__ as graft
     key = f"{args.config}|{args.camera}|m{args.method}" + ("|baked" if args.baked else "")
@@ -318,6 +329,58 @@ def frame_parity(got8, got_f, got_n, kernel, ref, row_stride):
     }
 
 
+def assembled_parity(frame8, ref, row_stride, world, full_render):
+    """N > 1: the frame rank 0 assembled from every rank's gathered tiles (the
+    last timed frame) against the oracle frame of the cpu_baseline, on the rows
+    the oracle rendered (0, s, 2s, ...).  Misses: the oracle leaves them 0, the
+    tiles write 0 (vr.h tile-list mode), so every pixel is compared.  The float
+    RGBA and sample counts come from rank 0's whole-frame render of the same
+    view (full_render, frame_parity): the tiles carry packed RGBA8 only."""
+    rows = slice(0, None, row_stride)
+    g8, r8 = frame8[rows], ref[0][rows]
+    return {
+        "against": "oracle frame of the cpu_baseline (same volume, camera, method)",
+        "frame": f"assembled on rank 0 from the tiles of {world} ranks (last timed frame)",
+        "rows": int(g8.shape[0]), "row_stride": row_stride, "pixels": int(g8.size),
+        "rgba8_mismatch": int(np.sum(g8 != r8)),
+        "max_abs": full_render["max_abs"], "tol": full_render["tol"],
+        "steps_mismatch": full_render["steps_mismatch"],
+        "float_and_steps_from": "rank 0's whole-frame render of the view",
+        "full_frame_render": full_render,
+    }
+
+
+def aggregate_roofline(per_rank, ms_per_step, peak_gbs=HBM_PEAK_GBS):
+    """Whole-node roofline of an N-rank frame.  per_rank: one row per rank of
+    (algorithmic bytes of its launch, U of its tile list or -1, its render ms
+    alone, pixels it renders).  Every rank reads its own footprint from its own
+    HBM, so the node's algorithmic bytes are the sum over ranks and its peak is
+    N x 8 TB/s: frac = sum(alg) / ms_per_step / (N x peak).  Beside it the same
+    bytes over the slowest rank's render alone (what the frame's compute could
+    reach without the gather, the assembly and the host) and the slowest
+    rank's own fraction."""
+    per_rank = np.asarray(per_rank, dtype=np.float64)
+    n = per_rank.shape[0]
+    alg, u, ms, px = per_rank.T
+    total = float(alg.sum())
+    node = total / (ms_per_step * 1e-3) / 1e9
+    slow = int(np.argmax(ms))
+    frac = lambda b, t, k: round(b / (t * 1e-3) / 1e9 / (k * peak_gbs), 4)
+    return {
+        "ranks": n, "peak": n * peak_gbs, "unit": "GB/s",
+        "alg_bytes_per_frame": int(total),
+        "U_records": int(u.sum()) if np.all(u >= 0) else None,
+        "achieved": round(node, 1), "frac": frac(total, ms_per_step, n),
+        "of": "sum over ranks of the algorithmic bytes / ms_per_step / (N x 8 TB/s)",
+        "render_ms_max_over_ranks": round(float(ms[slow]), 4),
+        "frac_at_render_max": frac(total, ms[slow], n),
+        "slowest_rank": slow, "slowest_rank_frac": frac(alg[slow], ms[slow], 1),
+        "per_rank": [{"rank": r, "alg_bytes": int(alg[r]), "U_records": int(u[r]) if u[r] >= 0 else None,
+                      "render_ms": round(float(ms[r]), 4), "pixels": int(px[r]),
+                      "frac": frac(alg[r], ms[r], 1)} for r in range(n)],
+    }
+
+
 def balanced_lists(pkg, lists, world, rank, W, H, m, method, dev, stream, backend):
     """Re-deal the tiles by measured cost (untimed, once per view): every rank
     renders its estimate-ordered list once with per-pixel sample counts, the
@@ -379,13 +442,13 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
     slabs (march order) are generated in HBM one at a time, untimed, as rank r
     holds slab r; each slab's march is timed with HIP events over --steps frames
     of its real input (slab 0: the camera rays; slab r: the alive list slab r - 1
-    handed on, kept in HBM); its U is counted on the same input.  Two passes:
-    equal slabs, then the cost-balanced cut bench.py's N-rank run makes after
-    its untimed first frame (slabs.bounds_by_cost).  The pipeline period of the
-    R-GPU chain is at least its slowest slab's march (the RCCL hand-off of the
-    alive list and the frame reduce run beside it on other streams and are not
-    in this number): value = W*H / max over slabs.  Not an N-GPU measurement:
-    n_gpus 1, scaling null."""
+    handed on, kept in HBM); its U is counted on the same input.  Passes: equal
+    slabs, then --rebalance cost-balanced cuts as the N-rank run makes them
+    (slabs.bounds_by_cost / two_segment_bounds), the best one re-measured.  The
+    line is an ESTIMATE of the R-GPU pipeline period, not a measurement: the
+    max over ranks of (alive lists received + march + sent + the frame into the
+    reduce), the transfers priced at --link-gbs (slabs.period_with_handoff);
+    value null, n_gpus 1, scaling null."""
     R = args.rehearsal_ranks
     direction = pkg.slabs.march_direction(m, W, H)
     frame = torch.zeros(W * H, dtype=torch.int32, device=dev)
@@ -393,8 +456,8 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
     bufs = [torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device=dev)
             for _ in range(2)]
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    # the library launches on `stream` (pkg.set_stream): the alive-list counter
-    # is zeroed on the same stream, so every launch starts from an empty list
+    # the library launches on `stream` (pkg.set_stream) and resets the alive-list
+    # counter there itself; the events and cnt.item() below use the same stream
     assert torch.cuda.current_stream(dev) == stream
 
     def chain(bounds, label):
@@ -411,11 +474,9 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
             gen_s = time.perf_counter() - tg
             out, inp = bufs[i % 2], bufs[(i + 1) % 2]
             slab = pkg.gmm_slab(z_lo, z_hi, out, cnt, d_rays_in=inp if i else None, n_rays_in=n_in)
-            cnt.zero_()
             u = pkg.gmm_count_footprint(desc, slab)
             ev = []
             for f in range(args.warmup + args.steps):
-                cnt.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 pkg.render_gmm(desc, slab)
@@ -428,9 +489,9 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
             if n_out > (n_in if i else W * H):
                 raise RuntimeError(f"slab {i}: {n_out} alive rays out of {n_in if i else W * H} in")
             # algorithmic bytes of the slab's launch: its footprint records, the
-            # alive list in and out (48 B a ray), the pixels of rays ending here
+            # alive list in and out, the pixels of rays ending here
             ended = (W * H if i == 0 else n_in) - n_out
-            alg = u * rec_bytes + (n_in + n_out) * 48 + max(ended, 0) * 4
+            alg = u * rec_bytes + (n_in + n_out) * pkg.slabs.RAY_WORDS * 4 + max(ended, 0) * 4
             rows.append({"slab": i, "z": [z_lo, z_hi], "resident_slices": ns,
                          "rays_in": n_in if i else W * H, "rays_out": n_out,
                          "ms": round(ms, 4), "U_records": int(u), "alg_bytes": int(alg),
@@ -454,13 +515,19 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
             per[r] += row["ms"]
         return max(per), per
 
+    def estimate(rows):
+        """the period estimate with the hand-off (what a pass is judged by)"""
+        return pkg.slabs.period_with_handoff(
+            [r["ms"] for r in rows], [r["rays_out"] for r in rows], owners(len(rows)), R,
+            W * H * 4, args.link_gbs)
+
     pkg.free_gmm()
     torch.cuda.empty_cache()
     bounds = pkg.slabs.slab_bounds(n, R, direction)
     rows_eq = rows = chain(bounds, "equal")
     free_now, _ = torch.cuda.mem_get_info(dev)
     cap = pkg.slabs.max_slices_for(n, n, K, free_now)
-    passes = [rank_period(rows)[0]]
+    passes = [estimate(rows)[0]]
     best = None  # the balanced cut with the shortest period (a run keeps that cut)
     for p in range(args.rebalance):
         costs = [r["ms"] for r in rows]
@@ -469,7 +536,7 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
         else:
             bounds = pkg.slabs.bounds_by_cost(n, R, direction, bounds, costs, cap)
         rows = chain(bounds, f"balanced {p + 1}")
-        passes.append(rank_period(rows)[0])
+        passes.append(estimate(rows)[0])
         if best is None or passes[-1] < best[0]:
             best = (passes[-1], bounds)
     rows_bal = rows
@@ -477,14 +544,29 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
         # the kept cut measured again: its period is this fresh run's, not the
         # minimum over noisy passes
         rows_bal = chain(best[1], "kept cut")
-    period, per_rank = rank_period(rows_bal)
+    march_period, per_rank = rank_period(rows_bal)
+    # the hand-off: every segment's alive list crosses one xGMI link to the next
+    # rank (none between the two segments rank N-1 holds), every rank's frame
+    # goes into the reduce; at the stated link rate (slabs.period_with_handoff)
+    serial, overlap, handoff = estimate(rows_bal)
+    for r in rows_bal:
+        r["bytes_out"] = r["rays_out"] * pkg.slabs.RAY_WORDS * 4
+    period = serial
     kernel = pkg.last_kernel()
     worst = max(rows_bal, key=lambda r: r["ms"])
     cpu = None if args.no_cpu_baseline else gmm_cpu_baseline(m, args.method, W, H, K)
     out = {
         "metric": f"Mrays/s + fps at {n}^3 x {K}-component GMM volume, {W}x{H}; % HBM roofline "
-                  f"({R}-rank slab chain rehearsed on one GPU: pipeline-period estimate)",
-        "value": round(W * H / (period * 1e-3) / 1e6, 3),
+                  f"({R}-rank slab chain rehearsed on one GPU: pipeline-period ESTIMATE, "
+                  "not a measured N-GPU rate)",
+        "value": None,
+        "estimated_Mrays_s": round(W * H / (period * 1e-3) / 1e6, 3),
+        "period_estimate_ms": round(period, 4),
+        "period_estimate": (f"max over ranks of (alive lists received + march + sent + frame "
+                            f"into the reduce), transfers at {args.link_gbs} GB/s per xGMI link "
+                            "(assumed, not measured: one GPU here), nothing overlapped"),
+        "period_overlapped_ms": round(overlap, 4),
+        "period_march_only_ms": round(march_period, 4),
         "unit": "Mrays/s",
         "n_gpus": 1,
         "physical_gpus": 1,
@@ -492,8 +574,8 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
         "rehearsal_ranks": R,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(period, 4),
-        "fps": round(1e3 / period, 2),
+        "ms_per_step": None,
+        "fps": None,
         "higher_is_better": True,
         "scaling": None,
         "vs_baseline": None,
@@ -508,9 +590,11 @@ def gmm_slab_rehearsal(args, pkg, torch, dev, stream, m, n, K, W, H, rec_bytes):
                            "GPU (each segment's march timed on its real alive-list input; "
                            "hand-off and frame reduce not timed)",
             "segments_per_rank": args.segments,
-            "period": "max over ranks of its segments' summed mean march time (HIP events, "
-                      f"{args.steps} frames after {args.warmup} warm-up)",
+            "march": "each segment's mean march time (HIP events, "
+                     f"{args.steps} frames after {args.warmup} warm-up)",
             "rank_ms": [round(v, 4) for v in per_rank],
+            "handoff": handoff,
+            "ray_bytes": pkg.slabs.RAY_WORDS * 4,
             "slabs_equal": rows_eq,
             "slabs_balanced": rows_bal,
             "period_ms_per_pass": [round(v, 4) for v in passes],
@@ -585,7 +669,6 @@ def gmm_two_segment_run(args, pkg, torch, dist, dev, stream, m, n, K, W, H, rank
                 out = f_out[ff % 2]
                 if state["sf"] is not None:
                     state["sf"].wait()
-                cnt.zero_()
                 if seg_ev is not None:
                     e0 = torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
@@ -611,7 +694,6 @@ def gmm_two_segment_run(args, pkg, torch, dist, dev, stream, m, n, K, W, H, rank
                     rin = b_in
                 if state["sb"] is not None:
                     state["sb"].wait()
-                cnt.zero_()
                 if seg_ev is not None:
                     e0 = torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
@@ -814,7 +896,6 @@ def main_gmm(args):
             frame.zero_()  # C:208
             n_in = 0
             if world > 1:
-                cnt.zero_()
                 if rank > 0:
                     n_in = pkg.slabs.recv_alive(rank - 1, rays_in, dist)
             if timed:
@@ -854,6 +935,16 @@ def main_gmm(args):
         # period 6.44 ms equal, 4.51 after one pass; profiles/r05).
         direction = pkg.slabs.march_direction(m, W, H)
         bounds = pkg.slabs.slab_bounds(n, world, direction)
+        cdev = dev if args.dist_backend == "nccl" else "cpu"
+        best = None  # (max rank ms, cut) of the best measured pass: the timed frames run it
+
+        def regenerate(cut):
+            pkg.free_gmm()
+            zb, ns = pkg.slabs.resident_slices(*cut[rank], n)
+            pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
+            torch.cuda.synchronize()
+            return cut[rank]
+
         for _ in range(max(args.rebalance, 1)):
             step(True)
             drain()
@@ -862,19 +953,22 @@ def main_gmm(args):
             alive.clear()
             pkg.free_gmm()
             free_now, _ = torch.cuda.mem_get_info(dev)
-            cdev = dev if args.dist_backend == "nccl" else "cpu"
             costs = torch.zeros(world, dtype=torch.float64, device=cdev)
             costs[rank] = ms
             dist.all_reduce(costs)
+            c = costs.cpu().tolist()
+            if best is None or max(c) < best[0]:
+                best = (max(c), list(bounds))
             cap = torch.tensor([pkg.slabs.max_slices_for(n, n, K, free_now)], dtype=torch.int64,
                                device=cdev)
             dist.all_reduce(cap, op=dist.ReduceOp.MIN)
-            bounds = pkg.slabs.bounds_by_cost(n, world, direction, bounds, costs.cpu().tolist(),
-                                              int(cap.item()))
-            z_lo, z_hi = bounds[rank]
-            zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
-            pkg.synthesize_gmm((n, n, n), K, SEED, z_base=zb, nslices=ns)
-            torch.cuda.synchronize()
+            bounds = pkg.slabs.bounds_by_cost(n, world, direction, bounds, c, int(cap.item()))
+            z_lo, z_hi = regenerate(bounds)
+        if list(bounds) != best[1]:
+            # the last re-cut was never measured (re-cuts that assume a uniform
+            # cost inside each slab can oscillate): time the best measured cut
+            bounds = best[1]
+            z_lo, z_hi = regenerate(bounds)
         balanced = True
     # U before the warm-up (as in main(): the counting pass warms clocks and translation)
     u = pkg.gmm_count_footprint(desc) if world == 1 else None
@@ -972,6 +1066,7 @@ def main():
         print(f"bench.py: starting {args.gpus} ranks: {' '.join(detail)}", file=sys.stderr,
               flush=True)
         sys.exit(relay_ranks(detail))
+    args.gpus = int(os.environ.get("WORLD_SIZE", "1"))  # launch_plan checked any explicit --gpus
     if args.config in GMM_CONFIGS:
         if args.baked:
             raise SystemExit("--baked applies to the histogram / codec volumes (DESIGN.md s12)")
@@ -1171,12 +1266,16 @@ def main():
                 ev.append((e0, e1))
         torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    render_ms_max = kern_ms
+    per_rank = None
     if world > 1:
-        t = torch.tensor([kern_ms], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        render_ms_max = float(t.item())
+        # every rank's (alg bytes, U, render ms, pixels), summed into a world x 4
+        # table: the whole-node roofline (aggregate_roofline)
+        per_rank = torch.zeros((world, 4), dtype=torch.float64,
+                               device=dev if args.dist_backend == "nccl" else "cpu")
+        per_rank[rank] = torch.tensor([float(alg_bytes or 0), float(u if u is not None else -1),
+                                       kern_ms, float(pixels)], dtype=torch.float64)
+        dist.all_reduce(per_rank)
+        per_rank = per_rank.cpu().numpy()
     if args.dump_frame and rank == 0:
         np.save(args.dump_frame, frame.cpu().numpy().view(np.uint32).reshape(H, W))
     kernel = pkg.last_kernel()
@@ -1215,17 +1314,25 @@ def main():
     value = W * H / (elapsed / args.steps) / 1e6
     phys = min(world, max(ndev, 1))
     rehearsal = world > phys
+    aggregate = (aggregate_roofline(per_rank, ms_per_step)
+                 if per_rank is not None and np.all(per_rank[:, 0] > 0) else None)
     out = None
     if rank == 0:
         cpu, parity = None, None
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
+            # N > 1 too: the same oracle frame the N = 1 line checks, compared
+            # with the frame rank 0 assembled from the ranks' tiles
             cpu, (ref, stride) = cpu_baseline(pkg, args.config, m, args.method,
                                               args.cpu_row_stride)
             parity = frame_parity(*check, ref=ref, row_stride=stride)
             parity["timed_kernel"] = kernel
+            if world > 1:
+                parity = assembled_parity(frame.cpu().numpy().view(np.uint32).reshape(H, W),
+                                          ref, stride, world, parity)
         elif world > 1:
             got = frame.cpu().numpy().view(np.uint32).reshape(H, W)
-            parity = {"against": "rank 0's whole-frame render of the same view",
+            parity = {"against": "rank 0's whole-frame render of the same view (no oracle: "
+                                 "--no-cpu-baseline)",
                       "pixels": W * H, "rgba8_mismatch": int(np.sum(got != check[0])),
                       "kernel": check[3]}
         out = {
@@ -1271,7 +1378,6 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": kernel,
                 "kernel_ms": round(kern_ms, 4),
-                "render_ms_max_over_ranks": round(render_ms_max, 4) if world > 1 else None,
                 "alg_bytes_per_launch": int(alg_bytes) if alg_bytes else None,
                 "U_records": int(u) if u is not None else None,
                 "compute": bounds,
@@ -1287,6 +1393,19 @@ def main():
             "parity": parity,
             "cpu_baseline": cpu,
         }
+        if world > 1:
+            # the node's line: achieved / peak / frac are the whole node's (sum of
+            # the ranks' algorithmic bytes over ms_per_step against N x 8 TB/s);
+            # rank 0's own launch (a smaller share: it also assembles) moves to "rank0"
+            roof = out["roofline"]
+            roof["rank0"] = {k: roof.pop(k) for k in ("achieved", "frac", "kernel_ms",
+                                                      "alg_bytes_per_launch", "U_records")}
+            roof["aggregate"] = aggregate
+            roof["achieved"] = aggregate["achieved"] if aggregate else None
+            roof["peak"] = aggregate["peak"] if aggregate else HBM_PEAK_GBS * world
+            roof["frac"] = aggregate["frac"] if aggregate else None
+            roof["render_ms_max_over_ranks"] = (aggregate["render_ms_max_over_ranks"]
+                                                if aggregate else None)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -311,22 +311,24 @@ uint32_t vr_tiles_y(uint32_t height);
 const char *vr_last_kernel(void);
 
 /* Tooling: while d_buf is non-null, every launch of the per-ray pipelined,
- * quad and ray-segmented marches writes 3 uint64 per wave: wall clock at the
+ * quad and ray-segmented marches overwrites 3 uint64 per wave (no zeroing
+ * needed, nothing accumulates): wall clock at the
  * wave's start and end (100 MHz) and __smid() (CU id, XCC id in the high
  * bits), at d_buf[(slot*4 + wave)*3] (pipelined, quad), d_buf[(slot*8 +
  * half*4 + wave)*3] (k_march_quad2) or d_buf[(slot*16 + part*4 + wave)*3]
  * (segmented).  d_buf must hold 48 * n_slots values.  nullptr turns it off. */
 int vr_debug_wave_clock(uint64_t *d_buf);
 
-/* Tooling: while d_buf (6 x uint64 device memory, caller-zeroed) is non-null, a
- * library built with -DVR_BOX_CHECK counts the LDS-box bound violations of the
- * staged marches (k_march, k_march_duo): d_buf[0] = reads whose box index or
- * footprint falls outside the wave's box (each such read is skipped),
- * d_buf[1] = the largest box index + 1 - box voxels seen, d_buf[2] = box
- * voxels of a box whose far corner lies outside the volume; and the decode
- * work: d_buf[3] = box voxels decoded, d_buf[4] = lane slots spent on them
- * (64 per group).  Returns 1 for a checking build, 0 for the default build
- * (which counts nothing). */
+/* Tooling: d_buf = 6 x uint64 of device memory, zeroed by this call on the
+ * library's stream (vr_set_stream); while it is non-null, every launch of the
+ * staged marches (k_march, k_march_duo) of a library built with -DVR_BOX_CHECK
+ * accumulates into it: d_buf[0] = reads whose box index or footprint falls
+ * outside the wave's box (each such read is skipped), d_buf[1] = the largest
+ * box index + 1 - box voxels seen, d_buf[2] = box voxels of a box whose far
+ * corner lies outside the volume; and the decode work: d_buf[3] = box voxels
+ * decoded, d_buf[4] = lane slots spent on them (64 per group); d_buf[5] is
+ * unused.  Returns 1 for a checking build, 0 for the default build (which
+ * counts nothing). */
 int vr_debug_box_check(uint64_t *d_buf);
 
 /* Device self-test: compares the entropy decode's fast float logarithms (the
@@ -432,9 +434,10 @@ int vr_gmm_select(int slot);
  * float sum[4], t, pos[3]; uint32 pixel, samples taken, 0, 0).  Rays that end in
  * the slab are written to the frame (d_output etc., pixel y*width + x); rays that
  * leave it alive are appended to d_rays_out (capacity: n_rays_in, or
- * width*height) and counted in *d_n_rays_out (caller-zeroed, device memory;
- * a count above the capacity means it was not zeroed: entries past the
- * capacity are dropped, never written).
+ * width*height) and counted in *d_n_rays_out (device memory; the call sets it
+ * to 0 on the library's stream before its launch, so the caller reads it
+ * after synchronising with that stream; entries past the capacity would be
+ * dropped, never written).
  * Slabs must be rendered in the order the view's rays cross them (every ray of
  * the frame must step the same way in z, else VR_ERR_UNSUPPORTED); the chain
  * then reproduces the whole-volume render bit for bit. */

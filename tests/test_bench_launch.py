@@ -91,3 +91,46 @@ def test_self_launched_ranks_failing_fail_the_parent():
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert "starting 2 ranks" in r.stderr
+
+
+def test_plan_without_gpus_flag_follows_the_launcher():
+    """ADVICE r5: `torchrun --nproc-per-node 8 bench.py` (no --gpus) runs 8 ranks;
+    only an explicit --gpus that differs from WORLD_SIZE is refused"""
+    b = _bench()
+    assert b.launch_plan(None, [], {"WORLD_SIZE": "8"}) == ("run", None)
+    assert b.launch_plan(None, [], {}) == ("run", None)
+    assert b.launch_plan(2, [], {"WORLD_SIZE": "8"})[0] == "error"
+
+
+def test_aggregate_roofline_sums_the_ranks():
+    """N > 1 bench line: the node's algorithmic bytes are the ranks' sum, its peak
+    N x 8 TB/s, against ms_per_step; the slowest rank's own fraction beside it"""
+    b = _bench()
+    # (alg bytes, U, render ms, pixels) of 4 ranks
+    rows = [[1.0e9, 10, 0.50, 1000], [2.0e9, 20, 0.80, 2000],
+            [1.5e9, 15, 0.60, 1500], [1.5e9, 15, 0.70, 1500]]
+    a = b.aggregate_roofline(rows, ms_per_step=1.0)
+    assert a["ranks"] == 4 and a["peak"] == 4 * 8000.0
+    assert a["alg_bytes_per_frame"] == 6_000_000_000 and a["U_records"] == 60
+    # 6 GB in 1 ms = 6000 GB/s of 32000
+    assert a["achieved"] == 6000.0 and a["frac"] == round(6000 / 32000, 4)
+    assert a["slowest_rank"] == 1 and a["render_ms_max_over_ranks"] == 0.8
+    assert a["slowest_rank_frac"] == round(2e9 / 0.8e-3 / 1e9 / 8000, 4)
+    assert a["frac_at_render_max"] == round(6e9 / 0.8e-3 / 1e9 / 32000, 4)
+    assert [r["rank"] for r in a["per_rank"]] == [0, 1, 2, 3]
+    # a rank without a footprint count (U = -1) leaves the node's U unknown
+    rows[2][1] = -1
+    assert b.aggregate_roofline(rows, 1.0)["U_records"] is None
+
+
+def test_assembled_parity_counts_every_pixel_of_the_oracle_rows():
+    import numpy as np
+    b = _bench()
+    ref8 = np.arange(24, dtype=np.uint32).reshape(6, 4)
+    got = ref8.copy()
+    got[1, 0] += 1  # a row the oracle skipped at stride 2: not compared
+    got[2, 3] += 1  # a compared row
+    full = {"max_abs": 0.0, "tol": 1e-4, "steps_mismatch": 0}
+    p = b.assembled_parity(got, (ref8, None, None), 2, 4, full)
+    assert p["rows"] == 3 and p["pixels"] == 12 and p["rgba8_mismatch"] == 1
+    assert p["row_stride"] == 2 and "4 ranks" in p["frame"]

@@ -41,10 +41,27 @@ def test_bench_single_and_two_rank_frames_agree(gpu, tmp_path):
     f2 = str(tmp_path / "f2.npy")
     # bench.py starts its own 2 ranks (no external launcher), as the driver's
     # `python bench.py --gpus N` does
-    out2 = _run([sys.executable, "bench.py", "--gpus", "2", *ARGS, "--dist-backend", "gloo",
+    # (with the CPU baseline: at N > 1 rank 0 compares the ASSEMBLED frame with
+    # the oracle's)
+    args2 = [a for a in ARGS if a != "--no-cpu-baseline"]
+    out2 = _run([sys.executable, "bench.py", "--gpus", "2", *args2, "--dist-backend", "gloo",
                  "--dump-frame", f2], tmp_path)
     assert out2["n_gpus"] == 2 and out2["physical_gpus"] == 1
     assert out2["rehearsal_shared_gpus"] is True and out2["scaling"] is None
+    cpu = out2["cpu_baseline"]
+    assert cpu["value"] > 0 and cpu["kind"] == "port" and cpu["cores"] >= 1
+    par = out2["parity"]
+    assert "assembled" in par["frame"] and par["against"].startswith("oracle")
+    assert par["pixels"] > 0 and par["rgba8_mismatch"] == 0
+    assert par["steps_mismatch"] == 0 and par["max_abs"] <= 1e-4
+    rf2 = out2["roofline"]
+    agg = rf2["aggregate"]
+    assert agg["ranks"] == 2 and agg["peak"] == 16000.0 and len(agg["per_rank"]) == 2
+    assert sum(r["pixels"] for r in agg["per_rank"]) >= 512 * 512
+    assert rf2["frac"] == agg["frac"] and 0 < agg["frac"] < 1
+    assert agg["render_ms_max_over_ranks"] == max(r["render_ms"] for r in agg["per_rank"])
+    assert rf2["traffic"] is None and rf2["traffic_source"]
+    assert rf2["rank0"]["kernel_ms"] > 0
     a, b = np.load(f1), np.load(f2)
     assert a.shape == (512, 512) and np.count_nonzero(a) > 0
     assert np.array_equal(a, b), f"{int(np.sum(a != b))} pixels differ between N=1 and N=2"
@@ -80,7 +97,8 @@ def test_bench_gmm_single_and_two_slab_frames_agree(gpu, tmp_path):
 
 def test_bench_gmm_slab_rehearsal(gpu, tmp_path):
     """--slab-rehearsal on one GPU: every segment of the chain generated and timed
-    in turn, one and two segments per rank; the period is the slowest rank's"""
+    in turn, one and two segments per rank; the line is an estimate (value
+    null): the slowest rank's march plus its hand-off and reduce"""
     for seg in ("1", "2"):
         out = _run([sys.executable, "bench.py", "--config", "gmm96", "--slab-rehearsal",
                     "--rehearsal-ranks", "3", "--segments", seg, "--steps", "2", "--warmup", "1",
@@ -88,5 +106,9 @@ def test_bench_gmm_slab_rehearsal(gpu, tmp_path):
         cfg = out["config"]
         assert out["n_gpus"] == 1 and out["scaling"] is None and out["rehearsal_shared_gpus"]
         assert len(cfg["slabs_balanced"]) == 3 * int(seg)
-        assert abs(out["ms_per_step"] - max(cfg["rank_ms"])) < 1e-3
+        assert out["value"] is None and out["ms_per_step"] is None
+        assert abs(out["period_march_only_ms"] - max(cfg["rank_ms"])) < 1e-3
+        assert out["period_estimate_ms"] > out["period_march_only_ms"]
+        assert out["period_overlapped_ms"] <= out["period_estimate_ms"]
+        assert len(cfg["handoff"]) == 3 and out["estimated_Mrays_s"] > 0
         assert cfg["slabs_balanced"][0]["rays_in"] == 256 * 256

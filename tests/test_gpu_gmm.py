@@ -106,7 +106,6 @@ def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs):
     for i, (z_lo, z_hi) in enumerate(bounds):
         zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, dims[2])
         pkg.synthesize_gmm(dims, K, z_base=zb, nslices=ns)
-        cnt.zero_()
         rin = bufs[(i + 1) % 2] if i else None
         s = pkg.gmm_slab(z_lo, z_hi, bufs[i % 2], cnt[0:1], d_rays_in=rin, n_rays_in=n_in)
         pkg.render_gmm(d, s)
@@ -130,8 +129,10 @@ def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs):
 def test_gmm_slab_footprint_and_list_capacity(pkg, orc, gpu):
     """U of every slab of a chain (vr_gmm_count_footprint_slab, what bench.py
     --slab-rehearsal prices each slab's launch with) equals the oracle's count of
-    that slab; and a slab launch whose alive-list counter was not zeroed drops
-    the entries past the list's capacity (include/vr.h) instead of writing past it"""
+    that slab; and the library resets the alive-list counter itself, on its own
+    stream, before every slab launch (include/vr.h): a counter the caller left
+    at any value counts exactly the rays that leave alive, and no entry lands
+    past the list's capacity"""
     import torch
     dims = (24, 20, 23)
     K, W, H = 16, 72, 56
@@ -147,20 +148,23 @@ def test_gmm_slab_footprint_and_list_capacity(pkg, orc, gpu):
     for i, (z_lo, z_hi) in enumerate(bounds):
         zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, dims[2])
         pkg.synthesize_gmm(dims, K, z_base=zb, nslices=ns)
-        cnt.zero_()
+        cnt.fill_(W * H - 3)  # stale: the count pass resets it
         s = pkg.gmm_slab(z_lo, z_hi, bufs[i % 2], cnt, d_rays_in=bufs[(i + 1) % 2] if i else None,
                          n_rays_in=n_in)
         u = pkg.gmm_count_footprint(d, s)
         r = orc.render_gmm(wm[zb:zb + ns], sg[zb:zb + ns], dims, p, z_base=zb, slab=(z_lo, z_hi),
                            rays_in=ref_rays, want_mark=True)
         assert u == r["U"] and (u > 0 or i > 0), (i, u, r["U"])
-        cnt.zero_()
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == r["rays_out"].shape[0]
+        cnt.fill_(0x7FFFFFFF)  # stale: the render resets it
         pkg.render_gmm(d, s)
         torch.cuda.synchronize()
         n_in, ref_rays = int(cnt.item()), r["rays_out"]
         assert n_in == ref_rays.shape[0]
-    # capacity: slab 0 from the camera holds at most W*H entries; a counter left at
-    # W*H - 3 lets 3 entries in and drops the rest, the rows past the list untouched
+    # capacity: slab 0 from the camera holds at most W*H entries; a counter left
+    # at W*H - 3 (by the caller, on its own stream) is reset
+    # by the launch: exactly the alive rays are listed, the rows past the list untouched
     zb, ns = pkg.slabs.resident_slices(*bounds[0], dims[2])
     pkg.synthesize_gmm(dims, K, z_base=zb, nslices=ns)
     big = torch.full((W * H + 64, 12), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
@@ -169,9 +173,9 @@ def test_gmm_slab_footprint_and_list_capacity(pkg, orc, gpu):
     torch.cuda.synchronize()
     alive = orc.render_gmm(wm[zb:zb + ns], sg[zb:zb + ns], dims, p, z_base=zb,
                            slab=bounds[0])["rays_out"].shape[0]
-    assert alive > 3 and int(cnt.item()) == W * H - 3 + alive
+    assert alive > 3 and int(cnt.item()) == alive
     assert bool((big[W * H:] == 0x5A5A5A5A).all()), "entries written past the list's capacity"
-    assert not bool((big[W * H - 3:W * H] == 0x5A5A5A5A).all())
+    assert not bool((big[:alive] == 0x5A5A5A5A).all(dim=1).any()), "an alive ray's row unwritten"
     pkg.free_gmm()
 
 
@@ -309,7 +313,6 @@ def test_config5_at_size(pkg, orc, gpu):
                 break
             zb, ns = pkg.slabs.resident_slices(z_lo, z_hi, n)
             pkg.synthesize_gmm((n, n, n), K, 20261015, z_base=zb, nslices=ns)
-            cnt.zero_()
             pkg.render_gmm(d, pkg.gmm_slab(z_lo, z_hi, bufs[i % 2], cnt,
                                            d_rays_in=bufs[(i + 1) % 2] if i else None,
                                            n_rays_in=n_in))

@@ -81,7 +81,6 @@ def run_chain(a, pkg, torch, np, s, bounds, n, K, W, H, desc, rays, cnt, frame, 
         ms = []
         with torch.cuda.stream(s):
             for _ in range(a.reps):
-                cnt.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
                 pkg.render_gmm(desc, pkg.gmm_slab(z_lo, z_hi, rout, cnt,

@@ -1857,10 +1857,14 @@ int vr_debug_wave_clock(uint64_t *d_buf) {
     return VR_OK;
 }
 
-// tooling: 4 x u64 device counters of LDS-box bound violations (k_march /
-// k_march_duo staged reads); counted only by a -DVR_BOX_CHECK build, which
-// reports whether it was built so (return 1) -- the default build returns 0
+// tooling: 6 x u64 device counters of the LDS-box marches (k_march /
+// k_march_duo staged reads; layout in vr.h: [0] violations, [1] worst overrun,
+// [2] out-of-volume box voxels, [3] decoded voxels, [4] lane slots, [5] spare),
+// zeroed here on the library's stream and accumulated by every later launch;
+// counted only by a -DVR_BOX_CHECK build, which reports whether it was built
+// so (return 1) -- the default build returns 0
 int vr_debug_box_check(uint64_t *d_buf) {
+    if (d_buf) VR_HIP(hipMemsetAsync(d_buf, 0, 6 * sizeof(uint64_t), g.stream));
     g.box_check = reinterpret_cast<unsigned long long *>(d_buf);
 #ifdef VR_BOX_CHECK
     return 1;
@@ -2190,7 +2194,12 @@ int vr_render_gmm(const vr_render_desc *desc, const vr_gmm_slab *slab) {
     uint32_t nblocks = 0;
     int rc = fill_gmm_params(desc, slab, P, nblocks);
     if (rc != VR_OK) return rc;
-    hipError_t e = vr::launch_march_gmm(g.gmm.K, desc->query_method, P, nblocks, false, g.stream);
+    // the alive-list counter starts from 0 on the stream the launch runs on
+    // (a caller zeroing it on another stream raced the launch)
+    hipError_t e = slab ? hipMemsetAsync(slab->d_n_rays_out, 0, sizeof(uint32_t), g.stream)
+                        : hipSuccess;
+    if (e == hipSuccess)
+        e = vr::launch_march_gmm(g.gmm.K, desc->query_method, P, nblocks, false, g.stream);
     if (e != hipSuccess) return hip_fail(e, "launch(k_march_gmm)");
     return VR_OK;
 }
@@ -2211,6 +2220,8 @@ int64_t vr_gmm_count_footprint_slab(const vr_render_desc *desc, const vr_gmm_sla
     VR_HIP(hipMalloc(&bits, nwords * 8 + 8));
     unsigned long long *total = bits + nwords;
     hipError_t e = hipMemsetAsync(bits, 0, nwords * 8 + 8, g.stream);
+    if (e == hipSuccess && slab)
+        e = hipMemsetAsync(slab->d_n_rays_out, 0, sizeof(uint32_t), g.stream);
     P.mark = bits;
     P.out = nullptr;  // count launch writes no pixels
     P.out_f = nullptr;

@@ -204,6 +204,40 @@ def two_segment_bounds(nz: int, world: int, direction: int, bounds=None, costs=N
     return [(nz - b, nz - a) for a, b in march]
 
 
+def period_with_handoff(march_ms, rays_out, owners, world: int, frame_bytes: int,
+                        link_gbs: float, ray_bytes: int = RAY_WORDS * 4):
+    """Pipeline period of a slab chain from its segments' measured marches and
+    the bytes its ranks exchange, at an assumed point-to-point link rate.
+
+    march_ms[i], rays_out[i]: segment i's march time and the rays it hands on
+    (march order); owners[i]: its rank.  The hand-off i -> i+1 (rays_out[i] x
+    ray_bytes + the 8-byte count) crosses one xGMI link unless both segments sit
+    on one rank; every rank also sends its frame (frame_bytes) into the reduce
+    to rank 0.  Per rank:
+      serial  = sum over its segments of (receive + march + send) + reduce:
+                nothing overlaps (the chain's recv -> march -> send order);
+      overlap = max(sum of marches, sum of receives, sum of sends + reduce):
+                transfers on their own streams, full-duplex links.
+    Returns (max serial, max overlap, per-rank rows)."""
+    n = len(march_ms)
+    recv, send = [0.0] * n, [0.0] * n
+    for i in range(n - 1):
+        if owners[i] != owners[i + 1]:
+            ms = (rays_out[i] * ray_bytes + 8) / (link_gbs * 1e9) * 1e3
+            send[i] += ms
+            recv[i + 1] += ms
+    red = frame_bytes / (link_gbs * 1e9) * 1e3
+    rows = []
+    for r in range(world):
+        seg = [i for i in range(n) if owners[i] == r]
+        m, rv, sd = (sum(v[i] for i in seg) for v in (march_ms, recv, send))
+        rows.append({"rank": r, "march_ms": round(m, 4), "recv_ms": round(rv, 4),
+                     "send_ms": round(sd, 4), "reduce_ms": round(red, 4),
+                     "serial_ms": round(rv + m + sd + red, 4),
+                     "overlap_ms": round(max(m, rv, sd + red), 4)})
+    return (max(r["serial_ms"] for r in rows), max(r["overlap_ms"] for r in rows), rows)
+
+
 def max_slices_for(nx: int, ny: int, ncomp: int, hbm_bytes: float, reserve: float = 0.1) -> int:
     """Largest slab (slices, excluding its halo slice) whose GMM records fit in
     hbm_bytes with a `reserve` fraction left for frame and alive-list buffers."""

@@ -113,7 +113,6 @@ class GmmStream:
             api.init_gmm(self.dwm[b][:ns], self.dsg[b][:ns], self.dims, z_base=zb, adopt=True)
             rin, rout = self.rays[(i + 1) % 2], self.rays[i % 2]
             with torch.cuda.stream(stream):
-                self.cnt.zero_()
                 api.render_gmm(desc, api.gmm_slab(lo, hi, rout, self.cnt,
                                                   d_rays_in=rin if i else None,
                                                   n_rays_in=n_in if i else 0))
