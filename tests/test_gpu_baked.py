@@ -243,12 +243,10 @@ def test_release_reupload_and_errors(pkg, orc, gpu, baked):
 
 
 @pytest.mark.parametrize("nb", [1, 4, 8, 32])
-@pytest.mark.parametrize("pipe", ["1", "0"])
-def test_baked_method7(pkg, orc, gpu, baked, nb, pipe, tune):
+def test_baked_method7(pkg, orc, gpu, baked, nb):
     """method 7 from the baked corner means (plane 3): the corner cache and double lerps of
-    K:395-480 over 4-byte corners, both m7 kernels, grid = volume and grid != volume"""
+    K:395-480 over 4-byte corners (k_march_m7<1, baked>), grid = volume and grid != volume"""
     import torch
-    tune.set("VR_M7_PIPE", pipe)
     vol = orc.synth_volume(18, 16, 14, nb)
     pkg.init_distribution(vol)
     pkg.bake_stats()

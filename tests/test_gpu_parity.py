@@ -425,11 +425,10 @@ def test_errors_do_not_exit(pkg, gpu):
     ("7", {"VR_SEG": "-2", "VR_WG_PER_CU": "3"}), ("1", {"VR_BOX_MAX": "64", "VR_WG_PER_CU": "3"}),
     ("2", {"VR_WG_PER_CU": "2"}), ("0", {"VR_WG_PER_CU": "3"}),
     ("0", {"VR_QUAD2": "1"}), ("0", {"VR_QUAD2": "1", "VR_WG_PER_CU": "1"}),
-    # K samples per footprint box (k_march_duo, m1/m2/m3), with direct-path fallbacks
+    # K samples per footprint box (k_march_duo m1/m2; m3 takes k_march), with
+    # direct-path fallbacks
     ("1", {"VR_DUO": "2"}), ("1", {"VR_DUO": "2", "VR_BOX_MAX": "64"}),
     ("1", {"VR_DUO": "3"}), ("1", {"VR_DUO": "4", "VR_BOX_MAX": "64"}),
-    # slice-compacted duo boxes (VR_DUO_COMPACT, off by default)
-    ("1", {"VR_DUO": "2", "VR_DUO_COMPACT": "1"}), ("1", {"VR_DUO": "4", "VR_DUO_COMPACT": "1"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
@@ -449,18 +448,15 @@ def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):
             assert_parity(got, ref, f"path {path} {env} nb={nb} m{method}")
 
 
-@pytest.mark.parametrize("compact", ["0", "1"])
 @pytest.mark.parametrize("k", ["2", "3", "4"])
 @pytest.mark.parametrize("nb", [1, 2, 8])
-def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune, compact):
-    """k_march_duo (K samples per footprint box; mean, variance and entropy -- the
-    entropy instance restored in round 5 with k_march's LDS log table and record
-    columns): rays ending on any sample of a box (opacity, tfar),
-    full frames and tile lists, bit-identical to the oracle"""
+def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune):
+    """k_march_duo (K samples per footprint box; mean and variance -- entropy keeps
+    one sample per box, k_march<B, 3>): rays ending on any sample of a box
+    (opacity, tfar), full frames and tile lists, bit-identical to the oracle"""
     import torch
     tune.set("VR_PATH", "1")
     tune.set("VR_DUO", k)
-    tune.set("VR_DUO_COMPACT", compact)
     vol = orc.synth_volume(30, 26, 22, nb)
     pkg.init_distribution(vol)
     cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),
@@ -470,7 +466,8 @@ def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune, compact):
             for method in (1, 2, 3):
                 got = gpu_render(pkg, None, 72, 40, cam, method, torch, density=density,
                                  brightness=bright)
-                want = "k_march_duo<" if k == "2" else f"k_march_duo{k}<"
+                want = ("k_march<" if method == 3 else "k_march_duo<" if k == "2"
+                        else f"k_march_duo{k}<")
                 assert pkg.last_kernel().startswith(want), pkg.last_kernel()
                 ref = orc.render(vol, orc.make_params(72, 40, cam, query_method=method,
                                                       density=density, brightness=bright))[:3]
@@ -491,100 +488,6 @@ def test_duo_march_early_exit(pkg, orc, gpu, nb, k, tune, compact):
     ref8 = orc.render(vol, orc.make_params(72, 40, cams[0], query_method=1), want_float=False,
                       want_steps=False)[0]
     assert np.array_equal(got, ref8)
-
-
-@pytest.mark.parametrize("order", [None, "0", "1,3", "2,2"])
-@pytest.mark.parametrize("rows,k", [("2", "2"), ("2", "4"), ("4", "2"), ("4", "4"),
-                                    ("2p", "2"), ("2p", "4")])
-@pytest.mark.parametrize("nb", [4, 8])
-def test_wgbox_march(pkg, orc, gpu, nb, rows, k, order, tune):
-    """k_march_wgbox (R tile rows per workgroup marching in lockstep, one union
-    footprint box per step) and k_march_wgpipe (the next box loaded during this
-    step's samples): every frame bit-identical to the oracle -- ragged
-    frames whose last group hangs off the image, rays ending on any sample of a
-    box, union boxes over the capacity (direct samples), grouped / raster frame
-    orders (VR_XBLOCK), a clipped render_kernel launch -- and tile lists keep the
-    per-wave duo"""
-    import torch
-    tune.set("VR_PATH", "1")
-    tune.set("VR_DUO", k)
-    pipe = rows.endswith("p")  # k_march_wgpipe: the next box in flight
-    rows = rows.rstrip("p")
-    tune.set("VR_WG_ROWS", rows)
-    tune.set("VR_WG_PIPE", "1" if pipe else "0")
-    if order is not None:
-        tune.set("VR_XBLOCK", order)
-    vol = orc.synth_volume(30, 26, 22, nb)
-    pkg.init_distribution(vol)
-    name = f"k_march_wg{'pipe' if pipe else 'box'}{rows}_k{k}<"
-    if nb == 8 and k == "4" and rows == "4":
-        name = "k_march_duo4<"
-    cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0)),
-            pkg.camera.display_inv_view((0.0, 90.0))]
-    for W, H in ((72, 40), (80, 44), (136, 96)):
-        for cam in cams:
-            for density, bright in ((0.05, 1.0), (3.0, 0.7)):
-                for method in (1, 2):
-                    got = gpu_render(pkg, None, W, H, cam, method, torch, density=density,
-                                     brightness=bright)
-                    assert pkg.last_kernel().startswith(name), pkg.last_kernel()
-                    ref = orc.render(vol, orc.make_params(W, H, cam, query_method=method,
-                                                          density=density, brightness=bright))[:3]
-                    assert_parity(got, ref, f"wgbox R={rows} K={k} nb={nb} {W}x{H} m{method} "
-                                            f"d={density} order={order}")
-    # union boxes over a small capacity: those steps sample directly
-    tune.set("VR_BOX_WG", "64")
-    m = cams[1]
-    got = gpu_render(pkg, None, 80, 44, m, 1, torch)
-    assert pkg.last_kernel().startswith(name), pkg.last_kernel()
-    assert_parity(got, orc.render(vol, orc.make_params(80, 44, m, query_method=1))[:3],
-                  f"wgbox R={rows} K={k} nb={nb} box_wg=64")
-    tune.clear("VR_BOX_WG")
-    # a render_kernel launch covering the top-left 50 x 30 pixels only
-    W, H, m = 80, 44, cams[0]
-    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-    pkg.copyInvViewMatrix(m, 48)
-    pkg.render_kernel((5, 3, 1), (10, 10, 1), out, W, H, 0.05, 1.0, 0.0, 1.0, 1, (30, 26, 22))
-    torch.cuda.synchronize()
-    full = orc.render(vol, orc.make_params(W, H, m, query_method=1), want_float=False,
-                      want_steps=False)[0]
-    got = out.cpu().numpy().view(np.uint32).reshape(H, W)
-    assert np.array_equal(got[:30, :50], full[:30, :50])
-    assert not got[30:, :].any() and not got[:, 50:].any()
-    # tile lists: the per-wave duo
-    lists = pkg.tiles.tile_lists(W, H, 2, m)
-    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
-    packed = torch.zeros((2, lists.shape[1] * 256), dtype=torch.int32, device="cuda")
-    pkg.render(pkg.make_desc(packed[0], W, H, m, query_method=1, d_tile_list=dl[0],
-                             n_tiles=lists.shape[1]))
-    assert pkg.last_kernel().startswith("k_march_duo"), pkg.last_kernel()
-
-
-@pytest.mark.parametrize("box_wg", [None, "64"])
-@pytest.mark.parametrize("rows", ["2", "4"])
-def test_wgbox_entropy(pkg, orc, gpu, rows, box_wg, tune):
-    """k_march_wgbox for 8-bin entropy (one sample per union box, k_march's LDS log
-    table and record columns): row-aligned and oblique full frames, ragged sizes,
-    dense and thin media, union boxes over the capacity (direct samples, 2 corners
-    in flight), bit-identical to the oracle"""
-    import torch
-    tune.set("VR_PATH", "1")
-    tune.set("VR_WG_ROWS", rows)
-    if box_wg:
-        tune.set("VR_BOX_WG", box_wg)
-    vol = orc.synth_volume(30, 26, 22, 8)
-    pkg.init_distribution(vol)
-    cams = [pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))]
-    for W, H in ((72, 40), (136, 96)):
-        for cam in cams:
-            for density in (0.05, 3.0):
-                got = gpu_render(pkg, None, W, H, cam, 3, torch, density=density)
-                assert pkg.last_kernel().startswith(f"k_march_wgbox{rows}_k1<B=8,M=3>"), \
-                    pkg.last_kernel()
-                ref = orc.render(vol, orc.make_params(W, H, cam, query_method=3,
-                                                      density=density))[:3]
-                assert_parity(got, ref, f"wgbox entropy R={rows} {W}x{H} d={density} "
-                                        f"box_wg={box_wg}")
 
 
 @pytest.mark.parametrize("seg", ["2", "4", "-2", "-4"])

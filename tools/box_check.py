@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="512x8:C0,512x8:C1,256x4:C0,1024x8:C0")
     ap.add_argument("--methods", default="1,2,3")
-    ap.add_argument("--duos", default="0,2,3,4,VR_DUO=2+VR_DUO_COMPACT=1,VR_DUO=3+VR_DUO_COMPACT=1",
+    ap.add_argument("--duos", default="0,2,3,4",
                     help="VR_DUO values; a value NAME=V,... sets those knobs instead")
     ap.add_argument("--any-build", action="store_true",
                     help="also run on a default build (frames compared, nothing counted)")

@@ -50,13 +50,6 @@ struct State {
     size_t perm_cap = 0;
     uint32_t perm_key[22] = {0};
     std::vector<uint32_t> perm_host;
-    // the same order per group of R tile rows (k_march_wgbox): the groups' top
-    // tiles, entries [perm_goff[i], + perm_gn[i]) for R = 2 (i = 0) and 4 (i = 1);
-    // perm_gn[i] = 0 when the order's blocks do not hold whole groups
-    uint32_t *perm_grp = nullptr;
-    size_t perm_grp_cap = 0;
-    size_t perm_goff[2] = {0, 0}, perm_gn[2] = {0, 0};
-    std::vector<uint32_t> perm_grp_host;
     // adaptive order (frame_order): 0 none, 1 estimate order in use and per-tile
     // costs to be recorded, 2 final; cost_recorded: a render recorded into tile_cost
     int order_state = 0;
@@ -340,10 +333,8 @@ float est_steps(const float *M, uint32_t W, uint32_t H, float x, float y) {
 // (lists_from_costs).  VR_NO_ADAPT keeps the estimate order.
 
 // Interleave the 8 per-XCD lists into the workgroup order (entry b runs on
-// XCD b % 8) and upload it as g.perm; the same order by groups of 2 and 4 tile
-// rows (each list keeps the top tiles of its groups) as g.perm_grp, when the
-// blocks (by tile rows each, row-aligned) hold whole groups.
-int upload_perm(const std::vector<std::vector<uint32_t>> &lists, uint32_t tx, uint32_t by) {
+// XCD b % 8) and upload it as g.perm.
+int upload_perm(const std::vector<std::vector<uint32_t>> &lists) {
     std::vector<uint32_t> &h = g.perm_host;
     h.clear();
     size_t longest = 0;
@@ -360,28 +351,6 @@ int upload_perm(const std::vector<std::vector<uint32_t>> &lists, uint32_t tx, ui
     }
     VR_HIP(hipMemcpyAsync(g.perm, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                           g.stream));
-    std::vector<uint32_t> &q = g.perm_grp_host;
-    q.clear();
-    for (int i = 0; i < 2; i++) {
-        const uint32_t R = 2u << i;
-        g.perm_goff[i] = q.size();
-        g.perm_gn[i] = 0;
-        if (by % R) continue;
-        for (size_t k = 0; k < longest; k++)
-            for (auto &l : lists)
-                if (k < l.size() && (l[k] / tx) % R == 0) q.push_back(l[k]);
-        g.perm_gn[i] = q.size() - g.perm_goff[i];
-    }
-    if (q.size() > g.perm_grp_cap) {
-        if (g.perm_grp) (void)hipFree(g.perm_grp);
-        g.perm_grp = nullptr;
-        g.perm_grp_cap = 0;
-        VR_HIP(hipMalloc(&g.perm_grp, q.size() * sizeof(uint32_t)));
-        g.perm_grp_cap = q.size();
-    }
-    if (!q.empty())
-        VR_HIP(hipMemcpyAsync(g.perm_grp, q.data(), q.size() * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, g.stream));
     return VR_OK;
 }
 
@@ -466,7 +435,7 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
             if (any) {  // kernels other than the per-ray pipelined march record nothing
                 std::vector<std::vector<uint32_t>> lists;
                 lists_from_costs(cost, tx, ty, bx, by, lists);
-                int rc = upload_perm(lists, tx, by);
+                int rc = upload_perm(lists);
                 if (rc != VR_OK) return rc;
                 perm = g.perm;
             }
@@ -500,7 +469,7 @@ int frame_order(const vr_render_desc *d, uint32_t tx, uint32_t ty, const uint32_
                     lists[x8].push_back(y * tx + x);
     }
     g.order_state = 0;  // until the new order is in place
-    int rc = upload_perm(lists, tx, by);
+    int rc = upload_perm(lists);
     if (rc != VR_OK) return rc;
     std::memcpy(g.perm_key, key, sizeof key);
     perm = g.perm;
@@ -794,12 +763,6 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         }
     }
     if (P.path != 2 && P.path != 7) P.axis_view = 0;  // 7: the segmented march reads the copy too
-    // k_march_duo boxes of only the slices the footprints read (VR_DUO_COMPACT=1):
-    // 512^3 x 8 C0 decodes 2.12 -> 2.00 U but runs 0.624 -> 0.681 ms (the slot
-    // table and the per-lane slot counts cost more than the skipped slices;
-    // round 5, profiles/r05/sweep), so the default keeps the whole z range
-    P.duo_compact = 0;
-    if (const char *e = vr::tuning("VR_DUO_COMPACT")) P.duo_compact = std::atoi(e) != 0;
     if (const char *e = vr::tuning("VR_DUO")) {  // 0 / 1: one sample per box, 2-4: that many
         const int v = std::atoi(e);
         if (v >= 0 && v <= 4) P.duo = v;
@@ -809,38 +772,6 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         if (v == 0 || v == 1 || v == 2 || v == 4 || v == 7) {
             P.path = v;
             P.axis_view = 0;  // a forced path reads the x rows
-        }
-    }
-    // Workgroup boxes (k_march_wgbox): R vertically adjacent tiles march in
-    // lockstep and fetch the union of their footprints once per step, so the
-    // rows a per-wave box shares with the tile below are not fetched twice.
-    // Full frames of the duo march (4 / 8 bins, mean / variance) on the
-    // records; VR_WG_ROWS = 0 / 2 / 4 overrides, VR_BOX_WG the capacity.
-    P.wg_rows = 0;
-    P.box_wg = 3072;
-    P.wg_pipe = 0;
-    if (const char *e = vr::tuning("VR_WG_PIPE")) P.wg_pipe = std::atoi(e) != 0;
-    const bool wg_m3 = g.nb == 8 && d->query_method == 3 && P.duo <= 1;  // k_march<8,3>'s frames
-    if (for_render && P.path == 1 && (P.duo >= 2 || wg_m3) && !d->d_tile_list && !codec && !flex &&
-        (g.nb == 4 || g.nb == 8) && (d->query_method == 1 || d->query_method == 2 || wg_m3) &&
-        !g.stats) {
-        if (const char *e = vr::tuning("VR_WG_ROWS")) {
-            const int v = std::atoi(e);
-            if (v == 0 || v == 2 || v == 4) P.wg_rows = v;
-        }
-        if (const char *e = vr::tuning("VR_BOX_WG")) {
-            const int v = std::atoi(e);
-            if (v >= 0 && v <= 8192) P.box_wg = v;
-        }
-        if (P.wg_pipe) P.box_wg = std::min(P.box_wg, 8000);  // two boxes in 64 KiB of LDS
-        // the instances march_b launches: K = 2 / 4, less 8-bin K = 4 at 4 rows;
-        // 8-bin entropy K = 1 (not pipelined)
-        if (wg_m3) {
-            if (P.box_wg == 0) P.wg_rows = 0;
-            P.wg_pipe = 0;
-        } else if ((P.duo != 2 && P.duo != 4) || P.box_wg == 0 ||
-                   (g.nb == 8 && P.duo == 4 && P.wg_rows == 4)) {
-            P.wg_rows = 0;
         }
     }
     // The quad march (path 0: oblique views, B = 8, methods 1-3) of a rank's tile
@@ -889,16 +820,6 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         nslots = (uint32_t)all;
     }
     P.n_tiles = nslots;
-    if (P.wg_rows) {  // one workgroup per group of wg_rows tile rows
-        const int i = P.wg_rows == 4 ? 1 : 0;
-        if (P.perm && g.perm_gn[i]) {
-            P.perm = g.perm_grp + g.perm_goff[i];
-            nslots = (uint32_t)g.perm_gn[i];
-        } else {  // raster groups (xcd_slot)
-            P.perm = nullptr;
-            nslots = tiles_x(d->width) * ((tiles_y(d->height) + P.wg_rows - 1) / P.wg_rows);
-        }
-    }
     return VR_OK;
 }
 

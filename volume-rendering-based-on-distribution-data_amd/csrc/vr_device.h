@@ -104,10 +104,6 @@ struct Params {
     // tooling (vr_debug_box_check): 6 x u64, [0] violations, [1] worst overrun,
     // [2] out-of-volume box voxels, [3] decoded voxels, [4] lane slots, [5] spare
     unsigned long long *box_check;
-    int duo_compact;             // k_march_duo: box of the used slices only (1) or the whole z range (0)
-    int wg_rows;                 // k_march_wgbox: tile rows per workgroup (2 / 4), 0 = per-wave boxes
-    int box_wg;                  // k_march_wgbox: workgroup box capacity (voxels)
-    int wg_pipe;                 // workgroup boxes with the next box in flight (k_march_wgpipe, 2 rows)
 };
 
 // Record index of voxel (x, y, z) in the 2x2 (x, y) micro-brick layout (one

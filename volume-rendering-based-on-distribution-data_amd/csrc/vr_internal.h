@@ -22,11 +22,22 @@ struct SynthArgs {
     uint64_t seed;
 };
 
+// the synthetic volumes' hash: k_synth, k_synth_codec
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 // records an error for vr_last_error() (vr_api.cpp); returns status
 int record_error(int status, const char *msg);
 
 hipError_t launch_march(int nb, int method, const float *vol, const Params &P,
                         uint32_t nslots, bool count, hipStream_t s);
+// method 7 (vr_m7.hip; -7: over the baked corner means); launch_march routes to it
+hipError_t launch_march_m7(int nb, int method, const float *vol, const Params &P,
+                           uint32_t nslots, hipStream_t s);
 // name of the march kernel the last non-counting launch_march() chose
 const char *last_march_kernel();
 void note_kernel(const char *kind, int B, int method);
