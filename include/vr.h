@@ -124,7 +124,7 @@ void dataProcessing(void);
  * (vr_release_stats, then vr_bake_stats).  vr_stats_info: device pointers
  * (nullptr = not baked) and plane lengths in floats.
  * Layout copy: the first oblique-view frame of a library-owned 8-bin volume
- * makes a second, 2x2 (x, y) micro-brick copy of its records (DESIGN.md 4.6;
+ * makes a second, 2x2 (x, y) micro-brick copy of its records (DESIGN.md 2;
  * as many bytes as the volume, made synchronously, only while HBM keeps
  * max(4 GiB, 5 %) free after it).  Views whose screen x runs along the volume's
  * z or y axis (|M[8]| or |M[4]| >= 0.95) of an owned volume with 1, 2, 4 or 8

@@ -1,6 +1,6 @@
 """Code-object checks of the built libvr.so (CPU: reads the gfx950 kernel
 metadata, runs nothing).  The LDS-box marches must use no scratch: the
-round-4 k_march_duo<8,3> fault (DESIGN.md 4.2.1) came from a register-capped
+round-4 k_march_duo<8,3> fault (DESIGN.md 4.2) came from a register-capped
 variant build whose duo spilled ~1 KB per lane to a private segment; the shipped
 k_march / k_march_duo instances keep private_segment_fixed_size 0, no dynamic
 stack and at most 256 VGPRs."""

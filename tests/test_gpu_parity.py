@@ -1039,7 +1039,7 @@ def test_environment_does_not_change_the_kernel(pkg, orc, gpu, monkeypatch):
 def test_axis_views_segmented(pkg, orc, gpu, nb):
     """small frames and rank tile lists of views along the volume's z or y take the
     pipelined ray-segmented march over the axis-rows copy (k_march_segp4_zrows /
-    segp2 / _yrows, DESIGN.md 4.7 and 7) by the default dispatch: bit-identical
+    segp2 / _yrows, DESIGN.md 2 and 7) by the default dispatch: bit-identical
     to the oracle, method 3 keeping the one-lane march"""
     import torch
     vol = orc.synth_volume(48, 40, 44, nb)

@@ -5,7 +5,7 @@ The oracle pins one canonical reading of what the reference does not fix
 rsqrtf as the correctly rounded 1/sqrtf (helper_math normalize, K:295), the
 float log as (float)log((double)x) (K:766).  tools/parity_margin.py renders the
 BASELINE configs with each alternative reading and counts how far the frame
-moves (profiles/r04/parity_margin.json, DESIGN.md section 3.1).  These tests pin
+moves (profiles/r04/parity_margin.json, DESIGN.md section 3).  These tests pin
 those figures at the two configs the CPU renders in a second, so a change to the
 oracle's arithmetic cannot silently change the stated risk.
 """

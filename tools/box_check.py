@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""LDS-box bound check of the staged marches (tooling, DESIGN.md 4.2.1).
+"""LDS-box bound check of the staged marches (tooling, DESIGN.md 4.2).
 
 Run against a -DVR_BOX_CHECK build of libvr.so (tools/build_variants.sh
 boxcheck:-DVR_BOX_CHECK; VRDD_LIB points the package at it): every frame of

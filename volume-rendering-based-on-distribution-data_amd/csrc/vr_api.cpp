@@ -631,7 +631,7 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     device_lds(P.lds_cu, P.lds_wg);
     // Views whose screen x runs along the volume's z or y (|M[8]| / |M[4]| >=
     // 0.95) march an axis-rows copy of an owned B <= 8 volume with the per-ray
-    // pipelined march (ensure_axis_copy, DESIGN.md 4.7); for the choices below
+    // pipelined march (ensure_axis_copy, DESIGN.md 2); for the choices below
     // they count as row-aligned (their x-row seg / quad alternatives read the
     // x rows across).  VR_ZROWS=0 keeps them oblique.
     const char *ez = vr::tuning("VR_ZROWS");
@@ -946,7 +946,7 @@ void blob_axis(int n, double c, double s, float *out) {
 // Oblique views of an 8-bin volume (the quad march, path 0) read a 2x2 (x, y)
 // micro-brick copy of the records: a footprint's four (x, y) corners share
 // one 128-B line when x0 and y0 are even, so a wave step touches fewer lines
-// than in x rows (DESIGN.md 4.6).  Made on the first such frame of an owned
+// than in x rows (DESIGN.md 2).  Made on the first such frame of an owned
 // volume (a caller-owned buffer adopted by vr_init_distribution may change
 // behind the library's back), only if HBM keeps max(4 GiB, 5 %) free after it; without
 // it the quad march reads the x rows.  VR_BRICK=0 (vr_set_tuning) disables it.
@@ -994,7 +994,7 @@ bool ensure_brick() {
 // that axis contiguous (axis_copy_strides) gives them what x rows give the
 // runSingleTest view -- consecutive lanes on consecutive records -- and the
 // per-ray pipelined march reads it (1024^3 x 8, yaw 90: 3.01 -> 1.63 ms,
-// DESIGN.md 4.7).  Both axis copies stay resident when the layout budget holds
+// DESIGN.md 2).  Both axis copies stay resident when the layout budget holds
 // them (vr_set_layout_budget); otherwise a view along the other axis replaces
 // the copy.  Made on the first such frame of an owned volume with B <= 8 (as
 // ensure_brick: synchronous, timed into vr_layout_info) by k_axis_copy, an
@@ -1049,7 +1049,7 @@ bool ensure_axis_copy(int axis) {
 // first such frame within the layout budget, dropped with the planes.
 // Axis 3 (round 5): oblique views get the plane in 8 x 2 x 2 bricks
 // (k_plane8, gather8 MODE 6), whose lines also hold a footprint's z pair
-// (per 64x4-tile line floor at 1024^3 C1: 3.77 -> 3.47 GB, DESIGN.md 4.8);
+// (per 64x4-tile line floor at 1024^3 C1: 3.77 -> 3.47 GB, DESIGN.md 4.3);
 // VR_PLANE8=0 keeps such views on the 16 x 2 x 1 plane.
 bool ensure_plane_copy(int plane, int axis) {
     if (const char *e = vr::tuning(axis == 3 ? "VR_PLANE8" : "VR_ZROWS"))

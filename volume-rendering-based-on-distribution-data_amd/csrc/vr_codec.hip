@@ -55,7 +55,7 @@ __device__ __forceinline__ void codec_decode_scr(const Params &P, const float *s
                 ev = e[j];
             }
             const int idx = (int)ev.x;
-            if (idx >= 0 && idx < B) {      // bin ids outside [0, B) skipped (DESIGN.md 4.4)
+            if (idx >= 0 && idx < B) {      // bin ids outside [0, B) skipped (DESIGN.md 4.6)
                 float v = scr[idx * 256] + ev.y;
                 if (v < 0) v = 0;
                 scr[idx * 256] = v;

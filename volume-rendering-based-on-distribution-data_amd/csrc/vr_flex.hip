@@ -18,7 +18,7 @@
 // every sub-span is a binary search.  One workgroup per corner decodes its
 // sub-spans in parallel into LDS and one lane per bin sums them in sub-span
 // order (the reference's shared-memory float atomics have no fixed order;
-// DESIGN.md 4.5 lists this and the other choices for undefined behaviour).
+// DESIGN.md 4.7 lists this and the other choices for undefined behaviour).
 #include "vr_internal.h"
 #include "vr_march.h"
 

@@ -520,7 +520,7 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 // ---- wave-staged march (B <= 8) ----
 // Exact-footprint staging per wave (8x8 rays), wave-synchronous: no workgroup
 // barriers (a workgroup-wide version with 5 barriers per step was latency-bound,
-// DESIGN.md 4.3), so the 16-20 resident waves of a CU
+// DESIGN.md 4.4), so the 16-20 resident waves of a CU
 // hide each other's HBM latency.  Per step: (y,z) row table by LDS atomics,
 // compaction by DPP scans, row-start marks + a max-scan give every lane its
 // (row, x) for consecutive records, so consecutive lanes load consecutive
@@ -1075,7 +1075,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MIN
 // BR: the volume is the 2x2 (x, y) micro-brick copy (P.bvol): lane g reads
 // half g & 1 of record x0 (g < 2) or x1 (g >= 2) of each (y, z) combo, so a
 // footprint's four (x, y) corners at one z share a line when x0 and y0 are
-// even (oblique views: fewer distinct lines per wave step, DESIGN.md 4.6).
+// even (oblique views: fewer distinct lines per wave step, DESIGN.md 2).
 template <int G, bool BR = false>
 __device__ __forceinline__ bool qc_gather(const float *__restrict__ vol, const Params &P,
                                           const FootPacked &fp, uint32_t g, float4 (&L)[4]) {
@@ -1441,11 +1441,11 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // The quad march uses no LDS; an LDS request caps it at 2 workgroups
             // (2 waves per SIMD) per CU, which trims the oblique view's line
             // re-reads: 1024^3x8 C1 3.73 -> 3.52 ms (3 per CU by registers, 1 per
-            // CU 3.91; DESIGN.md 4.3).  VR_WG_PER_CU overrides.
+            // CU 3.91; DESIGN.md 4.4).  VR_WG_PER_CU overrides.
             // A rank's tile list of <= 400 K rays (8 GPUs at 1080p) runs at 1 per
             // CU: its tiles are scattered over the frame, and fewer rays in flight
             // re-read fewer lines (cost-dealt C1 lists, max over 8 ranks: 0.71 ->
-            // 0.59 ms; 3 per CU 0.68; tools/rank_sim.py, DESIGN.md 4.6)
+            // 0.59 ms; 3 per CU 0.68; tools/rank_sim.py, DESIGN.md 2)
             const int qcap = P.wg_per_cu > 0 ? P.wg_per_cu
                              : (P.tile_list && (uint64_t)nslots * 256u <= 400000u) ? 1 : 2;
             // entropy: the log table (qc_group) at the front

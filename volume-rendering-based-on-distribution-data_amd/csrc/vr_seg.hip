@@ -195,7 +195,7 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
 }
 
 // GM: gather8's addressing (kGatherMode<M>; 3 = an axis-rows copy of the records,
-// the views whose screen x runs along the volume's z or y, DESIGN.md 4.7)
+// the views whose screen x runs along the volume's z or y, DESIGN.md 2)
 template <int B, int M, int S, bool PIPE, int GM = kGatherMode<M>>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_SEG_WAVES, 8))) void k_march_seg(const float *__restrict__ vol, Params P) {
     const uint32_t b = blockIdx.x;

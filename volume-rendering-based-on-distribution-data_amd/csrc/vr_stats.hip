@@ -127,7 +127,7 @@ hipError_t launch_bake_codec(const Params &P, float *out, uint64_t plane, uint64
 // an even (x, y): record (x, y, z) sits at z*bsz + (y>>1)*bsy + (x>>1)*4 +
 // (y&1)*2 + (x&1) (brick_index).  Like a cudaArray, the copy is the
 // library's own layout of the uploaded records (K:1913-1918); the quad march
-// of oblique views reads it (DESIGN.md section 4.6).  One thread per record, a
+// of oblique views reads it (DESIGN.md section 2).  One thread per record, a
 // workgroup per 128 x 2 records (y pair 2 by): lanes 4q .. 4q+3 write the
 // whole line of x pair q, and each row's 128 records are read as 4 KB runs.
 // (One row per workgroup wrote every line in two halves from two workgroups:
