@@ -141,7 +141,9 @@ int vr_stats_info(const float **d_raw, uint64_t *raw_plane, const float **d_code
  * within a byte budget: vr_set_layout_budget(bytes) caps their total HBM
  * (default UINT64_MAX = two record-volume copies plus three baked-plane
  * copies, 1/8 padding each, plus 64 MiB for small volumes' padding: one view
- * class and one change of view; 0 = never make
+ * class and one change of view; a baked plane's copy is kept per (view axis,
+ * method) while the budget holds it, so alternating methods builds each once;
+ * 0 = never make
  * one, every view marches the records' x rows) and drops resident copies that
  * exceed a lowered budget.  vr_layout_info: bytes resident in copies, copies
  * made since load, and the time and size of the last one made (each is built
@@ -430,8 +432,9 @@ int vr_gmm_select(int slot);
  * 11.2).  The launch takes the samples whose trilinear footprint starts in
  * slices [z_lo, z_hi) (it reads slices z_lo .. min(z_hi, Z-1), which must be
  * resident).  Rays come from the camera (d_rays_in == NULL: whole frame) or
- * from the alive list of the previous slab (n_rays_in entries of 48 bytes:
- * float sum[4], t, pos[3]; uint32 pixel, samples taken, 0, 0).  Rays that end in
+ * from the alive list of the previous slab (n_rays_in entries of 36 bytes:
+ * float sum[4], t, pos[3]; uint32 pixel | samples taken << 23; slab launches
+ * need width*height <= 2^23).  Rays that end in
  * the slab are written to the frame (d_output etc., pixel y*width + x); rays that
  * leave it alive are appended to d_rays_out (capacity: n_rays_in, or
  * width*height) and counted in *d_n_rays_out (device memory; the call sets it

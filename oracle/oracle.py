@@ -442,7 +442,7 @@ class Gmm(ctypes.Structure):
                 ("K", ctypes.c_int), ("z_base", ctypes.c_int), ("nzs", ctypes.c_int)]
 
 
-GMM_RAY_WORDS = 12  # 48-byte alive-list entry as uint32 words
+GMM_RAY_WORDS = 9  # 36-byte alive-list entry as uint32 words (vr_gmm.hip GmmRay)
 
 
 def synth_gmm(nx, ny, nz, K=16, seed=20261015, z_base=0, nslices=None, nthreads=0):
@@ -464,9 +464,9 @@ def gmm_stat(wm_rec, sg_rec, method):
 
 def render_gmm(wm, sg, dims, params, z_base=0, slab=None, rays_in=None, want_mark=False):
     """GMM render (whole volume when slab is None, else slab = (z_lo, z_hi)).
-    rays_in: (n, 12) uint32 alive-list entries or None (camera rays).
+    rays_in: (n, 9) uint32 alive-list entries or None (camera rays).
     Returns dict: out (H, W) uint32, out_f (H, W, 4), out_n (H, W) int32 (-2 where
-    not written), rays_out (m, 12) uint32 or None, samples, U (with want_mark)."""
+    not written), rays_out (m, 9) uint32 or None, samples, U (with want_mark)."""
     wm = np.ascontiguousarray(wm, dtype=np.float32)
     sg = np.ascontiguousarray(sg, dtype=np.float32)
     nx, ny, nz = (int(v) for v in dims)

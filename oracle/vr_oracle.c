@@ -1155,8 +1155,26 @@ static int gmm_march(const orc_gmm *v, const orc_gmm_proc *proc, const orc_rende
     }
 }
 
+/* alive-list entries: 9 words, pix | n << 23 in the last (vr_gmm.hip GmmRay) */
+static orc_gmm_ray gmm_unpack(const uint32_t *w) {
+    orc_gmm_ray s;
+    memcpy(s.sum, w, 4 * sizeof(float));
+    memcpy(&s.t, w + 4, sizeof(float));
+    memcpy(s.pos, w + 5, 3 * sizeof(float));
+    s.pix = w[8] & ((1u << 23) - 1u);
+    s.n = w[8] >> 23;
+    return s;
+}
+
+static void gmm_pack(const orc_gmm_ray *s, uint32_t *w) {
+    memcpy(w, s->sum, 4 * sizeof(float));
+    memcpy(w + 4, &s->t, sizeof(float));
+    memcpy(w + 5, s->pos, 3 * sizeof(float));
+    w[8] = s->pix | (s->n << 23);
+}
+
 int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, int z_hi,
-                       const orc_gmm_ray *rays_in, uint32_t n_in, orc_gmm_ray *rays_out,
+                       const uint32_t *rays_in, uint32_t n_in, uint32_t *rays_out,
                        uint32_t *n_out, uint32_t *out, float *out_f, int32_t *out_n,
                        uint64_t *mark) {
     const int slab = rays_out != NULL;
@@ -1170,7 +1188,7 @@ int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, i
         float tnear, tfar;
         int x, y;
         if (rays_in) {
-            s = rays_in[i];
+            s = gmm_unpack(rays_in + i * ORC_GMM_RAY_WORDS);
             x = (int)(s.pix % (uint32_t)p->width);
             y = (int)(s.pix / (uint32_t)p->width);
             if (!gmm_ray(p, x, y, &o, &d, &tnear, &tfar)) continue; /* not produced by a slab */
@@ -1191,7 +1209,7 @@ int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, i
         const int alive = gmm_march(v, NULL, p, z_lo, z_hi, slab, d, tfar, &s, mark);
         samples += (int64_t)(s.n - n0);
         if (alive) {
-            rays_out[k_out++] = s;
+            gmm_pack(&s, rays_out + (uint64_t)(k_out++) * ORC_GMM_RAY_WORDS);
             continue;
         }
         const float rgba[4] = {s.sum[0] * p->brightness, s.sum[1] * p->brightness,

@@ -143,11 +143,15 @@ void orc_synth_fill(int nx, int ny, int nz, int nbins, uint64_t seed, float *vol
  * Restates vr_gmm.hip (this build's extension; the reference has no GMM).
  * wm: (w, mu) pairs [voxel][K][2]; sg: sigma [voxel][K]; voxel order
  * x + nx*(y + ny*(z - z_base)) over the resident slices [z_base, z_base + nzs). */
-typedef struct {                  /* alive-list entry, 48 bytes (GmmRay)        */
+typedef struct {                  /* march state of one ray                     */
     float sum[4];
     float t, pos[3];
-    uint32_t pix, n, pad0, pad1;
+    uint32_t pix, n;
 } orc_gmm_ray;
+
+/* alive-list entry (vr_gmm.hip GmmRay): 9 uint32 words -- sum[4], t, pos[3]
+ * as float bits, then pix | n << 23 (pixel < 2^23, samples <= 500) */
+#define ORC_GMM_RAY_WORDS 9
 
 typedef struct {
     const float *wm, *sg;
@@ -164,13 +168,14 @@ void orc_synth_gmm(int nx, int ny, int nz, int K, uint64_t seed, int z_base, int
 
 /* Render with a GMM volume.  z_lo/z_hi: the slab (samples whose footprint z0
  * lies in [z_lo, z_hi)); whole volume: 0, nz with rays_out == NULL.  rays_in ==
- * NULL: camera rays of the whole frame; else n_in alive-list entries.  Rays
- * leaving the slab alive are appended to rays_out (in input / raster order),
+ * NULL: camera rays of the whole frame; else n_in alive-list entries
+ * (ORC_GMM_RAY_WORDS words each).  Rays leaving the slab alive are appended to
+ * rays_out (in input / raster order),
  * their count stored in *n_out.  out / out_f / out_n as orc_render (pixel
  * y*width + x).  mark: optional footprint bitset over nx*ny*nz voxels.
  * Returns the samples taken. */
 int64_t orc_render_gmm(const orc_gmm *v, const orc_render_params *p, int z_lo, int z_hi,
-                       const orc_gmm_ray *rays_in, uint32_t n_in, orc_gmm_ray *rays_out,
+                       const uint32_t *rays_in, uint32_t n_in, uint32_t *rays_out,
                        uint32_t *n_out, uint32_t *out, float *out_f, int32_t *out_n,
                        uint64_t *mark);
 

@@ -453,15 +453,17 @@ def test_period_with_handoff(pkg):
     S = pkg.slabs
     link = 100.0  # GB/s: 1e8 bytes = 1 ms
     march = [2.0, 1.0, 0.5, 0.25]
-    rays = [25_000_000 // 12, 10_000_000 // 12, 0, 0]  # 48-B rays: ~1 ms and ~0.4 ms hops
+    rb = S.RAY_WORDS * 4  # bytes per alive-list entry (36)
+    rays = [100_000_000 // rb, 40_000_000 // rb, 0, 0]  # ~1 ms and ~0.4 ms hops
     owners = [0, 1, 1, 0]  # two-segment snake of 2 ranks: 1 -> 1 is local
     serial, overlap, rows = S.period_with_handoff(march, rays, owners, 2, 10_000_000, link)
-    hop0 = (rays[0] * 48 + 8) / 1e8
+    hop0 = (rays[0] * rb + 8) / 1e8
     assert abs(rows[0]["send_ms"] - hop0) < 1e-4 and abs(rows[1]["recv_ms"] - hop0) < 1e-4
     assert rows[1]["send_ms"] == 0.0  # segment 1 -> 2 stays on rank 1
     hop2 = 8 / 1e8  # segment 2 -> 3: the count only
     assert abs(rows[0]["recv_ms"] - hop2) < 1e-4
     assert rows[0]["reduce_ms"] == 0.1
     assert abs(rows[0]["serial_ms"] - (2.25 + hop0 + hop2 + 0.1)) < 1e-3
+    assert S.RAY_WORDS == 9
     assert abs(rows[1]["overlap_ms"] - 1.5) < 1e-3
     assert serial == max(r["serial_ms"] for r in rows) and overlap <= serial

@@ -163,6 +163,37 @@ def test_baked_plane8_copy(pkg, orc, gpu, baked, dims, tune):
     assert pkg.layout_info()["resident_bytes"] == 0
 
 
+def test_baked_plane_copies_kept_per_method(pkg, orc, gpu, baked):
+    """a client alternating methods 1/2/3 on oblique baked frames builds
+    each method's 8 x 2 x 2 plane copy once (one copy per (axis, method) while the
+    layout budget holds them), every frame still bit-identical; a budget that
+    holds one copy only keeps replacing it, and the frames stay exact"""
+    import torch
+    vol = orc.synth_volume(30, 26, 22, 8)
+    pkg.init_distribution(vol)
+    pkg.bake_stats()
+    W, H = 96, 64
+    m = pkg.camera.display_inv_view((30.0, 45.0))
+    refs = {q: orc.render(vol, orc.make_params(W, H, m, query_method=q))[:3] for q in (1, 2, 3)}
+    b0 = pkg.layout_info()["builds"]
+    for _ in range(3):
+        for q in (1, 2, 3):
+            got = gpu_render(pkg, None, W, H, m, q, torch)
+            assert "plane8" in pkg.last_kernel(), pkg.last_kernel()
+            assert_parity(got, refs[q], f"alternating m{q}")
+    info = pkg.layout_info()
+    assert info["builds"] - b0 == 3, info  # one copy per method, made once
+    one = info["resident_bytes"] // 3
+    pkg.set_layout_budget(one + one // 2)  # room for one copy: drops all three
+    assert pkg.layout_info()["resident_bytes"] == 0
+    for q in (1, 2, 1):
+        got = gpu_render(pkg, None, W, H, m, q, torch)
+        assert_parity(got, refs[q], f"one-copy budget m{q}")
+        assert pkg.layout_info()["resident_bytes"] <= one + one // 2
+    pkg.set_layout_budget(None)
+    pkg.release_stats()
+
+
 def test_baked_tile_lists(pkg, orc, gpu, baked):
     """multi-GPU tile lists over the baked planes (segmented march for short lists):
     packed tiles unscatter to the oracle's frame"""

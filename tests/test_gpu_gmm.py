@@ -79,15 +79,16 @@ def test_synth_gmm_matches_oracle(pkg, orc, gpu):
     pkg.free_gmm()
 
 
-@pytest.mark.parametrize("c", ["C0", "C1", "below"])
-@pytest.mark.parametrize("nslabs", [2, 3, 5])
-def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs):
+@pytest.mark.parametrize("c,nslabs,K", [(c, n, 16) for c in ("C0", "C1", "below") for n in (2, 3, 5)]
+                         + [("C1", 3, 8), ("C0", 2, 8), ("C1", 3, 32), ("below", 5, 32)])
+def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs, K):
     """each slab generated on its own (only its slices + halo resident), the alive
     list handed from slab to slab on the device: the frame, the samples and every
-    alive ray's exact state equal the oracle's chain and the whole-volume render"""
+    alive ray's exact state (9-word entries, written by the K/4 lanes of a ray's
+    group: 2 lanes at K = 8) equal the oracle's chain and the whole-volume render"""
     import torch
     dims = (24, 20, 23)
-    K, method, W, H = 16, 1 if nslabs != 3 else 2, 72, 56
+    method, W, H = 1 if nslabs != 3 else 2, 72, 56
     m = cam(pkg, c)
     direction = pkg.slabs.march_direction(m, W, H)
     bounds = pkg.slabs.slab_bounds(dims[2], nslabs, direction)
@@ -99,7 +100,7 @@ def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs):
     steps = torch.full((H * W,), -2, dtype=torch.int32, device="cuda")
     d = pkg.make_desc(out, W, H, m, query_method=method, density=0.2, volume_size=(1, 1, 1),
                       d_output_f=out_f, d_steps=steps)
-    bufs = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
+    bufs = [torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device="cuda") for _ in range(2)]
     cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
     n_in = 0
     ref_rays = None
@@ -116,8 +117,9 @@ def test_gmm_slab_chain(pkg, orc, gpu, c, nslabs):
         ref_rays = r["rays_out"]
         assert n_in == ref_rays.shape[0], f"slab {i}: {n_in} alive rays vs {ref_rays.shape[0]}"
         got_rays = bufs[i % 2][:n_in].cpu().numpy().view(np.uint32)
-        order = np.argsort(got_rays[:, 8], kind="stable")
-        assert np.array_equal(got_rays[order], ref_rays[np.argsort(ref_rays[:, 8], kind="stable")])
+        pix = lambda a: a[:, 8] & 0x7FFFFF  # the entry's last word: pixel | samples << 23
+        order = np.argsort(pix(got_rays), kind="stable")
+        assert np.array_equal(got_rays[order], ref_rays[np.argsort(pix(ref_rays), kind="stable")])
     assert n_in == 0
     torch.cuda.synchronize()
     got = (out.cpu().numpy().view(np.uint32).reshape(H, W), out_f.cpu().numpy().reshape(H, W, 4),
@@ -142,7 +144,7 @@ def test_gmm_slab_footprint_and_list_capacity(pkg, orc, gpu):
     p = orc.make_params(W, H, m, query_method=1)
     out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     d = pkg.make_desc(out, W, H, m, query_method=1, volume_size=(1, 1, 1))
-    bufs = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
+    bufs = [torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device="cuda") for _ in range(2)]
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     n_in, ref_rays = 0, None
     for i, (z_lo, z_hi) in enumerate(bounds):
@@ -167,7 +169,7 @@ def test_gmm_slab_footprint_and_list_capacity(pkg, orc, gpu):
     # by the launch: exactly the alive rays are listed, the rows past the list untouched
     zb, ns = pkg.slabs.resident_slices(*bounds[0], dims[2])
     pkg.synthesize_gmm(dims, K, z_base=zb, nslices=ns)
-    big = torch.full((W * H + 64, 12), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    big = torch.full((W * H + 64, pkg.slabs.RAY_WORDS), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
     cnt.fill_(W * H - 3)
     pkg.render_gmm(d, pkg.gmm_slab(*bounds[0], big, cnt))
     torch.cuda.synchronize()
@@ -200,7 +202,7 @@ def test_gmm_errors(pkg, orc, gpu):
     dims = (16, 16, 16)
     pkg.synthesize_gmm(dims, 8, z_base=4, nslices=6)
     out = torch.zeros(32 * 32, dtype=torch.int32, device="cuda")
-    rays = torch.zeros((32 * 32, 12), dtype=torch.int32, device="cuda")
+    rays = torch.zeros((32 * 32, pkg.slabs.RAY_WORDS), dtype=torch.int32, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     m = pkg.camera.single_test_inv_view()
     d = pkg.make_desc(out, 32, 32, m, query_method=1, volume_size=(1, 1, 1))
@@ -304,7 +306,7 @@ def test_config5_at_size(pkg, orc, gpu):
     frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     steps = torch.full((W * H,), -2, dtype=torch.int32, device="cuda")
     d = pkg.make_desc(frame, W, H, m, query_method=1, volume_size=(1, 1, 1), d_steps=steps)
-    bufs = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
+    bufs = [torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device="cuda") for _ in range(2)]
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     n_in, done = 0, 0
     try:

@@ -45,7 +45,7 @@ def main():
     bounds = pkg.slabs.slab_bounds(n, a.slabs, direction)
     frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     desc = pkg.make_desc(frame, W, H, m, query_method=a.method, volume_size=(1, 1, 1))
-    rays = [torch.zeros((W * H, 12), dtype=torch.int32, device="cuda") for _ in range(2)]
+    rays = [torch.zeros((W * H, pkg.slabs.RAY_WORDS), dtype=torch.int32, device="cuda") for _ in range(2)]
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     rows = run_chain(a, pkg, torch, np, s, bounds, n, K, W, H, desc, rays, cnt, frame, "equal")
     if a.balance:

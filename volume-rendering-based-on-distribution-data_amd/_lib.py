@@ -69,7 +69,7 @@ class GmmSlab(ctypes.Structure):
     ]
 
 
-GMM_RAY_BYTES = 48  # alive-list entry: float sum[4], t, pos[3]; uint32 pixel, samples, 0, 0
+GMM_RAY_BYTES = 36  # alive-list entry: float sum[4], t, pos[3]; uint32 pixel | samples << 23
 
 
 class FlexTables(ctypes.Structure):

@@ -257,8 +257,8 @@ def stats_info():
 
 def set_layout_budget(nbytes=None) -> None:
     """Cap the HBM the library spends on layout copies (micro-brick and
-    axis-rows copies of the records, include/vr.h): None = no cap beyond the
-    free-memory guard, 0 = never make one."""
+    axis-rows copies of the records, baked-plane copies; include/vr.h): None =
+    the default budget, 0 = never make one."""
     check(_lib.load().vr_set_layout_budget(0xFFFFFFFFFFFFFFFF if nbytes is None else int(nbytes)))
 
 

@@ -89,13 +89,13 @@ struct State {
         uint64_t sx = 0, sy = 0, sz = 0, bytes = 0;
     } acopy[2];
     uint64_t brick_bytes = 0;
-    // axis copies of a baked plane for baked frames of views along y ([0]) or
-    // z ([1]) (ensure_plane_copy, k_plane_axis): which plane, its pitches
+    // copies of a baked plane (ensure_plane_copy): [axis - 1][plane], axis 1 / 2
+    // the y / z-rows copies for views along y or z (k_plane_axis), axis 3 the
+    // 8 x 2 x 2 brick copy for oblique views (k_plane8); plane 0-2 = methods 1-3
     struct PlaneCopy {
         float *buf = nullptr;
-        int plane = -1;
         uint64_t sy = 0, sz = 0, bytes = 0;
-    } pcopy[3];  // [2]: the 8 x 2 x 2 brick copy for oblique views (k_plane8)
+    } pcopy[3][3];
     // layout copies (micro-bricks, axis rows): byte budget (vr_set_layout_budget;
     // UINT64_MAX = the default, layout_budget_bytes) and the cost of the last one
     // made (vr_layout_info)
@@ -171,20 +171,21 @@ void release_axis_copy() {
     release_axis_copy(1);
 }
 
-void release_plane_copy(int i) {
-    if (g.pcopy[i].buf) (void)hipFree(g.pcopy[i].buf);
-    g.pcopy[i] = State::PlaneCopy();
+void release_plane_copy(int a, int p) {
+    if (g.pcopy[a][p].buf) (void)hipFree(g.pcopy[a][p].buf);
+    g.pcopy[a][p] = State::PlaneCopy();
 }
 
 void release_plane_copies() {
-    release_plane_copy(0);
-    release_plane_copy(1);
-    release_plane_copy(2);
+    for (int a = 0; a < 3; a++)
+        for (int p = 0; p < 3; p++) release_plane_copy(a, p);
 }
 
 uint64_t layout_resident() {
-    return g.brick_bytes + g.acopy[0].bytes + g.acopy[1].bytes + g.pcopy[0].bytes + g.pcopy[1].bytes +
-           g.pcopy[2].bytes;
+    uint64_t b = g.brick_bytes + g.acopy[0].bytes + g.acopy[1].bytes;
+    for (int a = 0; a < 3; a++)
+        for (int p = 0; p < 3; p++) b += g.pcopy[a][p].bytes;
+    return b;
 }
 
 // Room for a layout copy of `bytes`: within the budget (vr_set_layout_budget)
@@ -1051,12 +1052,17 @@ bool ensure_axis_copy(int axis) {
 // (k_plane8, gather8 MODE 6), whose lines also hold a footprint's z pair
 // (per 64x4-tile line floor at 1024^3 C1: 3.77 -> 3.47 GB);
 // VR_PLANE8=0 keeps such views on the 16 x 2 x 1 plane.
+// Each (axis, method plane) keeps its own copy while the layout budget holds
+// them, so a client alternating methods on one view class builds each copy
+// once (one copy per axis was rebuilt -- hipMalloc, k_plane8, a
+// stream sync, ~4.6 GB at 1024^3 -- on every method change); only when the
+// budget is short are this axis' other planes' copies dropped for the new one.
 bool ensure_plane_copy(int plane, int axis) {
     if (const char *e = vr::tuning(axis == 3 ? "VR_PLANE8" : "VR_ZROWS"))
         if (std::atoi(e) == 0) return false;
     const int i = axis - 1;
-    if (g.pcopy[i].buf && g.pcopy[i].plane == plane) return true;
     if (!g.stats || plane < 0 || plane > 2) return false;
+    if (g.pcopy[i][plane].buf) return true;
     const uint32_t nf = axis == 2 ? g.nz : g.ny, np = axis == 2 ? g.ny : g.nx;
     uint64_t ns = axis == 2 ? (uint64_t)g.nx : (uint64_t)g.nz;
     if (nf >= (1u << 16) || np > 65535 || ns > 65535 || g.nx > 65535) return false;
@@ -1070,9 +1076,12 @@ bool ensure_plane_copy(int plane, int axis) {
     // gather8 MODE 4/5/6: 32-bit offsets inside a slice (pair)
     if (dsz >= (1ull << 32)) return false;
     const uint64_t bytes = (dsz * ns + 4) * sizeof(float);
-    const uint64_t freed = g.pcopy[i].bytes;  // another plane's copy of this axis
-    if (!layout_room(bytes, freed)) return false;
-    release_plane_copy(i);
+    if (!layout_room(bytes, 0)) {  // room only without this axis' other planes' copies
+        uint64_t freed = 0;
+        for (int p = 0; p < 3; p++) freed += g.pcopy[i][p].bytes;
+        if (!layout_room(bytes, freed)) return false;
+        for (int p = 0; p < 3; p++) release_plane_copy(i, p);
+    }
     float *buf = nullptr;
     if (hipMalloc(&buf, bytes) != hipSuccess) {
         (void)hipGetLastError();
@@ -1093,11 +1102,10 @@ bool ensure_plane_copy(int plane, int axis) {
     g.layout_last_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     g.layout_last_bytes = bytes;
     g.layout_builds++;
-    g.pcopy[i].buf = buf;
-    g.pcopy[i].plane = plane;
-    g.pcopy[i].sy = dsy;
-    g.pcopy[i].sz = dsz;
-    g.pcopy[i].bytes = bytes;
+    g.pcopy[i][plane].buf = buf;
+    g.pcopy[i][plane].sy = dsy;
+    g.pcopy[i][plane].sz = dsz;
+    g.pcopy[i][plane].bytes = bytes;
     return true;
 }
 
@@ -1711,7 +1719,7 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
             // oblique views: the 8 x 2 x 2 brick copy (axis 3)
             if (!ax) ax = 3;
             if (ensure_plane_copy(qm - 1, ax)) {
-                const State::PlaneCopy &c = g.pcopy[ax - 1];
+                const State::PlaneCopy &c = g.pcopy[ax - 1][qm - 1];
                 baked = c.buf;
                 P.sy = c.sy;
                 P.sz = c.sz;
@@ -1968,6 +1976,10 @@ int fill_gmm_params(const vr_render_desc *d, const vr_gmm_slab *slab, vr::Params
         if ((uint64_t)slab->n_rays_in > (uint64_t)d->width * d->height)
             return fail(VR_ERR_ARG, "%u alive rays in for a %ux%u frame", slab->n_rays_in,
                         d->width, d->height);
+        // an alive-list entry holds the pixel in 23 bits (vr_gmm.hip GmmRay)
+        if ((uint64_t)d->width * d->height > (1ull << 23))
+            return fail(VR_ERR_ARG, "slab chains address at most 2^23 pixels (%ux%u)",
+                        d->width, d->height);
         // slabs must be taken in the order every ray crosses them: the sign of
         // a ray's z step is that of the linear form u M8 + v M9 - 2 M10, so the
         // four frame corners decide whether it is the same for the whole frame
@@ -1985,9 +1997,9 @@ int fill_gmm_params(const vr_render_desc *d, const vr_gmm_slab *slab, vr::Params
                         "slab-chained rendering needs one crossing order");
         P.z_lo = slab->z_lo;
         P.z_hi = slab->z_hi;
-        P.rays_in = reinterpret_cast<const uint4 *>(slab->d_rays_in);
+        P.rays_in = reinterpret_cast<const uint32_t *>(slab->d_rays_in);
         P.n_rays_in = slab->d_rays_in ? slab->n_rays_in : 0;
-        P.rays_out = reinterpret_cast<uint4 *>(slab->d_rays_out);
+        P.rays_out = reinterpret_cast<uint32_t *>(slab->d_rays_out);
         P.n_rays_out = slab->d_n_rays_out;
     }
     if (P.rays_in || (slab && slab->d_rays_in)) {

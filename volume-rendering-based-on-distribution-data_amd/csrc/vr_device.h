@@ -87,9 +87,9 @@ struct Params {
     int gk;
     int z_base, nzs;
     int z_lo, z_hi;              // slab: samples whose footprint z0 lies in [z_lo, z_hi)
-    const uint4 *rays_in;        // slab chain: alive rays entering (GmmRay), nullptr = camera
+    const uint32_t *rays_in;     // slab chain: alive rays entering (GmmRay, 9 words), nullptr = camera
     uint32_t n_rays_in;
-    uint4 *rays_out;             // alive rays leaving the slab (nullptr: slab = whole volume)
+    uint32_t *rays_out;          // alive rays leaving the slab (nullptr: slab = whole volume)
     uint32_t *n_rays_out;
     int wq_map;                  // k_march_wq pixel map: 0 a 64-pixel row per wave, 1 16x4 blocks
     int quad2;                   // quad march with two lanes per ray (k_march_quad2)

@@ -46,13 +46,18 @@
 
 namespace vr {
 
-// alive-list entry: 48 bytes, three uint4
+// alive-list entry: 36 bytes, 9 words -- the colour sums, t, the position and
+// the pixel (23 bits: W*H <= 2^23, 3840x2160 fits) with the samples taken
+// (9 bits: <= 500, K:381) in one word.  Every ray handed between ranks crosses
+// xGMI as one entry, so its size is the chain's hand-off cost.
+constexpr int kGmmRayWords = 9;
+constexpr uint32_t kGmmPixBits = 23;
 struct GmmRay {
     float sx, sy, sz, sw;
     float t, px, py, pz;
-    uint32_t pix, n, pad0, pad1;
+    uint32_t pix_n;               // pix | n << 23
 };
-static_assert(sizeof(GmmRay) == 48, "GmmRay is 3 x uint4");
+static_assert(sizeof(GmmRay) == 4 * kGmmRayWords, "GmmRay is 9 words");
 
 // ---- cross-lane sum over an L-lane group, T(p) above ----
 template <int CTRL>
@@ -119,7 +124,7 @@ __device__ __forceinline__ bool gmm_begin(const Params &P, uint32_t wave_base, u
         const uint32_t k = wave_base + e;
         if (k >= P.n_rays_in) return false;
         in = reinterpret_cast<const GmmRay *>(P.rays_in) + k;
-        s.pix = in->pix;
+        s.pix = in->pix_n & ((1u << kGmmPixBits) - 1u);
         x = s.pix % P.W;
         y = s.pix / P.W;
     } else {
@@ -138,7 +143,7 @@ __device__ __forceinline__ bool gmm_begin(const Params &P, uint32_t wave_base, u
     if (in) {
         s.sx = in->sx; s.sy = in->sy; s.sz = in->sz; s.sw = in->sw;
         s.t = in->t; s.px = in->px; s.py = in->py; s.pz = in->pz;
-        s.n = (int)in->n;
+        s.n = (int)(in->pix_n >> kGmmPixBits);
     } else {
         s.sx = s.sy = s.sz = s.sw = 0.0f;
         s.t = s.r.tnear;
@@ -195,17 +200,21 @@ __device__ __forceinline__ void gmm_emit(const Params &P, const GmmState &s, uin
     base = __shfl(base, __builtin_ctzll(out), 64);
     const uint32_t k = base + (uint32_t)__popcll(out & ((1ull << (lane & ~(uint32_t)(L - 1))) - 1ull));
     // the list's capacity (include/vr.h): no slab emits more rays than enter
-    // it, so only a counter the caller did not zero reaches it -- such entries
-    // are dropped (the count still says how many), never written past the end
+    // it and the library zeroes the counter before the launch, so this is a
+    // second guard -- entries past it are dropped, never written past the end
     const uint64_t cap = P.rays_in ? (uint64_t)P.n_rays_in : (uint64_t)P.W * P.H;
-    if (sub < 3 && (uint64_t)k < cap) {
-        uint4 v;
-        if (sub == 0) v = make_uint4(__float_as_uint(s.sx), __float_as_uint(s.sy),
-                                     __float_as_uint(s.sz), __float_as_uint(s.sw));
-        else if (sub == 1) v = make_uint4(__float_as_uint(s.t), __float_as_uint(s.px),
-                                          __float_as_uint(s.py), __float_as_uint(s.pz));
-        else v = make_uint4(s.pix, (uint32_t)s.n, 0u, 0u);
-        P.rays_out[(uint64_t)k * 3u + sub] = v;
+    if ((uint64_t)k < cap) {
+        // the group's L lanes share the 9 words: lane sub writes words sub,
+        // sub + L, ... (K = 8: two lanes, five and four words)
+        const uint32_t w[kGmmRayWords] = {
+            __float_as_uint(s.sx), __float_as_uint(s.sy), __float_as_uint(s.sz),
+            __float_as_uint(s.sw), __float_as_uint(s.t), __float_as_uint(s.px),
+            __float_as_uint(s.py), __float_as_uint(s.pz),
+            s.pix | ((uint32_t)s.n << kGmmPixBits)};
+        uint32_t *dst = P.rays_out + (uint64_t)k * kGmmRayWords;
+#pragma unroll
+        for (int j = 0; j < kGmmRayWords; j++)
+            if ((uint32_t)(j % L) == sub) dst[j] = w[j];
     }
 }
 

@@ -21,7 +21,7 @@ from typing import List, Optional, Tuple
 
 import numpy as np
 
-RAY_WORDS = 12  # alive-list entry: 48 bytes (float sum[4], t, pos[3]; u32 pixel, samples, 0, 0)
+RAY_WORDS = 9  # alive-list entry: 36 bytes (float sum[4], t, pos[3]; u32 pixel | samples << 23)
 
 
 def march_direction(inv_view, width: int, height: int) -> int:
@@ -258,7 +258,7 @@ def _staged(dist, group=None) -> bool:
 
 
 def send_alive(rays, count: int, dst: int, dist, group=None) -> None:
-    """Send an alive list (first `count` rows of an (n, 12) int32 tensor) to rank
+    """Send an alive list (first `count` rows of an (n, RAY_WORDS) int32 tensor) to rank
     dst: the count first, then the rows (RCCL point-to-point over xGMI on GPUs)."""
     import torch
     dev = "cpu" if _staged(dist, group) else rays.device
@@ -296,7 +296,7 @@ def isend_alive(rays, count: int, dst: int, dist, group=None) -> _Sends:
 
 
 def recv_alive(src: int, out, dist, group=None) -> int:
-    """Receive an alive list from rank src into out ((cap, 12) int32 tensor);
+    """Receive an alive list from rank src into out ((cap, RAY_WORDS) int32 tensor);
     returns its length."""
     import torch
     dev = "cpu" if _staged(dist, group) else out.device
