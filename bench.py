@@ -189,30 +189,38 @@ def lib_sha16(path):
     return h.hexdigest()[:16]
 
 
-def traffic_entry(args, kernel, world):
-    """(HBM bytes per launch, where they come from) of this workload from the
-    committed PMC passes (profiles/traffic.json, tools/pmc_traffic.py), or
-    (None, why not): only entries measured on this same libvr.so build (its
-    sha256) and kernel count -- a rebuilt library needs a new PMC pass"""
-    if world != 1:
-        return None, ("no PMC pass of a rank's tile list: the committed passes "
-                      "(profiles/traffic.json) are keyed by whole-frame single-GPU workloads, "
-                      "and rocprofv3 --pmc is not run under the multi-rank launcher")
+def traffic_entry(args, kernel, world, lists_sha=None, rank=0):
+    """(PMC entry, where it comes from) of this workload from the committed
+    passes (profiles/traffic.json), or (None, why not): only entries measured on
+    this same libvr.so build (its sha256) and kernel count -- a rebuilt library
+    needs a new PMC pass.  N = 1: a whole frame's HBM bytes per launch
+    (tools/pmc_traffic.py).  N > 1: every rank's bytes per launch of its tile
+    list, measured by tools/rank_traffic.py on one GPU for the very lists this
+    run dealt (the entry's lists_sha16 must equal this run's)."""
     if not args.traffic_json or not os.path.exists(args.traffic_json):
         return None, None
     import __graft_entry__ as graft
     key = f"{args.config}|{args.camera}|m{args.method}" + ("|baked" if args.baked else "")
+    if world > 1:
+        key += f"|N{world}"
     with open(args.traffic_json) as f:
         entry = json.load(f).get(key)
     if not entry:
-        return None, f"no PMC entry for {key}"
+        return None, f"no PMC entry for {key}" + (" (per-rank lists: tools/rank_traffic.py)"
+                                                  if world > 1 else "")
     sha = lib_sha16(graft.load_package().LIB_PATH)
-    if entry.get("kernel") != kernel or entry.get("lib_sha16") != sha:
-        return None, (f"PMC entry {key} was measured on {entry.get('kernel')} of libvr.so "
+    want = entry["kernels"][rank] if world > 1 and entry.get("kernels") else entry.get("kernel")
+    if want != kernel or entry.get("lib_sha16") != sha:
+        return None, (f"PMC entry {key} was measured on {want} of libvr.so "
                       f"{entry.get('lib_sha16')}, this run is {kernel} of {sha}")
+    if world > 1 and entry.get("lists_sha16") != lists_sha:
+        return None, (f"PMC entry {key} was measured on tile lists {entry.get('lists_sha16')}, "
+                      f"this run dealt {lists_sha}")
+    what = ("per rank, each rank's tile list rendered alone (tools/rank_traffic.py)"
+            if world > 1 else "per launch")
     return entry, (
-        f"{os.path.relpath(args.traffic_json, ROOT)}[{key}]: FETCH_SIZE x 2 + WRITE_SIZE per "
-        f"launch, rocprofv3 --pmc on this libvr.so build ({sha}), {entry.get('measured', '')}")
+        f"{os.path.relpath(args.traffic_json, ROOT)}[{key}]: FETCH_SIZE x 2 + WRITE_SIZE {what}, "
+        f"rocprofv3 --pmc on this libvr.so build ({sha}), {entry.get('measured', '')}")
 
 
 VALU_ISSUE_CYCLES = 2      # SIMD cycles per f32 wave64 VALU instruction (f64 adds: ~4.4,
@@ -350,7 +358,7 @@ def assembled_parity(frame8, ref, row_stride, world, full_render):
     }
 
 
-def aggregate_roofline(per_rank, ms_per_step, peak_gbs=HBM_PEAK_GBS):
+def aggregate_roofline(per_rank, ms_per_step, peak_gbs=HBM_PEAK_GBS, rank_traffic=None):
     """Whole-node roofline of an N-rank frame.  per_rank: one row per rank of
     (algorithmic bytes of its launch, U of its tile list or -1, its render ms
     alone, pixels it renders).  Every rank reads its own footprint from its own
@@ -358,7 +366,9 @@ def aggregate_roofline(per_rank, ms_per_step, peak_gbs=HBM_PEAK_GBS):
     N x 8 TB/s: frac = sum(alg) / ms_per_step / (N x peak).  Beside it the same
     bytes over the slowest rank's render alone (what the frame's compute could
     reach without the gather, the assembly and the host) and the slowest
-    rank's own fraction."""
+    rank's own fraction.  rank_traffic (optional): every rank's PMC bytes per
+    launch of its list (tools/rank_traffic.py): the node's fabric traffic per
+    frame is their sum."""
     per_rank = np.asarray(per_rank, dtype=np.float64)
     n = per_rank.shape[0]
     alg, u, ms, px = per_rank.T
@@ -366,7 +376,7 @@ def aggregate_roofline(per_rank, ms_per_step, peak_gbs=HBM_PEAK_GBS):
     node = total / (ms_per_step * 1e-3) / 1e9
     slow = int(np.argmax(ms))
     frac = lambda b, t, k: round(b / (t * 1e-3) / 1e9 / (k * peak_gbs), 4)
-    return {
+    out = {
         "ranks": n, "peak": n * peak_gbs, "unit": "GB/s",
         "alg_bytes_per_frame": int(total),
         "U_records": int(u.sum()) if np.all(u >= 0) else None,
@@ -379,34 +389,71 @@ def aggregate_roofline(per_rank, ms_per_step, peak_gbs=HBM_PEAK_GBS):
                       "render_ms": round(float(ms[r]), 4), "pixels": int(px[r]),
                       "frac": frac(alg[r], ms[r], 1)} for r in range(n)],
     }
+    if rank_traffic is not None:
+        tr = [int(v) for v in rank_traffic]
+        out["traffic"] = sum(tr)
+        out["traffic_x_alg"] = round(sum(tr) / total, 4)
+        out["traffic_GBps"] = round(sum(tr) / (ms_per_step * 1e-3) / 1e9, 1)
+        for r, row in enumerate(out["per_rank"]):
+            row["traffic"] = tr[r]
+            row["traffic_GBps"] = round(tr[r] / (ms[r] * 1e-3) / 1e9, 1)
+    return out
 
 
-def balanced_lists(pkg, lists, world, rank, W, H, m, method, dev, stream, backend):
-    """Re-deal the tiles by measured cost (untimed, once per view): every rank
-    renders its estimate-ordered list once with per-pixel sample counts, the
-    per-tile costs are summed over ranks (one all_reduce of a tiles-sized
-    vector, 32 KB at 1080p) and every rank derives the same cost-dealt lists
-    (tiles.tile_lists_by_cost): ranks and their XCDs get equal work, not only
-    equal pixel counts."""
-    import torch
-    import torch.distributed as dist
-    n_slots = lists.shape[1]
+def rank_costs(pkg, torch, lst, W, H, m, method, dev, stream):
+    """Per-tile costs (tiles.tile_costs_from_steps, int64) of one rank's tile list,
+    rendered once with per-pixel sample counts (untimed)."""
+    n_slots = lst.shape[0]
     n_tiles = pkg.tiles.tiles_x(W) * pkg.tiles.tiles_y(H)
     with torch.cuda.stream(stream):
-        tl = torch.from_numpy(lists[rank].view(np.int32).copy()).to(dev)
+        tl = torch.from_numpy(lst.view(np.int32).copy()).to(dev)
         buf = torch.zeros(n_slots * 256, dtype=torch.int32, device=dev)
         steps = torch.full((n_slots * 256,), -1, dtype=torch.int32, device=dev)
         pkg.render(pkg.make_desc(buf, W, H, m, query_method=method, d_tile_list=tl,
                                  n_tiles=n_slots, d_steps=steps))
     torch.cuda.synchronize()
-    cost = torch.from_numpy(pkg.tiles.tile_costs_from_steps(steps.cpu().numpy(), lists[rank],
-                                                            n_tiles))
+    return pkg.tiles.tile_costs_from_steps(steps.cpu().numpy(), lst, n_tiles)
+
+
+def deal_by_cost(pkg, world, W, H, cost):
+    """The cost-dealt lists every rank derives from the summed per-tile costs;
+    rank 0 takes a smaller share (it also receives and assembles the frame)."""
+    share = np.ones(world)
+    share[0] = pkg.tiles.rank0_share(world)
+    return pkg.tiles.tile_lists_by_cost(W, H, world, np.asarray(cost), share=share)
+
+
+def lists_sha16(lists):
+    """Identity of a split's tile lists (keys the per-rank PMC traffic entries)."""
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(lists, dtype=np.uint32).tobytes()).hexdigest()[:16]
+
+
+def balanced_lists(pkg, lists, world, rank, W, H, m, method, dev, stream, backend):
+    """Re-deal the tiles by measured cost (untimed, once per view): every rank
+    renders its estimate-ordered list once with per-pixel sample counts, the
+    per-tile costs are summed over ranks (one all_reduce of a tiles-sized int64
+    vector, 64 KB at 1080p) and every rank derives the same cost-dealt lists
+    (tiles.tile_lists_by_cost): ranks and their XCDs get equal work, not only
+    equal pixel counts.  The sums are integers, so emulated_rank_lists derives
+    the very same lists in one process."""
+    import torch
+    import torch.distributed as dist
+    cost = torch.from_numpy(rank_costs(pkg, torch, lists[rank], W, H, m, method, dev, stream))
     if backend == "nccl":
         cost = cost.to(dev)
     dist.all_reduce(cost)
-    share = np.ones(world)
-    share[0] = pkg.tiles.rank0_share(world)  # rank 0 also receives and assembles the frame
-    return pkg.tiles.tile_lists_by_cost(W, H, world, cost.cpu().numpy(), share=share)
+    return deal_by_cost(pkg, world, W, H, cost.cpu().numpy())
+
+
+def emulated_rank_lists(pkg, torch, world, W, H, m, method, dev, stream):
+    """The cost-dealt lists of a `world`-rank bench run, derived in one process
+    on one GPU (every rank's estimate list rendered in turn, the costs summed as
+    the all_reduce would): tools/rank_traffic.py profiles each rank's list."""
+    lists = pkg.tiles.tile_lists(W, H, world, m)
+    cost = sum(rank_costs(pkg, torch, lists[r], W, H, m, method, dev, stream)
+               for r in range(world))
+    return deal_by_cost(pkg, world, W, H, cost)
 
 
 def gmm_cpu_baseline(m, method, W, H, K):
@@ -1285,8 +1332,11 @@ def main():
     # HBM bytes per launch from the committed PMC passes of this same workload
     # (tools/pmc_traffic.py; FETCH_SIZE x 2 + WRITE_SIZE), only if they were
     # measured on this very libvr.so build (sha256 of the file) and kernel
-    pmc, traffic_src = traffic_entry(args, kernel, world)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    pmc, traffic_src = traffic_entry(args, kernel, world,
+                                     lists_sha16(lists) if world > 1 else None, rank)
+    rank_traffic = pmc.get("per_rank_hbm_bytes") if pmc and world > 1 else None
+    traffic = (rank_traffic[rank] if rank_traffic else None) if world > 1 else (
+        pmc.get("hbm_bytes_per_launch") if pmc else None)
     # the bounds that apply when the frame is not HBM-bound (the smaller configs)
     bounds = (compute_bounds(pkg, torch, stream, W, H, m, args.method, kern_ms, pmc)
               if world == 1 and not args.no_issue_bounds else None)
@@ -1314,7 +1364,7 @@ def main():
     value = W * H / (elapsed / args.steps) / 1e6
     phys = min(world, max(ndev, 1))
     rehearsal = world > phys
-    aggregate = (aggregate_roofline(per_rank, ms_per_step)
+    aggregate = (aggregate_roofline(per_rank, ms_per_step, rank_traffic=rank_traffic)
                  if per_rank is not None and np.all(per_rank[:, 0] > 0) else None)
     out = None
     if rank == 0:
@@ -1366,6 +1416,7 @@ def main():
                 "render_streams": NSTREAMS,
                 "tile_deal": (None if world == 1 else "estimate" if args.no_balance
                               else "measured cost (one untimed frame)"),
+                "lists_sha16": lists_sha16(lists) if world > 1 else None,
                 "parallelism": f"image tiles x{world}" + (
                 (" + RCCL gather" if args.dist_backend == "nccl" else " + gloo host gather")
                 if world > 1 else ""),
@@ -1401,6 +1452,10 @@ def main():
             roof["rank0"] = {k: roof.pop(k) for k in ("achieved", "frac", "kernel_ms",
                                                       "alg_bytes_per_launch", "U_records")}
             roof["aggregate"] = aggregate
+            roof["rank0"]["traffic"] = roof.pop("traffic")
+            roof["rank0"]["traffic_GBps"] = roof.pop("traffic_GBps")
+            roof["traffic"] = aggregate.get("traffic") if aggregate else None
+            roof["traffic_GBps"] = aggregate.get("traffic_GBps") if aggregate else None
             roof["achieved"] = aggregate["achieved"] if aggregate else None
             roof["peak"] = aggregate["peak"] if aggregate else HBM_PEAK_GBS * world
             roof["frac"] = aggregate["frac"] if aggregate else None

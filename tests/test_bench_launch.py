@@ -118,6 +118,12 @@ def test_aggregate_roofline_sums_the_ranks():
     assert a["slowest_rank_frac"] == round(2e9 / 0.8e-3 / 1e9 / 8000, 4)
     assert a["frac_at_render_max"] == round(6e9 / 0.8e-3 / 1e9 / 32000, 4)
     assert [r["rank"] for r in a["per_rank"]] == [0, 1, 2, 3]
+    # per-rank PMC traffic (tools/rank_traffic.py): the node's is the sum
+    t = b.aggregate_roofline(rows, 1.0, rank_traffic=[1.2e9, 2.4e9, 1.8e9, 1.8e9])
+    assert t["traffic"] == 7_200_000_000 and t["traffic_x_alg"] == 1.2
+    assert t["traffic_GBps"] == 7200.0 and t["per_rank"][1]["traffic"] == 2_400_000_000
+    assert t["per_rank"][1]["traffic_GBps"] == round(2.4e9 / 0.8e-3 / 1e9, 1)
+    assert "traffic" not in a
     # a rank without a footprint count (U = -1) leaves the node's U unknown
     rows[2][1] = -1
     assert b.aggregate_roofline(rows, 1.0)["U_records"] is None
@@ -134,3 +140,13 @@ def test_assembled_parity_counts_every_pixel_of_the_oracle_rows():
     p = b.assembled_parity(got, (ref8, None, None), 2, 4, full)
     assert p["rows"] == 3 and p["pixels"] == 12 and p["rgba8_mismatch"] == 1
     assert p["row_stride"] == 2 and "4 ranks" in p["frame"]
+
+
+def test_lists_sha_identifies_a_deal():
+    import numpy as np
+    b = _bench()
+    x = np.arange(24, dtype=np.uint32).reshape(3, 8)
+    y = x.copy()
+    y[2, 7] = 0xFFFFFFFF
+    assert b.lists_sha16(x) == b.lists_sha16(x.copy()) != b.lists_sha16(y)
+    assert len(b.lists_sha16(x)) == 16

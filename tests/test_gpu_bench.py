@@ -62,6 +62,22 @@ def test_bench_single_and_two_rank_frames_agree(gpu, tmp_path):
     assert agg["render_ms_max_over_ranks"] == max(r["render_ms"] for r in agg["per_rank"])
     assert rf2["traffic"] is None and rf2["traffic_source"]
     assert rf2["rank0"]["kernel_ms"] > 0
+    # the deal the two ranks made (all_reduce of integer costs) is the one
+    # tools/rank_traffic.py derives in one process for its per-rank PMC passes
+    import importlib.util
+    import torch
+    import __graft_entry__ as g
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    pkg = g.load_package()
+    n, nb, W, H = bench.CONFIGS["256x4"]
+    pkg.synthesize((n, n, n), nb, bench.SEED)
+    dev = torch.device("cuda", 0)
+    lists = bench.emulated_rank_lists(pkg, torch, 2, W, H, bench.camera_matrix(pkg, "C0"), 1,
+                                      dev, torch.cuda.current_stream())
+    assert bench.lists_sha16(lists) == out2["config"]["lists_sha16"]
+    pkg.freeCudaBuffers()
     a, b = np.load(f1), np.load(f2)
     assert a.shape == (512, 512) and np.count_nonzero(a) > 0
     assert np.array_equal(a, b), f"{int(np.sum(a != b))} pixels differ between N=1 and N=2"
