@@ -219,6 +219,12 @@ def test_gmm_errors(pkg, orc, gpu):
                          volume_size=(1, 1, 1))
     with pytest.raises(pkg.VRError, match="both directions"):
         pkg.render_gmm(side, pkg.gmm_slab(4, 9, rays, cnt))
+    # an alive-list entry holds the pixel in 23 bits: a slab launch of more than
+    # 2^23 pixels is refused before anything runs (3840 x 2160 fits; a whole-
+    # volume render has no list and no limit)
+    big = pkg.make_desc(out, 4096, 2049, m, query_method=1, volume_size=(1, 1, 1))
+    with pytest.raises(pkg.VRError, match="2\\^23"):
+        pkg.render_gmm(big, pkg.gmm_slab(4, 9, rays, cnt))
     with pytest.raises(pkg.VRError):
         pkg.synthesize_gmm(dims, 12)  # K must be 8, 16 or 32
     torch.cuda.synchronize()
