@@ -92,5 +92,22 @@ int main(void) {
         printf("%-28s mismatches: %lld\n", k ? "0.000021 multiply-only" : "0.0217 multiply-only", bad);
         total_bad += bad;
     }
+    /* the entropy's division by ln 2 (vr_device.h div_ln2): the reciprocal of
+     * RN(ln 2) split as Rh (29 significant bits, so m * Rh is exact for a
+     * float m) + Rl; fma(m, Rl, m * Rh) rounds m (Rh + Rl) once, and equals
+     * the correctly rounded m / RN(ln 2) -- double result compared -- for every
+     * float, zeros, infinities and NaN included (no selects) */
+    {
+        const double D = Ds[2], Rh = 0x1.7154765p+0, Rl = 0x1.5c17f278eff00p-31;
+        long long bad = 0;
+#pragma omp parallel for reduction(+ : bad) schedule(static)
+        for (int64_t i = 0; i <= 0xFFFFFFFFll; i++) {
+            const double m = (double)bits_f((uint32_t)i);
+            const double ref = m / D, got = fma(m, Rl, m * Rh);
+            if (d_bits(ref) != d_bits(got) && !(isnan(ref) && isnan(got))) bad++;
+        }
+        printf("%-28s mismatches: %lld\n", "log(2.0) split reciprocal", bad);
+        total_bad += bad;
+    }
     return total_bad != 0;
 }

@@ -2,7 +2,8 @@
 one FMA correction (vr_device.h div_const).  tests/c/divcheck.c proves, over all
 2^32 float inputs, that this is bit-identical to the reference's double division
 (K:758, 759, 766), and that the float-only variance division (div_var_f32) and the
-multiply-only form for float results (div_to_float) are too.  CPU only (gcc + OpenMP, ~15 s on 8 cores)."""
+multiply-only form for float results (div_to_float) are too, and so is the
+entropy's split-reciprocal division by ln 2 (div_ln2).  CPU only (gcc + OpenMP, ~15 s on 8 cores)."""
 import os
 import subprocess
 
@@ -15,4 +16,4 @@ def test_fast_division_is_exact_for_every_float(tmp_path):
                     os.path.join(HERE, "c", "divcheck.c"), "-o", str(exe), "-lm"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count("mismatches: 0") == 6, r.stdout
+    assert r.stdout.count("mismatches: 0") == 7, r.stdout

@@ -327,7 +327,7 @@ static hipError_t march_codec_b(int method, Params P, uint32_t nslots, hipStream
     // template table (if staged) at the front of the request, then the error
     // scratch (B floats per thread); VR_WG_PER_CU caps
     const size_t need = (((((size_t)P.tpl_lds + 15) & ~(size_t)15) + (size_t)B * 256u * 4u + 31) &
-                         ~(size_t)31) + (method == 6 ? 65 * sizeof(LogEnt) : 0);
+                         ~(size_t)31) + (method == 6 ? kLogTabN * sizeof(LogEnt) : 0);
     const size_t lds = cap_lds(P, P.wg_per_cu, need);
     const bool tl = P.tpl_lds != 0;
     if constexpr (B == 8 && !COUNT) {

@@ -254,6 +254,9 @@ __device__ __forceinline__ uint32_t pack_rgba(float r, float g, float b, float a
 // and each of the three divisors below (~16 cycles instead of ~58 for the
 // full IEEE double-division sequence on gfx950).
 __device__ __forceinline__ double div_const(double m, double D, double R) {
+#ifdef VR_ABLATE_DIV  // timing ablation builds only (tools/build_variants.sh): NOT exact
+    return m * R;
+#endif
     const double q0 = m * R;
     const double e = __builtin_fma(-q0, D, m);
     const double q = __builtin_fma(e, R, q0);
@@ -261,7 +264,6 @@ __device__ __forceinline__ double div_const(double m, double D, double R) {
 }
 constexpr double kMeanD = 0.0217, kMeanR = 1.0 / 0.0217;          // K:758
 constexpr double kVarD = 0.000021, kVarR = 1.0 / 0.000021;        // K:759
-constexpr double kLn2R = 1.0 / VR_LN2_D;                          // K:766
 
 // (float)((double)m / D) for a float m when only the float rounding is kept:
 // the reciprocal multiply (float)((double)m * (1/D)) is bit-identical for
@@ -363,40 +365,50 @@ __device__ __forceinline__ float raw_variance(const float (&p)[B], float mean) {
 // inputs evaluate the double log.  Exhaustively equal to (float)log((double)x)
 // over all positive floats (vr_selftest_logf, tests/test_gpu_parity.py).
 //
-// Reduction (vr_logtab.h, tools/gen_logtab.py): x = m 2^e, m in [1, 2) (exact
-// frexpf), c = 1 + i/64 the nearest of 65 centres, d = m - c exact (Sterbenz),
-// r = d / c in double (|r| <= 2^-7), log x = e ln2 + log c + log1p r with log c
-// and ln 2 as double-doubles and log1p r = r + r^2 (-1/2 + r/3 - ... + r^5/7)
-// (truncation < r^8/8, 2^-52 relative to r).  The two largest terms add
-// exactly where they cancel (x near 1: c = 1, log c = 0; x just below 1:
-// i = 64, e = -1, log c = ln 2 split like e ln 2).  No f64 division; the
-// midpoint test reads y's low 29 mantissa bits (a float's half-ulp pattern is
-// 1 << 28 there whatever y's binade), instead of float/ldexp arithmetic.
+// Reduction (vr_logtab.h, tools/gen_logtab.py): x = m 2^e with m in [0.75,
+// 1.5) (exact frexpf, one doubling), c = 0.75 + i/256 the nearest of 193
+// centres -- m + 1.5 * 2^15 rounds m to a multiple of 2^-8 (the ulp there), so
+// c = (m + K) - K exactly and i is read off the sum's bits, no conversions --
+// d = m - c exact (Sterbenz), r = d / c as d * RN(1/c) in double (|r| <=
+// 2^-8.58), log x = e ln2 + log c + log1p r with log1p r = r + r^2 (-1/2 +
+// r/3 - r^2/4 + r^3/5) (truncation < r^6/6: <= 2^-45.5 relative to the
+// result, whose smallest values |log x| >= 2^-9 away from c = 1 have |r| <=
+// 2^-9).  x near 1 has e = 0 and c = 1, so e ln2 + log c never cancels: plain
+// double arithmetic, one fma and one add for the sum (round 6: the 65-centre
+// form on m in [1, 2) needed degree 7 and a double-double sum -- 1024^3 x 8
+// C0 entropy 3.52 ms, of which the exact logarithm took 1.53 ms by ablation,
+// profiles/r06/logtab/).  The midpoint test reads y's low 29 mantissa bits (a
+// float's half-ulp pattern is 1 << 28 there whatever y's binade): more than
+// 512 double ulps (~2^-43 |y|) from a midpoint, the float rounding of y is
+// that of the exact logarithm.  Infinities and NaN leave the fast form.
 __device__ __forceinline__ bool logf_fast_tabp(float x, float &r, const LogEnt *tab) {
+    constexpr float kRound = 49152.0f;         // 1.5 * 2^15: ulp 2^-8
     int e;
     float m = frexpf(x, &e);                   // x = m 2^e, m in [0.5, 1), also subnormal x
-    m = m * 2.0f;                              // [1, 2), exact
-    e -= 1;
-    const int i = (int)((m - 1.0f) * 64.0f + 0.5f);   // 0 .. 64
-    const float c = i == 64 ? 2.0f : 1.0f + (float)i * 0x1p-6f;
-    const float d = m - c;                     // exact, |d| <= 1/128
+    if (m < 0.75f) {
+        m = m * 2.0f;                          // [1, 1.5), exact
+        e -= 1;
+    }
+    const float s = m + kRound;                // m rounded to 2^-8 (+ kRound)
+    const float c = s - kRound;                // exact: 0.75 + i/256
+    const float d = m - c;                     // exact, |d| <= 1/512
+    // i = 256 c - 192 = bits(s) - bits(kRound) - 192 (one ulp of s per 2^-8)
+    // (clamped: an infinite or NaN x, which leaves the fast form, must not
+    // index past the table)
+    const uint32_t i = min(__float_as_uint(s) - (__float_as_uint(kRound) + 192u), 192u);
     const LogEnt t = tab[i];
     const double rr = (double)d * t.inv;
-    double q = 1.0 / 7.0;
-    q = fma(q, rr, -1.0 / 6.0);
-    q = fma(q, rr, 1.0 / 5.0);
+    double q = 1.0 / 5.0;
     q = fma(q, rr, -1.0 / 4.0);
     q = fma(q, rr, 1.0 / 3.0);
     q = fma(q, rr, -0.5);
     const double p = fma(rr * rr, q, rr);      // log1p(rr)
-    const double de = (double)e;
-    const double a = fma(de, kLn2Hi, t.hi);    // e ln2_hi exact; exact where it cancels
-    const double b = fma(de, kLn2Lo, t.lo) + p;
-    const double y = a + b;
+    const double y = fma((double)e, kLn2, t.hi) + p;
     r = (float)y;
-    const uint64_t lo29 = (uint64_t)__double_as_longlong(y) & 0x1FFFFFFFull;
-    const uint64_t dist = lo29 > 0x10000000ull ? lo29 - 0x10000000ull : 0x10000000ull - lo29;
-    return dist > 512u;                        // > 2^-44 |y| from a midpoint
+    // |lo29 - 2^28| > 512 in 32-bit unsigned arithmetic: one sub, one compare
+    const uint32_t lo29 = __double2loint(y) & 0x1FFFFFFFu;
+    return __float_as_uint(x) < 0x7F800000u &&                  // finite (x > 0 here)
+           lo29 - (0x10000000u - 512u) > 1024u;                 // > ~2^-43 |y| from a midpoint
 }
 
 // the table in constant memory / a copy in the kernel's LDS (copy_logtab)
@@ -404,10 +416,10 @@ __device__ __forceinline__ bool logf_fast_tab(float x, float &r) {
     return logf_fast_tabp(x, r, kLogTab);
 }
 
-// Copies the log table into LDS (65 x 32 bytes); the workgroup must then
-// __syncthreads() before the first use.
+// Copies the log table into LDS (kLogTabN x 16 bytes); the workgroup must
+// then __syncthreads() before the first use.
 __device__ __forceinline__ void copy_logtab(LogEnt *dst) {
-    if (threadIdx.x < 65) dst[threadIdx.x] = kLogTab[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLogTabN; i += blockDim.x) dst[i] = kLogTab[i];
 }
 
 // The round-1 form: atanh series of (m - 1)/(m + 1), one f64 division, no
@@ -454,10 +466,24 @@ __device__ __forceinline__ float logf_canon(float x) {
 }
 
 __device__ __forceinline__ float logf_canon_p(float x, const LogEnt *tab) {
-    float r;
-    if (x == 1.0f) return 0.0f;
+#ifdef VR_ABLATE_LOG  // timing ablation builds only (tools/build_variants.sh): NOT exact
+    return __logf(x);
+#endif
+    float r;  // x = 1 takes the fast form: i = 64, c = 1, d = 0, y = +0
     if (logf_fast_tabp(x, r, tab)) return r;
     return (float)log((double)x);
+}
+
+// The entropy's (double)logf(p) / log(2.0) (K:766) for a float's log m:
+// 1 / RN(ln 2) split as Rh (29 significant bits: m * Rh exact for a float m)
+// + Rl, and fma(m, Rl, m * Rh) -- one rounding of m (Rh + Rl) -- equals the
+// correctly rounded quotient for every float m, zeros, infinities and NaN
+// included (tests/c/divcheck.c): two f64 ops, no selects (the Markstein form
+// took a multiply, two fmas and an infinity select)
+constexpr double kLn2RecHi = 0x1.7154765p+0, kLn2RecLo = 0x1.5c17f278eff00p-31;
+__device__ __forceinline__ double div_ln2(float m) {
+    const double md = (double)m;
+    return __builtin_fma(md, kLn2RecLo, md * kLn2RecHi);
 }
 
 // K:761-769 with the log table at `tab` (an LDS copy)
@@ -467,8 +493,7 @@ __device__ __forceinline__ float entropy_p(const float (&p)[B], float enorm, con
 #pragma unroll
     for (int i = 0; i < B; i++) {
         const float pr = p[i];
-        const double t =
-            pr <= 0 ? 0.0 : div_const((double)logf_canon_p(pr, tab), VR_LN2_D, kLn2R);
+        const double t = pr <= 0 ? 0.0 : div_ln2(logf_canon_p(pr, tab));
         ent = (float)((double)ent + (double)pr * t);
     }
     ent = -ent;
@@ -482,8 +507,7 @@ __device__ __forceinline__ float entropy(const float (&p)[B], float enorm) {
 #pragma unroll
     for (int i = 0; i < B; i++) {
         const float pr = p[i];
-        const double t =
-            pr <= 0 ? 0.0 : div_const((double)logf_canon<TAB>(pr), VR_LN2_D, kLn2R);
+        const double t = pr <= 0 ? 0.0 : div_ln2(logf_canon<TAB>(pr));
         ent = (float)((double)ent + (double)pr * t);
     }
     ent = -ent;
@@ -633,7 +657,7 @@ __device__ __forceinline__ float record_stat_rt(const float *__restrict__ p, int
         for (int i = 0; i < nb; i++) {
             const float pr = p[i];
             const double t =
-                pr <= 0 ? 0.0 : div_const((double)logf_canon(pr), VR_LN2_D, kLn2R);
+                pr <= 0 ? 0.0 : div_ln2(logf_canon(pr));
             ent = (float)((double)ent + (double)pr * t);
         }
         ent = -ent;

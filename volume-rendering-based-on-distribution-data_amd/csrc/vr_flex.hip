@@ -176,7 +176,7 @@ __global__ __launch_bounds__(64) void k_flex_blocks(int nb, const float *__restr
         float ent = 0.0f;
         for (int i = 0; i < nb; i++) {
             const float pr = h[i];
-            const double t = pr <= 0 ? 0.0 : div_const((double)logf_canon(pr), VR_LN2_D, kLn2R);
+            const double t = pr <= 0 ? 0.0 : div_ln2(logf_canon(pr));
             ent = (float)((double)ent + (double)pr * t);
         }
         ent = -ent;

@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_MARCH_MI
         __syncthreads();
         tab = t;
         // this wave's bin-major record column (entropy_stash) behind the table
-        st = lds + 4u * (uint32_t)P.box_max + 65u * (sizeof(LogEnt) / 4u) + (threadIdx.x >> 6) * 64u * B;
+        st = lds + 4u * (uint32_t)P.box_max + (uint32_t)kLogTabN * (sizeof(LogEnt) / 4u) + (threadIdx.x >> 6) * 64u * B;
     }
     const uint32_t lane = threadIdx.x & 63u;
     float *box = lds + (threadIdx.x >> 6) * (uint32_t)P.box_max;
@@ -1055,7 +1055,7 @@ __device__ __forceinline__ int march_wq_tile(const float *__restrict__ vol, cons
 
 template <int B, int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_WIDE_MINW, M == 3 && B >= 32 ? 8 : VR_WIDE_WAVES))) void k_march_wq(const float *__restrict__ vol, Params P) {
-    __shared__ LogEnt s_lt[M == 3 ? 65 : 1];  // entropy: the exact-log table (copy_logtab)
+    __shared__ LogEnt s_lt[M == 3 ? kLogTabN : 1];  // entropy: the exact-log table (copy_logtab)
     // entropy: each wave's bin-major record columns (entropy_stash)
     __shared__ float s_col[M == 3 && B >= 32 ? 4 * 64 * B : 1];
     if constexpr (M == 3) {
@@ -1429,7 +1429,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
     // caps the workgroups resident per CU (160 KiB of LDS per CU)
     // (+ the log table and the record columns of the wide entropy march, k_march)
     const size_t lds = cap_lds(P, P.wg_per_cu, B > 0 ? (size_t)P.box_max * 4u * sizeof(float) +
-                                                   (B >= 8 && method == 3 ? 65 * sizeof(LogEnt) + 4u * 64u * B * sizeof(float) : 0) : 0);
+                                                   (B >= 8 && method == 3 ? kLogTabN * sizeof(LogEnt) + 4u * 64u * B * sizeof(float) : 0) : 0);
     if constexpr (!COUNT && B > 0 && B <= 8) {
         if (P.path == 7) {
             hipError_t err = hipSuccess;
@@ -1449,7 +1449,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             const int qcap = P.wg_per_cu > 0 ? P.wg_per_cu
                              : (P.tile_list && (uint64_t)nslots * 256u <= 400000u) ? 1 : 2;
             // entropy: the log table (qc_group) at the front
-            const size_t qlds = cap_lds(P, qcap, method == 3 ? 65 * sizeof(LogEnt) : 0);
+            const size_t qlds = cap_lds(P, qcap, method == 3 ? kLogTabN * sizeof(LogEnt) : 0);
             if (P.quad2) {  // two lanes per ray, two workgroups per tile
                 note_kernel(P.bvol ? "k_march_quad2_brick" : "k_march_quad2", B, method);
                 const dim3 grid2(((nslots + 7u) / 8u) * 16u);
@@ -1492,7 +1492,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             switch (method) {
             case 1: hipLaunchKernelGGL((k_march_ws<B, 1>), grid, block, 0, s, vol, P); break;
             case 2: hipLaunchKernelGGL((k_march_ws<B, 2>), grid, block, 0, s, vol, P); break;
-            case 3: hipLaunchKernelGGL((k_march_ws<B, 3>), grid, block, 65 * sizeof(LogEnt), s, vol, P); break;
+            case 3: hipLaunchKernelGGL((k_march_ws<B, 3>), grid, block, kLogTabN * sizeof(LogEnt), s, vol, P); break;
             }
             return hipGetLastError();
         }
@@ -1562,7 +1562,7 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             // an occupancy cap's LDS request leaves room for the kernel's static LDS
             // (the entropy march's log table and record columns)
             const size_t wl = cap_lds(P, P.wg_per_cu, 0,
-                                      method == 3 ? 65 * sizeof(LogEnt) + (B >= 32 ? 4 * 64 * B * sizeof(float) : 4) : 64);
+                                      method == 3 ? kLogTabN * sizeof(LogEnt) + (B >= 32 ? 4 * 64 * B * sizeof(float) : 4) : 64);
             int kind = (B == 16 && !P.oblique && method != 3) ? 1 : 2;
             if (const char *ew = tuning("VR_WIDE")) {
                 const int v = std::atoi(ew);

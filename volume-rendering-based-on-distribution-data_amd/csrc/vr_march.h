@@ -326,7 +326,7 @@ __device__ __forceinline__ float entropy_col(const float (&p)[B], float *col, fl
     for (int i = 0; i < B; i++) {
         const float pr = col[i * STRIDE];  // written by this lane: program order suffices
         const double t =
-            pr <= 0 ? 0.0 : div_const((double)logf_canon_p(pr, tab), VR_LN2_D, kLn2R);
+            pr <= 0 ? 0.0 : div_ln2(logf_canon_p(pr, tab));
         ent = (float)((double)ent + (double)pr * t);
     }
     ent = -ent;
@@ -339,10 +339,10 @@ __device__ __forceinline__ float entropy_stash(const float (&p)[B], float *st, u
     return entropy_col<B, 64>(p, st + lane, enorm, tab);
 }
 
-// an entropy march's LDS: the log table (65 entries) + 4 waves' record columns
+// an entropy march's LDS: the log table (kLogTabN entries) + 4 waves' record columns
 template <int B>
 struct EntropyLds {
-    LogEnt tab[65];
+    LogEnt tab[kLogTabN];
     float col[4 * 64 * B];
 };
 

@@ -39,7 +39,7 @@ template <int B>
 __global__ __launch_bounds__(256) void k_bake_raw(const float *__restrict__ vol, Params P,
                                                   float *__restrict__ out, uint64_t plane,
                                                   uint64_t psy, uint64_t psz) {
-    __shared__ LogEnt tab[65];
+    __shared__ LogEnt tab[kLogTabN];
     copy_logtab(tab);
     __syncthreads();
     const uint32_t x = blockIdx.x * 256u + threadIdx.x;
