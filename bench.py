@@ -1216,8 +1216,9 @@ def main():
     # ~50 ms of saturating reads before the warm-up frames, so those start on the
     # clocks of a loaded GPU (the frame time settles over the first ~50 ms of work,
     # DESIGN.md section 6)
+    # (a codec volume, methods 4/5/6, has no record volume to stream: none)
     ceiling = None
-    if world == 1:
+    if world == 1 and args.method not in (4, 5, 6):
         rb, rms, rmean = pkg.stream_read(8)
         ceiling = {"kernel": "k_stream_read", "bytes": rb, "ms": round(rms, 4),
                    "mean_ms": round(rmean, 4), "GBps": round(rb / (rms * 1e-3) / 1e9, 1),

@@ -486,15 +486,56 @@ __device__ __forceinline__ double div_ln2(float m) {
     return __builtin_fma(md, kLn2RecLo, md * kLn2RecHi);
 }
 
+// The entropy terms t = (double)logf(p) / log(2.0) of N bins (K:766; 0 for
+// p <= 0, whose bins the reference skips).  The N fast logarithms run without
+// a branch -- independent f64 chains the scheduler interleaves -- and the rare
+// double-log fallbacks share one branch (a branch per bin around each log
+// serialised the chains).  N = 4 (1024^3 x 8 entropy, one process, against
+// the branch per bin: C0 2.78 -> 2.63 ms, C1 6.35 -> 5.88; N = 2 2.74 / 5.96,
+// N = 8 3.00 / 5.87: registers; profiles/r06/logtab/r6w_*.log).
+// A zero or negative p gives a bounded table index and its value is
+// discarded by the select; NaN takes the fallback.
+#ifndef VR_ENT_CHUNK
+#define VR_ENT_CHUNK 4
+#endif
+constexpr int kEntChunk = VR_ENT_CHUNK;
+template <int N>
+__device__ __forceinline__ void ent_terms(const float (&p)[N], const LogEnt *tab, double (&t)[N]) {
+    float l[N];
+#ifdef VR_ABLATE_LOG  // timing ablation builds only (tools/build_variants.sh): NOT exact
+#pragma unroll
+    for (int k = 0; k < N; k++) l[k] = __logf(p[k]);
+#else
+    bool all = true, f[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        f[k] = logf_fast_tabp(p[k], l[k], tab);
+        all = all && f[k];
+    }
+    if (!all) {
+#pragma unroll
+        for (int k = 0; k < N; k++)
+            if (!f[k] && !(p[k] <= 0)) l[k] = (float)log((double)p[k]);
+    }
+#endif
+#pragma unroll
+    for (int k = 0; k < N; k++) t[k] = p[k] <= 0 ? 0.0 : div_ln2(l[k]);
+}
+
 // K:761-769 with the log table at `tab` (an LDS copy)
 template <int B>
 __device__ __forceinline__ float entropy_p(const float (&p)[B], float enorm, const LogEnt *tab) {
+    constexpr int N = B < kEntChunk ? B : kEntChunk;
     float ent = 0.0f;
 #pragma unroll
-    for (int i = 0; i < B; i++) {
-        const float pr = p[i];
-        const double t = pr <= 0 ? 0.0 : div_ln2(logf_canon_p(pr, tab));
-        ent = (float)((double)ent + (double)pr * t);
+    for (int i = 0; i < B; i += N) {
+        float q[N];
+        double t[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) q[k] = p[i + k];
+        ent_terms<N>(q, tab, t);
+#pragma unroll
+        for (int k = 0; k < N; k++) ent = (float)((double)ent + (double)q[k] * t[k]);
     }
     ent = -ent;
     return ent / enorm;

@@ -321,13 +321,17 @@ __device__ __forceinline__ float entropy_col(const float (&p)[B], float *col, fl
                                              const LogEnt *tab) {
 #pragma unroll
     for (int i = 0; i < B; i++) col[i * STRIDE] = p[i];
+    constexpr int N = B < kEntChunk ? B : kEntChunk;
     float ent = 0.0f;
-#pragma unroll 2
-    for (int i = 0; i < B; i++) {
-        const float pr = col[i * STRIDE];  // written by this lane: program order suffices
-        const double t =
-            pr <= 0 ? 0.0 : div_ln2(logf_canon_p(pr, tab));
-        ent = (float)((double)ent + (double)pr * t);
+#pragma unroll 1
+    for (int i = 0; i < B; i += N) {  // N bins per iteration (ent_terms)
+        float q[N];
+        double t[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) q[k] = col[(i + k) * STRIDE];  // this lane's writes
+        ent_terms<N>(q, tab, t);
+#pragma unroll
+        for (int k = 0; k < N; k++) ent = (float)((double)ent + (double)q[k] * t[k]);
     }
     ent = -ent;
     return ent / enorm;
