@@ -84,8 +84,7 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
         for L in libs.values():
             assert L.vr_bake_stats() == 0, L.vr_last_error()
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-    cams = {"C0": pkg.camera.single_test_inv_view(),
-            "C1": pkg.camera.display_inv_view((30.0, 45.0))}
+    cams = {c: bench.camera_matrix(pkg, c) for c in ("C0", "C1", "S")}
     descs = {c: pkg.make_desc(out, W, H, cams[c], query_method=args.method,
                               volume_size=(n, n, n)) for c in args.cameras.split(",")}
     envs = []

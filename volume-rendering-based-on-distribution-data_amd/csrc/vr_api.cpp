@@ -635,14 +635,21 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // pipelined march (ensure_axis_copy); for the choices below
     // they count as row-aligned (their x-row seg / quad alternatives read the
     // x rows across).  VR_ZROWS=0 keeps them oblique.
+    // 8-bin entropy of such views takes the LDS-box march on the x rows instead:
+    // the pipelined march decodes all 8 corners' 64 logarithms per step
+    // unrolled and spills (1024^3 x 8 side view S m3: 18.8 ms; box 3.38, quad
+    // 5.55, wave-staged 5.12; profiles/r06/knobs/side_m3.log)
+    const bool axis_dir = std::fabs(d->inv_view[8]) >= 0.95f || std::fabs(d->inv_view[4]) >= 0.95f;
+    const bool axis_m3 = !along_rows && axis_dir && d->query_method == 3 && g.nb == 8;
     const char *ez = vr::tuning("VR_ZROWS");
     P.axis_view = 0;
     if (!along_rows && !codec && !flex && g.owned && d->query_method >= 1 &&
         d->query_method <= 3 && (g.nb == 1 || g.nb == 2 || g.nb == 4 || g.nb == 8) &&
-        !(ez && std::atoi(ez) == 0))
+        !axis_m3 && !(ez && std::atoi(ez) == 0))
         P.axis_view = std::fabs(d->inv_view[8]) >= 0.95f ? 2 : std::fabs(d->inv_view[4]) >= 0.95f ? 1 : 0;
     const bool row_like = along_rows || P.axis_view != 0;
     if (P.axis_view) P.path = 2;
+    if (axis_m3 && !codec && !flex) P.path = 1;
     // Launches of few rays (a rank's tile list at 4 or 8 GPUs, 1080p) are bound
     // by the per-ray step chain, not by HBM: there the pipelined ray-segmented
     // march (2 lanes per ray, next window gathered before this one decodes,
