@@ -85,6 +85,7 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
             assert L.vr_bake_stats() == 0, L.vr_last_error()
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     cams = {c: bench.camera_matrix(pkg, c) for c in ("C0", "C1", "S")}
+    cams["T"] = pkg.camera.display_inv_view((90.0, 90.0))  # top view: screen x along y
     descs = {c: pkg.make_desc(out, W, H, cams[c], query_method=args.method,
                               volume_size=(n, n, n)) for c in args.cameras.split(",")}
     envs = []

@@ -694,10 +694,16 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // (k_march_duo): 512^3 x 8 C0 m1 0.694 -> 0.623 ms, m2 0.571 -> 0.496; three
     // or four per box 0.655 / 0.707; at 1024^3 (VR_PATH=1) the doubled boxes lose,
     // 1.69 -> 2.26 (profiles/r04/variants_*_duo_r4l.log)
-    if (along_rows && !d->d_tile_list && (g.nb == 8 || g.nb == 16 || g.nb == 32) &&
-        (d->query_method == 1 || d->query_method == 2 || wide3) &&
+    // Side and top views of such a coarse volume too, on the x rows without the
+    // axis copy (the face across the view is then y-z or x-z): 512^3 x 8 1080p
+    // side view m1 1.14 -> 0.74 ms, m2 1.13 -> 0.55; top view m1 1.08 -> 0.75,
+    // m2 1.09 -> 0.54 (profiles/r06/knobs/side_512x8_m*.log)
+    const uint64_t face = P.axis_view == 2 ? (uint64_t)g.ny * g.nz
+                          : P.axis_view == 1 ? (uint64_t)g.nx * g.nz : (uint64_t)g.nx * g.ny;
+    if (row_like && !d->d_tile_list && (g.nb == 8 || g.nb == 16 || g.nb == 32) &&
+        (d->query_method == 1 || d->query_method == 2 || (wide3 && along_rows)) &&
         (uint64_t)d->width * d->height > seg_rays &&
-        (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny) {
+        (uint64_t)d->width * d->height >= 4ull * face) {
         P.path = 1;
         P.duo = 2;
     }
