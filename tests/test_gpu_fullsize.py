@@ -224,11 +224,12 @@ def test_render_kernel_grid_covers_the_frame(pkg, orc, gpu):
     assert TOL == 1e-4
 
 
-@pytest.mark.parametrize("cam", ["C0", "C1"])
+@pytest.mark.parametrize("cam", ["C0", "C1", "S"])
 def test_wide_entropy_at_size(pkg, orc, gpu, cam):
     """32-bin records (the reference's width, C:86-87) at 1080p, entropy (method 3):
-    the LDS-box march (C0) and the quad march (C1) with the rolled per-bin sums
-    over LDS record columns (round 4), every 8th row against the oracle"""
+    the LDS-box march with the rolled per-bin sums over LDS record columns (round
+    4) -- row-aligned, and since round 6 the oblique and side views of this coarse
+    volume too -- every 8th row against the oracle"""
     import torch
     n, nb, W, H = 512, 32, 1920, 1080
     _scene.vol = None
@@ -239,7 +240,7 @@ def test_wide_entropy_at_size(pkg, orc, gpu, cam):
     try:
         m = camera(pkg, cam)
         got = render_frames(pkg, torch, W, H, m, 3, n_frames=1)[0]
-        want = "k_march<B=32,M=3>" if cam == "C0" else "k_march_wq<B=32,M=3>"
+        want = "k_march<B=32,M=3>"
         assert got[3] == want, got[3]
         ref = orc.render(vol, orc.make_params(W, H, m, query_method=3), row_stride=8)[:3]
         rows = slice(0, None, 8)

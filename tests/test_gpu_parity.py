@@ -78,7 +78,8 @@ def test_wide_records_take_batched_march(pkg, orc, gpu, nb, cam, wide, tune):
     cooperative march (k_march_wq; the lane-per-record k_march_wide for row-aligned
     16-bin views; VR_WIDE=1 / 2 force either), full
     frames and packed tile lists bit-identical to the oracle; VR_PATH=1 keeps the
-    LDS-box march; entropy always takes the quad march"""
+    LDS-box march; entropy takes the quad march (the LDS-box march for oblique
+    views of a coarse volume)"""
     import torch
     tune.set("VR_WIDE", wide)
     kind = wide or ("1" if nb == 16 and cam == "C0" else "2")
@@ -110,7 +111,9 @@ def test_wide_records_take_batched_march(pkg, orc, gpu, nb, cam, wide, tune):
     got = gpu_render(pkg, None, W, H, m, 3, torch)
     assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=3))[:3],
                   f"{nb} bins {cam} m3")
-    assert pkg.last_kernel().startswith("k_march_wq<"), pkg.last_kernel()
+    # (oblique entropy of this coarse volume: the LDS-box march, round 6)
+    want3 = "k_march<" if cam == "C1" else "k_march_wq<"
+    assert pkg.last_kernel().startswith(want3), pkg.last_kernel()
     # method 7: quad-cooperative corner refreshes, method-7 grid = volume or not
     for grid in ((21, 18, 15), (10, 12, 20)):
         got = gpu_render(pkg, None, W, H, m, 7, torch, m7=grid)
@@ -238,7 +241,41 @@ def test_wide_coarse_rows_take_box_march(pkg, orc, gpu, nb, tune):
             got = gpu_render(pkg, None, 96, 64, m, method, torch)
             ref = orc.render(vol, orc.make_params(96, 64, m, query_method=method))[:3]
             assert_parity(got, ref, f"coarse {nb} bins m{method}")
-            assert pkg.last_kernel().startswith(kern), pkg.last_kernel()
+            # (oblique entropy too takes the box, round 6)
+            want = "k_march<" if method == 3 else kern
+            assert pkg.last_kernel().startswith(want), pkg.last_kernel()
+
+
+@pytest.mark.parametrize("nb", [16, 32])
+def test_wide_axis_views_take_box_march(pkg, orc, gpu, nb):
+    """16 / 32 bins, views along the volume's z or y (side / top, no axis copy for
+    B > 8): full frames take the LDS-box march on the x rows (round 6), methods
+    1/2/3, bit-identical; rank tile lists keep the quad-cooperative march"""
+    import torch
+    vol = orc.synth_volume(22, 19, 17, nb)
+    pkg.init_distribution(vol)
+    W, H = 72, 56
+    for rot in ((0.0, 90.0), (90.0, 90.0), (-10.0, -80.0)):
+        m = pkg.camera.display_inv_view(rot)
+        for method in (1, 2, 3):
+            got = gpu_render(pkg, None, W, H, m, method, torch)
+            ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
+            assert_parity(got, ref, f"wide axis view {rot} {nb} bins m{method}")
+            assert pkg.last_kernel().startswith("k_march<"), (rot, pkg.last_kernel())
+    lists = pkg.tiles.tile_lists(W, H, 3, m)
+    n_slots = lists.shape[1]
+    dl = torch.from_numpy(lists.view(np.int32).copy()).cuda()
+    packed = torch.full((3, n_slots * 256), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    for r in range(3):
+        pkg.render(pkg.make_desc(packed[r], W, H, m, query_method=1, d_tile_list=dl[r],
+                                 n_tiles=n_slots))
+        assert not pkg.last_kernel().startswith("k_march<"), pkg.last_kernel()
+    frame = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    pkg.unscatter_tiles(packed, dl, 3, n_slots, frame, W, H)
+    torch.cuda.synchronize()
+    ref8 = orc.render(vol, orc.make_params(W, H, m, query_method=1), want_float=False,
+                      want_steps=False)[0]
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32).reshape(H, W), ref8)
 
 
 def test_edge_images(pkg, orc, gpu):
@@ -973,9 +1010,9 @@ def test_small_frames_take_segmented_march(pkg, orc, gpu, dims, nb, W, H, want):
 def test_midsize_rows_take_box_march_with_four_samples(pkg, orc, gpu, nb, want):
     """row-aligned full frames between 128 K and 700 K rays of a volume with >= 4
     pixels per voxel face (BASELINE config 2's shape): 4 and 8 bins, methods 1/2, on
-    k_march_duo with four samples per box, 2 bins on the one-lane march; entropy on
-    k_march (the 2-bin frame too, round 4's small-frame entropy rule); rays ending on
-    any sample of a box; bit-identical"""
+    k_march_duo with four samples per box, 2 bins on the one-lane march; 8-bin
+    entropy on k_march, 2- and 4-bin entropy on the one-lane march (round 6); rays
+    ending on any sample of a box; bit-identical"""
     import torch
     vol = orc.synth_volume(44, 38, 30, nb)
     pkg.init_distribution(vol)
@@ -985,7 +1022,9 @@ def test_midsize_rows_take_box_march_with_four_samples(pkg, orc, gpu, nb, want):
         got = gpu_render(pkg, None, W, H, m, method, torch, density=density)
         ref = orc.render(vol, orc.make_params(W, H, m, query_method=method, density=density))[:3]
         assert_parity(got, ref, f"nb={nb} m{method} d={density}")
-        k = want if method != 3 else "k_march<"  # entropy: the one-sample box
+        # entropy: the one-sample box (8 bins); 2 and 4 bins the one-lane pipelined
+        # march (round 6)
+        k = want if method != 3 else "k_march<" if nb == 8 else "k_march_pipe<"
         assert pkg.last_kernel().startswith(k), (method, pkg.last_kernel())
 
 
@@ -993,14 +1032,19 @@ def test_midsize_rows_take_box_march_with_four_samples(pkg, orc, gpu, nb, want):
 def test_small_frame_entropy_dispatch(pkg, orc, gpu, nb):
     """entropy of small and mid-size full frames with 1-4 bins (round 4): 2-lane
     windows for frames up to 128 K rays and for oblique frames up to 700 K, the LDS
-    box for row-aligned frames of a coarse volume above 128 K rays; bit-identical,
-    dense and sparse (early exit) transfer"""
+    box for row-aligned frames of a coarse volume above 128 K rays; 2 and 4 bins
+    on the one-lane pipelined march (round 6); bit-identical, dense and sparse
+    (early exit) transfer"""
     import torch
     vol = orc.synth_volume(36, 30, 28, nb)
     pkg.init_distribution(vol)
     rows, obl = pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))
-    for m, W, H, want in ((rows, 200, 150, "k_march_segp2<"), (obl, 200, 150, "k_march_segp2<"),
-                          (rows, 400, 360, "k_march<"), (obl, 400, 360, "k_march_segp2<")):
+    # round 6: 2 and 4 bins on the one-lane pipelined march
+    cases = ((rows, 200, 150, "k_march_segp2<"), (obl, 200, 150, "k_march_segp2<"),
+             (rows, 400, 360, "k_march<"), (obl, 400, 360, "k_march_segp2<"))
+    if nb != 1:
+        cases = tuple((m, W, H, "k_march_pipe<") for m, W, H, _ in cases)
+    for m, W, H, want in cases:
         for density in (0.05, 2.0):
             got = gpu_render(pkg, None, W, H, m, 3, torch, density=density)
             ref = orc.render(vol, orc.make_params(W, H, m, query_method=3, density=density))[:3]

@@ -63,6 +63,7 @@ def main():
                                      ctypes.POINTER(ctypes.c_int),
                                      ctypes.POINTER(ctypes.c_void_p)]
         L.vr_last_error.restype = ctypes.c_char_p
+        L.vr_last_kernel.restype = ctypes.c_char_p
         L.vr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         libs[name] = L
     torch.cuda.set_device(0)
@@ -97,6 +98,7 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
         envs.append(d)
     configs = list(itertools.product(libs.keys(), envs, descs.keys()))
     times = {i: [] for i in range(len(configs))}
+    kern = {}
     for rnd in range(args.rounds):
         for i, (name, env, cam) in enumerate(configs):
             L = libs[name]
@@ -121,6 +123,7 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
             assert L.vr_render(ctypes.byref(d)) == 0, L.vr_last_error()
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / args.reps)
+            kern[i] = L.vr_last_kernel().decode()
         print(f"round {rnd} done", file=sys.stderr, flush=True)
     for L in libs.values():
         L.vr_clear_tuning()
@@ -130,7 +133,7 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
         t = np.array(times[i])
         envs_s = ",".join(f"{k}={v}" for k, v in env.items()) or "-"
         print(f"{name:10s} {envs_s:34s} {cam}  median {np.median(t):7.3f} ms  min {t.min():7.3f}"
-              f"  ({W * H / np.median(t) / 1e3:8.1f} Mrays/s)")
+              f"  ({W * H / np.median(t) / 1e3:8.1f} Mrays/s)  {kern[i]}")
 
 
 if __name__ == "__main__":

@@ -613,7 +613,10 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // per-ray), 2 per-ray pipelined, 4 wave-staged rows, 7 ray-segmented
     // (VR_SEG lanes per ray).
     const bool along_rows = std::fabs(d->inv_view[0]) >= 0.95f;
-    P.path = along_rows ? (d->query_method == 3 ? 4 : 2) : 0;
+    // (entropy of 1-4 bins: the one-lane pipelined march, round 6 -- 1024^3 x 2
+    // 1080p C0 4.66 -> 3.25 ms, x 4 4.51 -> 4.35 against the wave-staged march;
+    // profiles/r06/knobs/m3_1024x*.log)
+    P.path = along_rows ? (d->query_method == 3 && g.nb >= 8 ? 4 : 2) : 0;
     // 8-bin entropy of row-aligned views: the LDS-box march with the rolled
     // LDS-column entropy (k_march<8,3>, 128 VGPRs) beats the wave-staged march:
     // 1024^3 C0 4.31 -> 3.52 ms, 512^3 3.10 -> 1.63 (round 4,
@@ -625,7 +628,11 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     // ... and of oblique views of a volume coarse for the frame (>= 4 pixels per
     // voxel of the x-y face): 512^3 C1 m3 8.32 -> 5.11 ms; at 1024^3 the quad
     // march stays ahead (8.42 vs 8.61; profiles/r04/variants_*_m3_r4g.log)
-    if (!along_rows && d->query_method == 3 && g.nb == 8 && !d->d_tile_list &&
+    // (16 and 32 bins too, round 6: 512^3 x 16 C1 m3 8.60 -> 5.56 ms, x 32 15.9 ->
+    // 10.3; at 1024^3 the quad march stays ahead, 9.05 vs 10.3 and 16.9 vs 19.1;
+    // profiles/r06/knobs/wide_*.log, m3_512x32.log)
+    if (!along_rows && d->query_method == 3 && (g.nb == 8 || g.nb == 16 || g.nb == 32) &&
+        !d->d_tile_list &&
         (uint64_t)d->width * d->height >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny)
         P.path = 1;
     P.oblique = along_rows ? 0 : 1;
@@ -650,6 +657,14 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
     const bool row_like = along_rows || P.axis_view != 0;
     if (P.axis_view) P.path = 2;
     if (axis_m3 && !codec && !flex) P.path = 1;
+    // Side and top views of 16- and 32-bin records (no axis copy: B <= 8 only)
+    // likewise take the LDS-box march on the x rows instead of the quad march:
+    // 1024^3 x 32 side view m1 13.7 -> 6.9 ms, m3 15.4 -> 7.6, top view m1 7.6 ->
+    // 7.0, m3 15.4 -> 7.5; 1024^3 x 16 side m1 6.7 -> 4.9, m3 8.6 -> 4.4; 512^3 x
+    // 16 side m1 3.7 -> 1.3, m3 8.2 -> 1.9 (profiles/r06/knobs/wide_*.log)
+    if (!along_rows && axis_dir && (g.nb == 16 || g.nb == 32) && !d->d_tile_list &&
+        d->query_method >= 1 && d->query_method <= 3 && !codec && !flex)
+        P.path = 1;
     // Launches of few rays (a rank's tile list at 4 or 8 GPUs, 1080p) are bound
     // by the per-ray step chain, not by HBM: there the pipelined ray-segmented
     // march (2 lanes per ray, next window gathered before this one decodes,
@@ -766,9 +781,16 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         // 128^3 x 1 at 256^2 C0 1.066 -> 0.481 ms, C1 0.988 -> 0.514; 256^3 x 4 at
         // 512^2 C0 1.600 -> 1.185 (box), C1 2.299 -> 1.707; 256^3 x 2 at 512^2 C0
         // 1.343 -> 0.783 (box), C1 1.113 -> 1.064 (profiles/r04/variants_midsize_m3_r4ag.log)
+        // Round 6, after the cheaper exact log: 2 and 4 bins take the one-lane
+        // pipelined march instead (256^3 x 4 at 512^2 C0 1.14 -> 0.99 ms, C1 1.66 ->
+        // 1.12; 384^3 x 4 at 768^2 C0 1.84 -> 1.54, C1 2.96 -> 1.65; 256^3 x 2 C0
+        // 0.76 -> 0.68, C1 1.04 -> 0.90); one bin keeps the 2-lane windows (128^3
+        // x 1 C0 0.47 vs 0.51, C1 0.50 vs 0.80; profiles/r06/knobs/m3_*.log)
         if (!d->d_tile_list && !codec && !flex && d->query_method == 3 && !P.axis_view &&
             (g.nb == 1 || g.nb == 2 || g.nb == 4) && rays <= seg_rays) {
-            if (along_rows && rays > 131072 && rays >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny) {
+            if (g.nb != 1) {
+                P.path = 2;
+            } else if (along_rows && rays > 131072 && rays >= 4ull * (uint64_t)g.nx * (uint64_t)g.ny) {
                 P.path = 1;
             } else {
                 P.path = 7;
