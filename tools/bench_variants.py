@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--cameras", default="C0,C1")
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--variants", default="")
+    ap.add_argument("--codec", action="store_true",
+                    help="synthesize a codec volume (methods 4/5/6; the in-tree build only)")
     ap.add_argument("--baked", action="store_true",
                     help="bake the statistics planes (basicDataProcessing) before timing")
     ap.add_argument("--pads", nargs="*", default=[""],
@@ -49,6 +51,8 @@ def main():
     paths = {"main": pkg.LIB_PATH}
     for p in sorted(glob.glob(os.path.join(ROOT, "tools/build/variants/*/libvr.so"))):
         paths[os.path.basename(os.path.dirname(p))] = p
+    if args.codec:
+        args.variants = "main"
     if args.variants:
         keep = set(args.variants.split(","))
         paths = {k: v for k, v in paths.items() if k in keep}
@@ -74,6 +78,9 @@ def main():
 def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
     first = next(iter(libs.values()))
     ext = pkg._lib.Extent(n, n, n)
+    if args.codec:  # the package's own library instance is "main"
+        pkg.synthesize_codec((n, n, n), nb, bench.CODEC_TEMPLATES, bench.CODEC_SLOTS, bench.SEED)
+        return run_timed(args, pkg, libs, pad, n, nb, W, H, torch, bench)
     first.vr_set_tuning(b"VR_PAD", pad.encode() if pad else None)
     assert first.vr_synthesize(ext, nb, bench.SEED) == 0
     first.vr_set_tuning(b"VR_PAD", None)
@@ -82,6 +89,13 @@ def run_pad(args, pkg, libs, pad, n, nb, W, H, torch, bench):
     for L in list(libs.values())[1:]:  # other variants adopt the same (dense) volume
         assert L.vr_init_distribution(ptr, ext, nb, 2) == 0
     if args.baked:
+        for L in libs.values():
+            assert L.vr_bake_stats() == 0, L.vr_last_error()
+    return run_timed(args, pkg, libs, pad, n, nb, W, H, torch, bench)
+
+
+def run_timed(args, pkg, libs, pad, n, nb, W, H, torch, bench):
+    if args.codec and args.baked:
         for L in libs.values():
             assert L.vr_bake_stats() == 0, L.vr_last_error()
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
