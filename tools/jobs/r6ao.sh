@@ -1,0 +1,13 @@
+# round 6: per-rank PMC traffic of the N-rank splits of the headline workload
+# (tools/rank_traffic.py), then the N = 2 bench line reading it
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
+O=gpurun_out/r6ao; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_bench.py -x -q --timeout 400 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+cp profiles/traffic.json $O/traffic.json
+for N in 2 4 8; do
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/rt$N/f -o f -- python tools/rank_traffic.py run --world $N > $O/rt${N}_run.json 2> $O/rt${N}_f.log || { echo "fetch pass N=$N failed"; tail -5 $O/rt${N}_f.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/rt$N/w -o w -- python tools/rank_traffic.py run --world $N > $O/rt${N}_run_w.json 2> $O/rt${N}_w.log || { echo "write pass N=$N failed"; tail -5 $O/rt${N}_w.log; exit 1; }
+  PMC_TAG=r6ao python tools/rank_traffic.py fold $O/traffic.json $O/rt${N}_run.json $O/rt$N/f $O/rt$N/w > $O/rt${N}_fold.log 2>&1 || { cat $O/rt${N}_fold.log; exit 1; }
+done
+timeout -k 10 900 python -u bench.py --gpus 2 --dist-backend gloo --no-cpu-baseline --traffic-json $O/traffic.json > $O/bench_n2_traffic.log 2>&1 || exit 1
+echo ok
