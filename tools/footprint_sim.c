@@ -13,7 +13,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifndef N
 #define N 1024
+#endif
 #define W 1920
 #define H 1080
 
