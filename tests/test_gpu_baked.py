@@ -94,6 +94,8 @@ def test_baked_render_parity(pkg, orc, gpu, baked, nb):
 @pytest.mark.parametrize("path,env", [
     ("1", {}), ("1", {"VR_BOX_MAX": "64"}), ("7", {"VR_SEG": "-2"}), ("7", {"VR_SEG": "4"}),
     ("7", {"VR_SEG": "-4"}), ("2", {"VR_WG_PER_CU": "2"}), ("7", {"VR_SEG": "2"}),
+    ("7", {"VR_SEG": "4", "VR_SEG_MAP": "1"}), ("7", {"VR_SEG": "-2", "VR_SEG_MAP": "1"}),
+    ("2", {"VR_SEG_MAP": "1"}),
 ])
 def test_baked_paths(pkg, orc, gpu, baked, path, env, tune):
     """every kernel a baked frame can take (VR_PATH 2 / 7; 1, the LDS-box march over x

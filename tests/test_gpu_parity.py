@@ -466,6 +466,9 @@ def test_errors_do_not_exit(pkg, gpu):
     # direct-path fallbacks
     ("1", {"VR_DUO": "2"}), ("1", {"VR_DUO": "2", "VR_BOX_MAX": "64"}),
     ("1", {"VR_DUO": "3"}), ("1", {"VR_DUO": "4", "VR_BOX_MAX": "64"}),
+    # a wave's rays as a compact pixel block (segmented and one-lane pipelined marches)
+    ("7", {"VR_SEG": "4", "VR_SEG_MAP": "1"}), ("7", {"VR_SEG": "-2", "VR_SEG_MAP": "1"}),
+    ("7", {"VR_SEG": "-4", "VR_SEG_MAP": "1"}), ("2", {"VR_SEG_MAP": "1"}),
 ])
 @pytest.mark.parametrize("nb", [4, 8])
 def test_every_kernel_path(pkg, orc, gpu, path, env, nb, tune):

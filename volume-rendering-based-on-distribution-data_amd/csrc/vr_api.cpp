@@ -827,6 +827,21 @@ int fill_params(const vr_render_desc *d, vr::Params &P, uint32_t &nslots,
         const int v = std::atoi(e);
         if (v == 2 || v == 4 || v == -2 || v == -4) P.seg_lanes = v;
     }
+    // A wave's rays as a compact pixel block (16 x 4 one lane per ray, (64 / S / 4)
+    // x 4 in S-lane windows) instead of a 64- or 64/S-pixel row: its loads touch
+    // fewer lines per instruction.  Measured per launch kind (tools/bench_variants.py,
+    // tools/rank_sim.py, profiles/r06/segmap/): small full frames on pipelined
+    // windows 128^3 x 1 at 256^2 m1 C0 0.075 -> 0.070 ms, C1 0.078 -> 0.077, m3 C0
+    // 0.490 -> 0.438 (C1 0.493 vs 0.501: kept as rows), 256^3 x 4 at 512^2 m1 C1
+    // 0.143 -> 0.137; row-aligned 2/4-bin entropy on the one-lane march 1024^3 x 2
+    // 1080p C0 3.23 -> 3.03, x 4 4.35 -> 4.16 (oblique: 256^3 x 4 C1 1.13 vs 1.22,
+    // kept as rows).  Also kept as rows: the 8-bin one-lane march (headline 1.342
+    // vs 1.352, side view 1.588 vs 1.628) and the rank lists of records (C0 N = 4
+    // 0.376 vs 0.386, N = 8 0.204 vs 0.219).  VR_SEG_MAP=0/1 overrides.
+    P.seg_map = (!d->d_tile_list && P.path == 7 && P.seg_lanes < 0 &&
+                 (along_rows || d->query_method != 3)) ||
+                (P.path == 2 && P.nb <= 4 && d->query_method == 3 && along_rows && !P.axis_view);
+    if (const char *e = vr::tuning("VR_SEG_MAP")) P.seg_map = std::atoi(e) != 0;
     // A rank's list at 8 GPUs (<= 400 K rays, 2-lane windows) is bound by the step
     // chains of its longest tiles: its first 64 slots -- the 8 longest tiles of
     // every XCD sublist -- take 4 lanes per ray in the same launch
@@ -885,6 +900,11 @@ int baked_path(const vr_render_desc *d, vr::Params &P) {
         else if (rays <= 700000) path = 7, seg = -2;
     }
     if (path == 7 && !vr::tuning("VR_SEG")) P.seg_lanes = seg;
+    // compact pixel blocks per wave (fill_params): baked frames gain everywhere
+    // but on row-aligned 4-lane windows (1024^3 x 8 1080p C1 0.844 -> 0.817 ms,
+    // C0 one-lane 0.310 -> 0.295; rank lists C1 N = 8 0.168 -> 0.153, C0 N = 4
+    // 0.133 -> 0.124, C0 N = 8 4-lane 0.093 vs 0.096; profiles/r06/segmap/)
+    P.seg_map = !(along_rows && path == 7 && P.seg_lanes > 0);
     // oblique full frames of a fine volume (< 4 pixels per voxel of the x-y
     // face): 4 workgroups per CU, fewer rays' lines in flight per L2 (1024^3
     // C1 1.28 -> 1.11 ms; 2-3 per CU 1.25, 6 1.19); coarse volumes (512^3:
@@ -892,6 +912,7 @@ int baked_path(const vr_render_desc *d, vr::Params &P) {
     if (!along_rows && !d->d_tile_list && P.wg_per_cu == 0 &&
         (uint64_t)d->width * d->height < 4ull * (uint64_t)P.nx * (uint64_t)P.ny)
         P.wg_per_cu = 4;
+    if (const char *e = vr::tuning("VR_SEG_MAP")) P.seg_map = std::atoi(e) != 0;
     if (const char *e = vr::tuning("VR_PATH")) {  // the LDS-box march (1) reads x rows only
         const int v = std::atoi(e);
         if (v == 2 || v == 7) path = v;

@@ -100,6 +100,7 @@ struct Params {
     int head_lanes;
     int head_tail;               // the rest of such a list: 0 seg_lanes windows, 1 one lane per ray (k_march_pipe_head)
     int plane_axis;              // baked frame on a plane's copy: 1 y rows, 2 z rows (gather8 MODE 4 / 5), 3 8x2x2 bricks (MODE 6)
+    int seg_map;                 // segmented / pipelined marches: 1 = a wave's rays as a compact pixel block (tuning)
     int duo;                     // LDS-box march (path 1, B <= 8, m1/m2/m3): samples per box (k_march_duo), 0/1 = k_march
     // tooling (vr_debug_box_check): 6 x u64, [0] violations, [1] worst overrun,
     // [2] out-of-volume box voxels, [3] decoded voxels, [4] lane slots, [5] spare

@@ -381,7 +381,12 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
                                                uint32_t slot, uint32_t tile, uint32_t tid,
                                                float *st = nullptr, const LogEnt *tab = nullptr) {
     uint32_t lx, ly;
-    tile_pixel(tid, lx, ly);
+    if (P.seg_map) {  // a wave takes a 16x4 pixel block
+        lx = (tid >> 6) * 16u + (tid & 15u);
+        ly = (tid >> 4) & 3u;
+    } else {
+        tile_pixel(tid, lx, ly);
+    }
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.CW || y >= P.CH) return -1;  // no cross-lane work in this kernel

@@ -78,8 +78,18 @@ __device__ __forceinline__ void march_seg_part(const float *__restrict__ vol, co
     // at the same step (adjacent records), as in the one-lane march
     constexpr uint32_t R = 64u / S;
     const uint32_t lane = threadIdx.x & 63u, rl = lane % R, k = lane / R;
-    const uint32_t p = part * RPW + (threadIdx.x >> 6) * R + rl;  // pixel inside the 64x4 tile
-    const uint32_t lx = p % kTileW, ly = p / kTileW;
+    uint32_t lx, ly;
+    if (P.seg_map) {
+        // a wave's R rays as an (R/4) x 4 pixel block, the workgroup's as a
+        // (RPW/4) x 4 column block of the tile: compact footprints per load
+        constexpr uint32_t BW = R / 4u;
+        lx = part * (RPW / 4u) + (threadIdx.x >> 6) * BW + rl % BW;
+        ly = rl / BW;
+    } else {
+        const uint32_t p = part * RPW + (threadIdx.x >> 6) * R + rl;  // pixel inside the 64x4 tile
+        lx = p % kTileW;
+        ly = p / kTileW;
+    }
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.CW || y >= P.CH) return;  // the whole group leaves
