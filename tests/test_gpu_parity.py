@@ -677,6 +677,21 @@ def test_codec_methods(pkg, orc, gpu, method, nb):
     assert pkg.last_kernel().startswith("k_march_codec")
 
 
+@pytest.mark.parametrize("nb", [4, 8, 32])
+def test_codec_block_map(pkg, orc, gpu, nb, tune):
+    """VR_CODEC_MAP=1: the one-lane codec march with a 16x4 pixel block per wave,
+    row-aligned and oblique views, methods 4/5/6, bit-identical"""
+    import torch
+    tune.set("VR_CODEC_MAP", "1")
+    cb, t, e = orc.synth_codec(22, 18, 14, nb, seed=nb + 11)
+    pkg.init_codec(cb, t, e)
+    for cam in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view()):
+        for method in (4, 5, 6):
+            got = codec_render(pkg, 72, 56, cam, method, torch)
+            ref = orc.render_codec(cb, t, e, orc.make_params(72, 56, cam, query_method=method))[:3]
+            assert_parity(got, ref, f"codec block map nb={nb} m{method}")
+
+
 @pytest.mark.parametrize("cap", ["1", "3"])
 def test_codec_occupancy_cap(pkg, orc, gpu, cap, tune):
     """VR_WG_PER_CU reaches the codec march (its LDS request holds the template table at

@@ -1795,6 +1795,11 @@ int render_frame(const vr_render_desc *desc, uint32_t clip_w, uint32_t clip_h) {
     } else if (is_flex_method(desc->query_method)) {
         e = vr::launch_march_flex(desc->query_method, P, nslots, g.stream);
     } else if (desc->query_method >= 4 && desc->query_method <= 6) {
+        // the one-lane codec march of a row-aligned view: a 16x4 pixel block per
+        // wave (1024^3 x 8 1080p C0 m4 2.91 -> 2.88 ms, m5 5.26 -> 5.17, m6 7.07 ->
+        // 6.90; profiles/r06/segmap/codec_*.log); VR_CODEC_MAP=0/1 overrides
+        P.seg_map = std::fabs(desc->inv_view[0]) >= 0.95f;
+        if (const char *em = vr::tuning("VR_CODEC_MAP")) P.seg_map = std::atoi(em) != 0;
         e = vr::launch_march_codec(P.nb, desc->query_method, P, nslots, false, g.stream);
         if (e == hipErrorInvalidValue)
             return fail(VR_ERR_UNSUPPORTED, "codec volumes with %d bins (compiled: 1,2,4,8,16,32)",
