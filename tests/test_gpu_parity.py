@@ -1214,3 +1214,34 @@ def test_wide32_row_aligned_frames_take_box_march(pkg, orc, gpu, tune):
             assert pkg.last_kernel().startswith("k_march<B=32"), pkg.last_kernel()
             ref = orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3]
             assert_parity(got, ref, f"32 bins box map {bmap} m{method}")
+
+
+@pytest.mark.parametrize("nb", [2, 8, 16, 32])
+def test_block_map_m7_and_wide(pkg, orc, gpu, nb, tune):
+    """VR_M7_MAP=1 / VR_WIDE_MAP=1: the one-lane method-7 marches and the 16-bin
+    row march with a 16x4 pixel block per wave, bit-identical (method-7 grid equal
+    to the volume and not; row-aligned and oblique views)"""
+    import torch
+    tune.set("VR_M7_MAP", "1")
+    tune.set("VR_WIDE_MAP", "1")
+    tune.set("VR_M7_WQ", "0")
+    tune.set("VR_M7_QUAD", "0")
+    vol = orc.synth_volume(21, 18, 15, nb)
+    pkg.init_distribution(vol)
+    W, H = 80, 56
+    for m in (pkg.camera.single_test_inv_view(), pkg.camera.display_inv_view((30.0, 45.0))):
+        for grid in ((21, 18, 15), (10, 12, 20)):
+            got = gpu_render(pkg, None, W, H, m, 7, torch, m7=grid)
+            assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=7,
+                                                               m7_dims=grid))[:3],
+                          f"{nb} bins m7 grid {grid} block map")
+            assert pkg.last_kernel().startswith("k_march_m7"), pkg.last_kernel()
+    if nb == 16:
+        tune.set("VR_WIDE", "1")
+        tune.set("VR_PATH", "2")
+        m = pkg.camera.single_test_inv_view()
+        for method in (1, 2):
+            got = gpu_render(pkg, None, W, H, m, method, torch)
+            assert pkg.last_kernel().startswith("k_march_wide<"), pkg.last_kernel()
+            assert_parity(got, orc.render(vol, orc.make_params(W, H, m, query_method=method))[:3],
+                          f"wide block map m{method}")

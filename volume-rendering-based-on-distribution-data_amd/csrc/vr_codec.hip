@@ -95,12 +95,7 @@ __global__ __launch_bounds__(256) void k_march_codec(const float *__restrict__ u
         __syncthreads();
     }
     uint32_t lx, ly;
-    if (P.seg_map) {  // a wave takes a 16x4 pixel block
-        lx = (threadIdx.x >> 6) * 16u + (threadIdx.x & 15u);
-        ly = (threadIdx.x >> 4) & 3u;
-    } else {
-        tile_pixel(threadIdx.x, lx, ly);
-    }
+    lane_pixel(P, threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.CW || y >= P.CH) return;

@@ -802,7 +802,7 @@ __device__ __forceinline__ int march_wide_tile(const float *__restrict__ vol, co
     constexpr int CG = 64 / B, NB = 8 / CG;
     static_assert(NB % 2 == 0, "batches alternate between two register sets");
     uint32_t lx, ly;
-    tile_pixel(tid, lx, ly);
+    lane_pixel(P, tid, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.CW || y >= P.CH) return -1;  // no cross-lane work in this kernel
@@ -1576,6 +1576,10 @@ static hipError_t march_b(int method, const float *vol, Params P, uint32_t nslot
             if (const char *em = tuning("VR_WQ_MAP")) P.wq_map = std::atoi(em) != 0;
             if (kind == 1) {
                 note_kernel("k_march_wide", B, method);
+                // a 16x4 pixel block per wave (1024^3 x 16 1080p C0 m1 2.719 -> 2.673
+                // ms, profiles/r06/segmap/wide_1024x16.log); VR_WIDE_MAP=0: rows
+                P.seg_map = 1;
+                if (const char *em = tuning("VR_WIDE_MAP")) P.seg_map = std::atoi(em) != 0;
                 if (method == 1)
                     hipLaunchKernelGGL((k_march_wide<B, 1>), grid, block, wl, s, vol, P);
                 else

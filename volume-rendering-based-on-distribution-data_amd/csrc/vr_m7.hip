@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, VR_M7_PI
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
     uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
+    lane_pixel(P, threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.CW || y >= P.CH) return;
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void k_march_m7(const float *__restrict__ vol,
     const uint32_t tile = tile_of(P, slot);
     if (tile == kPad) return;
     uint32_t lx, ly;
-    tile_pixel(threadIdx.x, lx, ly);
+    lane_pixel(P, threadIdx.x, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.CW || y >= P.CH) return;
@@ -678,9 +678,19 @@ static hipError_t march_m7_b(int method, const float *vol, const Params &P, uint
     return hipGetLastError();
 }
 
-hipError_t launch_march_m7(int nb, int method, const float *vol, const Params &P,
+hipError_t launch_march_m7(int nb, int method, const float *vol, const Params &P0,
                            uint32_t nslots, hipStream_t s) {
     if (nslots == 0) return hipSuccess;
+    // the one-lane method-7 marches (k_march_m7_pipe / k_march_m7): a 16x4 pixel
+    // block per wave, except 8+-bin row-aligned views of a fine volume (< 4 pixels
+    // per voxel of the x-y face), which keep 64-pixel rows: 256^3 x 4 at 512^2 C0
+    // 0.322 -> 0.222 ms, C1 0.201 -> 0.175; 512^3 x 8 1080p C0 1.201 -> 1.125;
+    // 1024^3 x 4 C0 0.795 -> 0.775, C1 2.67 -> 2.39; 1024^3 x 8 C0 1.447 vs 1.468
+    // (rows; profiles/r06/segmap/m7_*.log).  VR_M7_MAP=0/1 overrides.
+    Params P = P0;
+    P.seg_map = !(nb >= 8 && !P.oblique &&
+                  (uint64_t)P.CW * P.CH < 4ull * (uint64_t)P.nx * (uint64_t)P.ny);
+    if (const char *e = tuning("VR_M7_MAP")) P.seg_map = std::atoi(e) != 0;
     switch (nb) {
     case 1: return march_m7_b<1>(method, vol, P, nslots, s);
     case 2: return march_m7_b<2>(method, vol, P, nslots, s);

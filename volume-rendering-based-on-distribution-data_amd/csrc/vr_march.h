@@ -75,6 +75,17 @@ __device__ __forceinline__ void tile_pixel(uint32_t t, uint32_t &lx, uint32_t &l
     lx = t & (kTileW - 1);
     ly = t / kTileW;
 }
+// P.seg_map: a wave's 64 lanes take a 16x4 pixel block of the tile instead of a
+// 64-pixel row (compact footprints per load instruction; where it is the default:
+// vr_api.cpp fill_params)
+__device__ __forceinline__ void lane_pixel(const Params &P, uint32_t t, uint32_t &lx, uint32_t &ly) {
+    if (P.seg_map) {
+        lx = (t >> 6) * 16u + (t & 15u);
+        ly = (t >> 4) & 3u;
+    } else {
+        tile_pixel(t, lx, ly);
+    }
+}
 
 __device__ __forceinline__ void write_miss(const Params &P, uint64_t o) {
     if (P.out_n) P.out_n[o] = -1;
@@ -381,12 +392,7 @@ __device__ __forceinline__ int march_pipe_tile(const float *__restrict__ vol, co
                                                uint32_t slot, uint32_t tile, uint32_t tid,
                                                float *st = nullptr, const LogEnt *tab = nullptr) {
     uint32_t lx, ly;
-    if (P.seg_map) {  // a wave takes a 16x4 pixel block
-        lx = (tid >> 6) * 16u + (tid & 15u);
-        ly = (tid >> 4) & 3u;
-    } else {
-        tile_pixel(tid, lx, ly);
-    }
+    lane_pixel(P, tid, lx, ly);
     const uint32_t x = (tile % P.tiles_x) * kTileW + lx;
     const uint32_t y = (tile / P.tiles_x) * kTileH + ly;
     if (x >= P.CW || y >= P.CH) return -1;  // no cross-lane work in this kernel
