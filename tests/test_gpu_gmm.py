@@ -294,8 +294,9 @@ def test_config5_at_size(pkg, orc, gpu):
     3840x2160, C0, method 1, rendered on one GPU as the 8-rank z-slab chain
     renders it -- each rank's slab (its slices + halo, 207 GB) generated in HBM
     in turn, the alive list handed on in HBM -- against the oracle's
-    whole-volume render of 64 rows, whose records it computes from the voxel
-    index as a sample reads them (no host holds the volume).  Slabs after the
+    whole-volume render of every 8th row (270 of 2160), whose records it
+    computes from the voxel index as a sample reads them (no host holds the
+    volume).  Slabs after the
     one that ends the last ray receive no rays and are not generated."""
     import torch
     n, K, W, H = 2048, 16, 3840, 2160
@@ -331,11 +332,11 @@ def test_config5_at_size(pkg, orc, gpu):
     finally:
         pkg.free_gmm()
     assert n_in == 0 and done >= 2
-    rows = np.linspace(0, H - 1, 64).round().astype(np.int32)
+    rows = np.arange(0, H, 8, dtype=np.int32)  # 270 rows (~40 s of oracle on 16 threads)
     ref, ref_n, samples = orc.render_gmm_rows_proc(
         (n, n, n), K, orc.make_params(W, H, m, query_method=1), rows, nthreads=orc.max_threads())
     got = frame.cpu().numpy().view(np.uint32).reshape(H, W)[rows]
     got_n = steps.cpu().numpy().reshape(H, W)[rows]
-    assert int(np.sum(ref_n > 0)) > 64 * W // 4 and samples > 0
+    assert int(np.sum(ref_n > 0)) > len(rows) * W // 4 and samples > 0
     assert np.array_equal(got_n, ref_n), f"{int(np.sum(got_n != ref_n))} sample counts differ"
     assert np.array_equal(got, ref), f"{int(np.sum(got != ref))} RGBA8 pixels differ"
