@@ -6,7 +6,7 @@ For PMC passes of a variant (rocprofv3 --pmc ... -- python tools/pmc_frames.py
 compared bit for bit with a frame of the default dispatch (the default's
 parity with the oracle is what the GPU tests and bench lines check).
 
-  python tools/pmc_frames.py --config 512x8 --camera C0 --method 1 --tune VR_LOCK=1 --frames 3
+  python tools/pmc_frames.py --config 512x8 --camera C0 --method 1 --tune VR_DUO=0 --frames 3
 """
 import argparse
 import os
